@@ -1,0 +1,83 @@
+// Host-visible kernel API of the engine: parameter structs and the extern "C" launchers that the
+// torch bindings (bindings.cpp) call with raw pointers and torch's current HIP stream.
+#pragma once
+#include "common.h"
+
+namespace dsse {
+
+constexpr int kBS = 32;  // KV-cache page size in tokens (fixed for every kernel)
+
+enum GemmMode { kStoreBf16 = 0, kStoreF32 = 1, kResidAdd = 2, kSiluMul = 3, kQkvRope = 4 };
+
+struct GemmEpi {
+  void* out;          // bf16 / f32 output (modes 0, 1, 3)
+  int ldo;
+  float* resid;       // mode 2
+  int ldr;
+  const int* positions;   // mode 4: per-row absolute position
+  const int* slots;       // mode 4: per-row KV slot (-1 = do not write)
+  const float2* rope;     // mode 4: [max_pos][64] (cos, sin)
+  bf16* q_out;            // mode 4: [M, nh*128]
+  bf16* k_cache;          // [blocks, nkv, kBS, 128]
+  bf16* v_cache;          // [blocks, nkv, 128, kBS] (token-permuted inside a page)
+  int nh, nkv;
+};
+
+struct AttnParams {
+  const bf16* q;            // [T, Hq, 128]
+  const bf16* k_cache;
+  const bf16* v_cache;
+  const int* block_tables;  // [B, max_blocks]
+  int max_blocks;
+  const int* q_start;       // [B] first query row of the sequence in q / out
+  const int* q_len;         // [B] number of query tokens (0 = inactive)
+  const int* ctx_len;       // [B] number of keys in the cache including the queries
+  const int* work_seq;      // [num_work] sequence of work item
+  const int* work_tile;     // [num_work] query-tile block (in units of QW tiles)
+  bf16* out;                // [T, Hq, 128]
+  float* part_o;            // [num_work, Hkv, nparts, QW, 16, 128]
+  float2* part_ml;          // [num_work, Hkv, nparts, QW, 16]
+  int hq, hkv, group;       // group = hq / hkv; 16 % group == 0
+  int part;                 // keys per partition (multiple of 32 * KWV)
+  int nparts;               // grid.z
+  float scale_log2;         // log2(e) / sqrt(128)
+};
+
+struct SampleParams {
+  const float* logits;  // [B, ld]
+  int ld, V;            // row stride, local vocab size
+  int vocab_offset;     // global index of local column 0
+  const float* temperature;  // [B]; <= 0 -> greedy
+  const int* top_k;          // [B]; <= 0 -> off
+  const float* top_p;        // [B]; >= 1 -> off
+  const uint2* seeds;        // [B]
+  const int* positions;      // [B] position of the sampled token's predecessor (RNG counter)
+  const int* active;         // [B] or null (all active)
+  int* next_ids;             // [B] written when !candidates_only
+  int* ring;                 // [ring_size, ring_stride] or null
+  const int* ring_counter;
+  int ring_size, ring_stride;
+  int* positions_inc;        // [B] or null: positions[b] += 1 for active rows
+  float2* cand;              // [B] (score, index-as-bits) when candidates_only
+  int candidates_only;
+};
+
+}  // namespace dsse
+
+extern "C" {
+hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int ldx, int M,
+                            const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
+hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
+hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);
+hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::SampleParams* p,
+                            hipStream_t st);
+hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
+                        const int* ids, const void* w, void* y, float eps, hipStream_t st);
+hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
+                              const int* slots, const float2* rope, void* q_out, void* k_cache,
+                              void* v_cache, hipStream_t st);
+hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
+hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
+                            int max_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
+hipError_t dsse_ring_advance(int* counter, hipStream_t st);
+}

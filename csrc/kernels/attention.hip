@@ -1,0 +1,239 @@
+// Paged GQA attention on MFMA for gfx950 (K5 decode and K12 prefill of SURVEY.md §2.4).
+//
+// KV cache layout (engine-owned, page = 32 tokens):
+//   K: [blocks, Hkv, 32, 128]   one key row = 256 contiguous bytes
+//   V: [blocks, Hkv, 128, 32]   transposed, tokens permuted inside the page by vperm() so the
+//                               PV operand of lane group g is one 16-byte run
+//
+// One MFMA tile column is a (query token, q-head of the GQA group) pair: with G = Hq/Hkv heads
+// per kv head, a 16-column tile holds QT = 16/G query tokens of one sequence.  Decode uses
+// QT = 1 token (G columns live), prefill uses all 16 columns.  Scores are computed swapped,
+// Sᵀ[key, col] = K · Qᵀ, so the softmax statistics of a column live in one lane column and
+// the exponentiated scores are already the B operand of Oᵀ = Vᵀ · Pᵀ — no LDS round trip and
+// no transposes inside the key loop.
+//
+// Work decomposition: a workgroup = QW × KWV waves.  The QW waves take consecutive query tiles
+// (prefill: they share K/V lines through L1), the KWV waves split the key range and are merged
+// in LDS; grid.z splits the key range into partitions of `part` keys (flash-decoding), merged
+// by attn_combine_kernel.  Online softmax in base 2 with a finite initial max, so fully masked
+// columns stay finite and produce zeros.
+#include "api.h"
+
+namespace dsse {
+
+constexpr int kPage = 32;
+constexpr int kD = 128;
+
+
+template <int QW, int KWV>
+__global__ void __launch_bounds__(64 * QW * KWV)
+paged_attention_kernel(AttnParams p) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int qw = w / KWV, kw = w % KWV;
+  const int item = blockIdx.x, h = blockIdx.y, pz = blockIdx.z;
+  const int b = p.work_seq[item];
+  const int qlen = p.q_len[b];
+  const int ctx = p.ctx_len[b];
+  const int G = p.group, QT = 16 / G;
+  const int tile = p.work_tile[item] * QW + qw;  // this wave's query tile
+  const int q0 = tile * QT;                       // first query index (within the sequence)
+
+  // Column r of this wave: query qi = q0 + r / G, head h*G + r % G.
+  const int qi = q0 + r / G;
+  const bool col_valid = qi < qlen;
+  const int qpos = ctx - qlen + qi;          // absolute position; keys [0, qpos] visible
+  const int col_limit = col_valid ? qpos + 1 : 0;
+
+  // Key range needed by the whole workgroup (all QW tiles): up to the last live query.
+  const int last_q = min(qlen, (p.work_tile[item] + 1) * QW * QT) - 1;
+  const int kmax = (qlen > 0 && last_q >= 0) ? (ctx - qlen + last_q + 1) : 0;
+  const int kbeg = pz * p.part;
+  const int kend = min(kmax, kbeg + p.part);
+  if (kbeg >= kend) return;  // uniform for the whole workgroup
+
+  // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32g + 8s + j].
+  bf16x8 qf[4];
+  {
+    const int qrow = p.q_start[b] + (col_valid ? qi : 0);
+    const bf16* qp = p.q + ((size_t)qrow * p.hq + h * G + (r % G)) * kD + 32 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = col_valid ? ld_bf16x8(qp + 8 * s) : zero_bf16x8();
+  }
+
+  float m_run = -1e30f, l_run = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  for (int kb = kbeg + 32 * kw; kb < kend; kb += 32 * KWV) {
+    const int page = bt[kb / kPage];
+    const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
+    const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
+    // K rows for keys kb + r and kb + 16 + r, 64 contiguous bytes per lane each.
+    bf16x8 k0[4], k1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * g + 8 * s);
+      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * g + 8 * s);
+    }
+    bf16x8 vf[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_bf16x8(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
+
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = mfma16x16x32(k0[s], qf[s], s0);
+      s1 = mfma16x16x32(k1[s], qf[s], s1);
+    }
+    // element i: key kb + 4g + i (s0) / kb + 16 + 4g + i (s1), column r
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ka = kb + 4 * g + i, kb2 = kb + 16 + 4 * g + i;
+      s0[i] = (ka < col_limit) ? s0[i] * p.scale_log2 : -INFINITY;
+      s1[i] = (kb2 < col_limit) ? s1[i] * p.scale_log2 : -INFINITY;
+      tmax = fmaxf(tmax, fmaxf(s0[i], s1[i]));
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    bf16x8 pf;
+    float psum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e0 = exp2f(s0[i] - m_new), e1 = exp2f(s1[i] - m_new);
+      psum += e0 + e1;
+      pf[i] = f2bf(e0);
+      pf[4 + i] = f2bf(e1);
+    }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      f32x4 acc = o[dt] * alpha;
+      o[dt] = mfma16x16x32(vf[dt], pf, acc);
+    }
+  }
+  // l_run is a per-lane partial over this lane's keys: sum the 4 lane groups of the column.
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+
+  // ---- merge the KWV key-split waves of each query tile in LDS ----
+  if constexpr (KWV > 1) {
+    __shared__ float s_o[QW * KWV][8 * 4][64];
+    __shared__ float s_m[QW * KWV][16], s_l[QW * KWV][16];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_o[w][dt * 4 + i][lane] = o[dt][i];
+    if (g == 0) { s_m[w][r] = m_run; s_l[w][r] = l_run; }
+    __syncthreads();
+    if (kw != 0) return;
+    float mm = m_run;
+#pragma unroll
+    for (int v = 1; v < KWV; ++v) mm = fmaxf(mm, s_m[w + v][r]);
+    float sc[KWV], ll = 0.f;
+#pragma unroll
+    for (int v = 0; v < KWV; ++v) {
+      const float mv = v == 0 ? m_run : s_m[w + v][r];
+      const float lv = v == 0 ? l_run : s_l[w + v][r];
+      sc[v] = exp2f(mv - mm);
+      ll += lv * sc[v];
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float acc = o[dt][i] * sc[0];
+#pragma unroll
+        for (int v = 1; v < KWV; ++v) acc += s_o[w + v][dt * 4 + i][lane] * sc[v];
+        o[dt][i] = acc;
+      }
+    m_run = mm;
+    l_run = ll;
+  }
+
+  // ---- write: final (single partition) or partial (flash-decoding) ----
+  // element (dt, i) of lane (r, g): d = 16dt + 4g + i, column r
+  if (p.nparts == 1) {
+    if (!col_valid) return;
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + h * G + (r % G)) * kD;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) op[16 * dt + 4 * g + i] = f2bf(o[dt][i] * inv);
+  } else {
+    const size_t base = (((size_t)item * p.hkv + h) * p.nparts + pz) * QW + qw;
+    float* po = p.part_o + base * 16 * kD + (size_t)r * kD;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) po[16 * dt + 4 * g + i] = o[dt][i];
+    if (g == 0) p.part_ml[base * 16 + r] = make_float2(m_run, l_run);
+  }
+}
+
+// Merge flash-decoding partitions: grid (num_work, hkv, QW), block 256 = (16 columns × 16 lanes),
+// each thread owns 8 head dims of one column.
+template <int QW>
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
+  const int item = blockIdx.x, h = blockIdx.y, qw = blockIdx.z;
+  const int col = threadIdx.x >> 4, sub = threadIdx.x & 15;
+  const int b = p.work_seq[item];
+  const int qlen = p.q_len[b], ctx = p.ctx_len[b];
+  const int G = p.group, QT = 16 / G;
+  const int qi = (p.work_tile[item] * QW + qw) * QT + col / G;
+  if (qi >= qlen) return;
+  const int last_q = min(qlen, (p.work_tile[item] + 1) * QW * QT) - 1;
+  const int kmax = ctx - qlen + last_q + 1;
+  const int np = min(p.nparts, (kmax + p.part - 1) / p.part);
+  float mm = -1e30f;
+  for (int z = 0; z < np; ++z) {
+    const size_t base = (((size_t)item * p.hkv + h) * p.nparts + z) * QW + qw;
+    mm = fmaxf(mm, p.part_ml[base * 16 + col].x);
+  }
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float ll = 0.f;
+  for (int z = 0; z < np; ++z) {
+    const size_t base = (((size_t)item * p.hkv + h) * p.nparts + z) * QW + qw;
+    const float2 ml = p.part_ml[base * 16 + col];
+    const float sc = exp2f(ml.x - mm);
+    ll += ml.y * sc;
+    const float4* po = reinterpret_cast<const float4*>(p.part_o + (base * 16 + col) * kD + 8 * sub);
+    const float4 a = po[0], c = po[1];
+    acc[0] += a.x * sc; acc[1] += a.y * sc; acc[2] += a.z * sc; acc[3] += a.w * sc;
+    acc[4] += c.x * sc; acc[5] += c.y * sc; acc[6] += c.z * sc; acc[7] += c.w * sc;
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+  bf16x8 ov;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
+  bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + h * G + (col % G)) * kD + 8 * sub;
+  *reinterpret_cast<bf16x8*>(op) = ov;
+}
+
+}  // namespace dsse
+
+// mode 0 = decode (QW = 1, KWV = 4), mode 1 = prefill (QW = 4, KWV = 1).
+extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p,
+                                           hipStream_t st) {
+  using namespace dsse;
+  if (num_work <= 0) return hipSuccess;
+  if (mode == 0) {
+    hipLaunchKernelGGL((paged_attention_kernel<1, 4>), dim3(num_work, p->hkv, p->nparts), dim3(256),
+                       0, st, *p);
+    if (p->nparts > 1)
+      hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
+  } else {
+    hipLaunchKernelGGL((paged_attention_kernel<4, 1>), dim3(num_work, p->hkv, p->nparts), dim3(256),
+                       0, st, *p);
+    if (p->nparts > 1)
+      hipLaunchKernelGGL((attn_combine_kernel<4>), dim3(num_work, p->hkv, 4), dim3(256), 0, st, *p);
+  }
+  return hipGetLastError();
+}

@@ -1,0 +1,385 @@
+// torch operator registrations for the gfx950 kernels (namespace torch.ops.dsse).
+//
+// Every op validates device, dtype, contiguity and the shape contract the kernel's grid assumes
+// BEFORE launching (a wrong shape on a hand-written kernel would fault the GPU), then launches on
+// torch's current HIP stream so the ops compose with hipGraph capture (torch.cuda.CUDAGraph).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstdlib>
+#include <string>
+
+#include "api.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define DSSE_CHECK_HIP(expr)                                                        \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    TORCH_CHECK(_e == hipSuccess, "dsse kernel launch failed: ", hipGetErrorString(_e)); \
+  } while (0)
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+// Tile selection for the skinny GEMM.  NT = output tiles per wave, KW = waves splitting K.
+// Defaults come from the gfx950 sweep in tools/tune_gemm.py; DSSE_GEMM_NT / DSSE_GEMM_KW override.
+void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
+  mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  nt = 1;
+  const int chunks = K / 128;
+  kw = chunks >= 32 ? 8 : 4;
+  const int e_nt = env_int("DSSE_GEMM_NT", 0), e_kw = env_int("DSSE_GEMM_KW", 0);
+  if (e_nt) nt = e_nt;
+  if (e_kw) kw = e_kw;
+  if (mt == 4 && nt == 2 && kw == 8) kw = 4;  // spill guard (see gemm_skinny.hip)
+  if (N % (16 * nt) != 0) nt = 1;
+  (void)mode;
+}
+
+void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x and w must be 2-D");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "K mismatch: x ", K, " vs w ", w.size(1));
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny GEMM supports 1 <= M <= 64, got ", M);
+  TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
+  TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
+  int mt, nt, kw;
+  pick_tiles(M, N, K, mode, mt, nt, kw);
+  DSSE_CHECK_HIP(dsse_skinny_gemm(mode, mt, nt, kw, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                  cur_stream()));
+}
+
+void gemm_out(const Tensor& x, const Tensor& w, Tensor& out) {
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) == w.size(0),
+              "out must be [M, N]");
+  dsse::GemmEpi ep{};
+  ep.out = out.data_ptr();
+  ep.ldo = (int)out.size(1);
+  int mode;
+  if (out.scalar_type() == at::kBFloat16) mode = dsse::kStoreBf16;
+  else if (out.scalar_type() == at::kFloat) mode = dsse::kStoreF32;
+  else TORCH_CHECK(false, "out must be bf16 or fp32");
+  run_gemm(mode, x, w, ep);
+}
+
+void gemm_resid(const Tensor& x, const Tensor& w, Tensor& resid) {
+  check_gpu(resid, "resid");
+  check_dtype(resid, at::kFloat, "resid");
+  TORCH_CHECK(resid.dim() == 2 && resid.size(0) == x.size(0) && resid.size(1) == w.size(0),
+              "resid must be [M, N]");
+  dsse::GemmEpi ep{};
+  ep.resid = resid.data_ptr<float>();
+  ep.ldr = (int)resid.size(1);
+  run_gemm(dsse::kResidAdd, x, w, ep);
+}
+
+void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out) {
+  check_gpu(out, "out");
+  check_dtype(out, at::kBFloat16, "out");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) * 2 == w.size(0),
+              "out must be [M, N/2]");
+  dsse::GemmEpi ep{};
+  ep.out = out.data_ptr();
+  ep.ldo = (int)out.size(1);
+  run_gemm(dsse::kSiluMul, x, w, ep);
+}
+
+void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
+                   const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
+                   int64_t nkv) {
+  for (auto* t : {&positions, &slots, &rope}) check_gpu(*t, "metadata");
+  check_gpu(q_out, "q_out");
+  check_gpu(k_cache, "k_cache");
+  check_gpu(v_cache, "v_cache");
+  check_dtype(positions, at::kInt, "positions");
+  check_dtype(slots, at::kInt, "slots");
+  check_dtype(rope, at::kFloat, "rope");
+  check_dtype(q_out, at::kBFloat16, "q_out");
+  TORCH_CHECK(w.size(0) == (nh + 2 * nkv) * 128, "w rows must be (nh + 2 nkv) * 128");
+  TORCH_CHECK(positions.numel() >= x.size(0) && slots.numel() >= x.size(0), "metadata too short");
+  TORCH_CHECK(q_out.numel() >= x.size(0) * nh * 128, "q_out too small");
+  TORCH_CHECK(rope.dim() == 3 && rope.size(1) == 64 && rope.size(2) == 2, "rope must be [P, 64, 2]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(2) == dsse::kBS &&
+                  k_cache.size(3) == 128, "k_cache must be [blocks, nkv, 32, 128]");
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), nkv, 128, dsse::kBS}),
+              "v_cache must be [blocks, nkv, 128, 32]");
+  dsse::GemmEpi ep{};
+  ep.positions = positions.data_ptr<int>();
+  ep.slots = slots.data_ptr<int>();
+  ep.rope = reinterpret_cast<const float2*>(rope.data_ptr<float>());
+  ep.q_out = reinterpret_cast<bf16*>(q_out.data_ptr());
+  ep.k_cache = reinterpret_cast<bf16*>(k_cache.data_ptr());
+  ep.v_cache = reinterpret_cast<bf16*>(v_cache.data_ptr());
+  ep.nh = (int)nh;
+  ep.nkv = (int)nkv;
+  run_gemm(dsse::kQkvRope, x, w, ep);
+}
+
+void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
+             const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids) {
+  check_gpu(resid, "resid");
+  check_gpu(w, "w");
+  check_gpu(y, "y");
+  check_dtype(resid, at::kFloat, "resid");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(y, at::kBFloat16, "y");
+  const int M = (int)y.size(0), H = (int)y.size(1);
+  TORCH_CHECK(H % 1024 == 0 && H <= 8192, "hidden size must be a multiple of 1024 and <= 8192");
+  TORCH_CHECK(resid.size(0) >= M && resid.size(1) == H && w.numel() == H, "shape mismatch");
+  int mode = 0;
+  const void* dptr = nullptr;
+  const void* eptr = nullptr;
+  const int* iptr = nullptr;
+  if (embed.has_value()) {
+    TORCH_CHECK(ids.has_value(), "embedding mode needs ids");
+    check_gpu(*embed, "embed");
+    check_gpu(*ids, "ids");
+    check_dtype(*ids, at::kInt, "ids");
+    TORCH_CHECK(embed->size(1) == H && ids->numel() >= M, "embedding shape mismatch");
+    mode = 2;
+    eptr = embed->data_ptr();
+    iptr = ids->data_ptr<int>();
+  } else if (delta.has_value()) {
+    check_gpu(*delta, "delta");
+    check_dtype(*delta, at::kBFloat16, "delta");
+    TORCH_CHECK(delta->size(0) >= M && delta->size(1) == H, "delta shape mismatch");
+    mode = 1;
+    dptr = delta->data_ptr();
+  }
+  DSSE_CHECK_HIP(dsse_rmsnorm(mode, M, resid.data_ptr<float>(), H, dptr, eptr, iptr, w.data_ptr(),
+                              y.data_ptr(), (float)eps, cur_stream()));
+}
+
+void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& rope,
+                   Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh, int64_t nkv) {
+  check_gpu(qkv, "qkv");
+  check_dtype(qkv, at::kBFloat16, "qkv");
+  const int T = (int)qkv.size(0);
+  TORCH_CHECK(qkv.size(1) == (nh + 2 * nkv) * 128, "qkv width mismatch");
+  TORCH_CHECK(positions.numel() >= T && slots.numel() >= T, "metadata too short");
+  TORCH_CHECK(q_out.numel() >= (int64_t)T * nh * 128, "q_out too small");
+  TORCH_CHECK(k_cache.size(1) == nkv && v_cache.size(1) == nkv, "cache head mismatch");
+  DSSE_CHECK_HIP(dsse_rope_kv_write(T, qkv.data_ptr(), (int)nh, (int)nkv, positions.data_ptr<int>(),
+                                    slots.data_ptr<int>(),
+                                    reinterpret_cast<const float2*>(rope.data_ptr<float>()),
+                                    q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                    cur_stream()));
+}
+
+void silu_mul(const Tensor& gu, Tensor& h) {
+  check_gpu(gu, "gu");
+  check_gpu(h, "h");
+  const int T = (int)gu.size(0), F = (int)h.size(1);
+  TORCH_CHECK(gu.size(1) == 2 * F && h.size(0) == T && F % 8 == 0, "silu_mul shape mismatch");
+  DSSE_CHECK_HIP(dsse_silu_mul(T, F, gu.data_ptr(), h.data_ptr(), cur_stream()));
+}
+
+void decode_prep(const Tensor& active, const Tensor& positions, const Tensor& block_tables,
+                 Tensor& slots, Tensor& ctx_len, Tensor& q_len) {
+  for (const Tensor* t : {&active, &positions, &block_tables, (const Tensor*)&slots, (const Tensor*)&ctx_len, (const Tensor*)&q_len}) {
+    check_gpu(*t, "decode metadata");
+    check_dtype(*t, at::kInt, "decode metadata");
+  }
+  const int B = (int)active.numel();
+  TORCH_CHECK(positions.numel() >= B && slots.numel() >= B && ctx_len.numel() >= B &&
+                  q_len.numel() >= B && block_tables.size(0) >= B, "decode metadata too short");
+  DSSE_CHECK_HIP(dsse_decode_prep(B, active.data_ptr<int>(), positions.data_ptr<int>(),
+                                  block_tables.data_ptr<int>(), (int)block_tables.size(1),
+                                  slots.data_ptr<int>(), ctx_len.data_ptr<int>(), q_len.data_ptr<int>(),
+                                  cur_stream()));
+}
+
+void ring_advance(Tensor& counter) {
+  check_gpu(counter, "counter");
+  check_dtype(counter, at::kInt, "counter");
+  DSSE_CHECK_HIP(dsse_ring_advance(counter.data_ptr<int>(), cur_stream()));
+}
+
+void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                     const Tensor& block_tables, const Tensor& q_start, const Tensor& q_len,
+                     const Tensor& ctx_len, const Tensor& work_seq, const Tensor& work_tile,
+                     Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part, int64_t nparts) {
+  for (const Tensor* t : {&q, &k_cache, &v_cache, (const Tensor*)&out}) {
+    check_gpu(*t, "attention tensor");
+    check_dtype(*t, at::kBFloat16, "attention tensor");
+  }
+  for (auto* t : {&block_tables, &q_start, &q_len, &ctx_len, &work_seq, &work_tile}) {
+    check_gpu(*t, "attention metadata");
+    check_dtype(*t, at::kInt, "attention metadata");
+  }
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == dsse::kBS && k_cache.size(3) == 128,
+              "k_cache must be [blocks, Hkv, 32, 128]");
+  const int hq = (int)q.size(1), hkv = (int)k_cache.size(1);
+  TORCH_CHECK(hq % hkv == 0 && 16 % (hq / hkv) == 0, "GQA group must divide 16");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  const int num_work = (int)work_seq.numel();
+  TORCH_CHECK(work_tile.numel() == num_work, "work lists differ in length");
+  const int kwv = mode == 0 ? 4 : 1, qw = mode == 0 ? 1 : 4;
+  TORCH_CHECK(part % (32 * kwv) == 0 && part > 0, "partition size must be a multiple of ", 32 * kwv);
+  TORCH_CHECK(nparts >= 1, "nparts >= 1");
+  if (nparts > 1) {
+    check_gpu(part_o, "part_o");
+    check_gpu(part_ml, "part_ml");
+    TORCH_CHECK(part_o.numel() >= (int64_t)num_work * hkv * nparts * qw * 16 * 128, "part_o too small");
+    TORCH_CHECK(part_ml.numel() >= (int64_t)num_work * hkv * nparts * qw * 16 * 2, "part_ml too small");
+  }
+  dsse::AttnParams p{};
+  p.q = reinterpret_cast<const bf16*>(q.data_ptr());
+  p.k_cache = reinterpret_cast<const bf16*>(k_cache.data_ptr());
+  p.v_cache = reinterpret_cast<const bf16*>(v_cache.data_ptr());
+  p.block_tables = block_tables.data_ptr<int>();
+  p.max_blocks = (int)block_tables.size(1);
+  p.q_start = q_start.data_ptr<int>();
+  p.q_len = q_len.data_ptr<int>();
+  p.ctx_len = ctx_len.data_ptr<int>();
+  p.work_seq = work_seq.data_ptr<int>();
+  p.work_tile = work_tile.data_ptr<int>();
+  p.out = reinterpret_cast<bf16*>(out.data_ptr());
+  p.part_o = nparts > 1 ? part_o.data_ptr<float>() : nullptr;
+  p.part_ml = nparts > 1 ? reinterpret_cast<float2*>(part_ml.data_ptr<float>()) : nullptr;
+  p.hq = hq;
+  p.hkv = hkv;
+  p.group = hq / hkv;
+  p.part = (int)part;
+  p.nparts = (int)nparts;
+  p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
+  DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
+}
+
+dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
+                                 const Tensor& seeds, const Tensor& positions,
+                                 const c10::optional<Tensor>& active, Tensor& next_ids,
+                                 const c10::optional<Tensor>& ring,
+                                 const c10::optional<Tensor>& ring_counter,
+                                 const c10::optional<Tensor>& positions_inc) {
+  check_dtype(temperature, at::kFloat, "temperature");
+  check_dtype(top_k, at::kInt, "top_k");
+  check_dtype(top_p, at::kFloat, "top_p");
+  check_dtype(seeds, at::kInt, "seeds");
+  check_dtype(positions, at::kInt, "positions");
+  check_dtype(next_ids, at::kInt, "next_ids");
+  dsse::SampleParams p{};
+  p.temperature = temperature.data_ptr<float>();
+  p.top_k = top_k.data_ptr<int>();
+  p.top_p = top_p.data_ptr<float>();
+  p.seeds = reinterpret_cast<const uint2*>(seeds.data_ptr<int>());
+  p.positions = positions.data_ptr<int>();
+  p.active = active.has_value() ? active->data_ptr<int>() : nullptr;
+  p.next_ids = next_ids.data_ptr<int>();
+  if (ring.has_value()) {
+    TORCH_CHECK(ring_counter.has_value(), "ring needs ring_counter");
+    p.ring = ring->data_ptr<int>();
+    p.ring_counter = ring_counter->data_ptr<int>();
+    p.ring_size = (int)ring->size(0);
+    p.ring_stride = (int)ring->size(1);
+  }
+  p.positions_inc = positions_inc.has_value() ? positions_inc->data_ptr<int>() : nullptr;
+  return p;
+}
+
+void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
+            const Tensor& seeds, const Tensor& positions, const c10::optional<Tensor>& active,
+            Tensor& next_ids, const c10::optional<Tensor>& ring,
+            const c10::optional<Tensor>& ring_counter, const c10::optional<Tensor>& positions_inc,
+            const c10::optional<Tensor>& cand, int64_t vocab_offset) {
+  check_gpu(logits, "logits");
+  check_dtype(logits, at::kFloat, "logits");
+  const int B = (int)logits.size(0), V = (int)logits.size(1);
+  TORCH_CHECK(V <= 32768, "sampler supports V <= 32768 per rank");
+  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B &&
+                  seeds.numel() >= 2 * B && positions.numel() >= B && next_ids.numel() >= B,
+              "sampling metadata too short");
+  if (ring.has_value()) TORCH_CHECK(ring->size(1) >= B, "ring too narrow");
+  dsse::SampleParams p = sample_params(temperature, top_k, top_p, seeds, positions, active, next_ids,
+                                       ring, ring_counter, positions_inc);
+  p.logits = logits.data_ptr<float>();
+  p.ld = V;
+  p.V = V;
+  p.vocab_offset = (int)vocab_offset;
+  if (cand.has_value()) {
+    TORCH_CHECK(cand->numel() >= 2 * B, "cand too small");
+    p.cand = reinterpret_cast<float2*>(cand->data_ptr<float>());
+    p.candidates_only = 1;
+  }
+  DSSE_CHECK_HIP(dsse_sample(B, &p, cur_stream()));
+}
+
+void sample_pick(const Tensor& cand_all, int64_t world, const Tensor& temperature, const Tensor& top_k,
+                 const Tensor& top_p, const Tensor& seeds, const Tensor& positions,
+                 const c10::optional<Tensor>& active, Tensor& next_ids, const c10::optional<Tensor>& ring,
+                 const c10::optional<Tensor>& ring_counter,
+                 const c10::optional<Tensor>& positions_inc) {
+  check_gpu(cand_all, "cand_all");
+  const int B = (int)(cand_all.numel() / (2 * world));
+  TORCH_CHECK(next_ids.numel() >= B, "next_ids too short");
+  dsse::SampleParams p = sample_params(temperature, top_k, top_p, seeds, positions, active, next_ids,
+                                       ring, ring_counter, positions_inc);
+  DSSE_CHECK_HIP(dsse_sample_pick(B, (int)world, cand_all.data_ptr(), &p, cur_stream()));
+}
+
+int64_t kernels_abi_version() { return 1; }
+
+}  // namespace
+
+TORCH_LIBRARY(dsse, m) {
+  m.def("gemm_out(Tensor x, Tensor w, Tensor(a!) out) -> ()");
+  m.def("gemm_resid(Tensor x, Tensor w, Tensor(a!) resid) -> ()");
+  m.def("gemm_silu(Tensor x, Tensor w, Tensor(a!) out) -> ()");
+  m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
+  m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
+        "Tensor? ids=None) -> ()");
+  m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
+  m.def("silu_mul(Tensor gu, Tensor(a!) h) -> ()");
+  m.def("decode_prep(Tensor active, Tensor positions, Tensor block_tables, Tensor(a!) slots, "
+        "Tensor(b!) ctx_len, Tensor(c!) q_len) -> ()");
+  m.def("ring_advance(Tensor(a!) counter) -> ()");
+  m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
+        "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
+  m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor positions, "
+        "Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, Tensor? ring_counter=None, "
+        "Tensor(c!)? positions_inc=None, Tensor(d!)? cand=None, int vocab_offset=0) -> ()");
+  m.def("sample_pick(Tensor cand_all, int world, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
+        "Tensor positions, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, Tensor? ring_counter=None, "
+        "Tensor(c!)? positions_inc=None) -> ()");
+  m.def("kernels_abi_version() -> int", &kernels_abi_version);
+}
+
+TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
+  m.impl("gemm_out", &gemm_out);
+  m.impl("gemm_resid", &gemm_resid);
+  m.impl("gemm_silu", &gemm_silu);
+  m.impl("gemm_qkv_rope", &gemm_qkv_rope);
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("rope_kv_write", &rope_kv_write);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("decode_prep", &decode_prep);
+  m.impl("ring_advance", &ring_advance);
+  m.impl("paged_attention", &paged_attention);
+  m.impl("sample", &sample);
+  m.impl("sample_pick", &sample_pick);
+}

@@ -1,0 +1,78 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of the decode engine.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; lane l is split as r = l & 15 (column / row inside a 16-wide MFMA tile)
+//     and g = l >> 4 (lane group 0..3), matching the operand maps of
+//     v_mfma_f32_16x16x32_bf16:  A[row r][k = 8g + j], B[k = 8g + j][col r],
+//     C/D[row 4g + i][col r] (i = 0..3).
+//   * bf16 tensors are raw __bf16; 16-byte vectors are bf16x8 (one MFMA operand fragment).
+//   * Every kernel takes an explicit hipStream_t from the caller (torch's current stream),
+//     so the whole decode step can be captured into one hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define DEV __device__ __forceinline__
+
+namespace dsse {
+
+constexpr int kWave = 64;
+
+DEV float bf2f(bf16 x) { return (float)x; }
+DEV bf16 f2bf(float x) { return (bf16)x; }
+
+DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+DEV bf16x8 ld_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+DEV bf16x8 zero_bf16x8() {
+  bf16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (bf16)0.0f;
+  return z;
+}
+
+// Non-temporal 16-byte load for once-read streams (weights, KV pages).
+DEV bf16x8 ld_nt_bf16x8(const bf16* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+}
+
+template <typename T>
+DEV T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+template <typename T>
+DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+DEV float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Philox4x32-10 counter-based RNG (one 32-bit output used per call site).
+DEV uint4 philox4x32(uint4 ctr, uint2 key) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += 0x9E3779B9u;
+    key.y += 0xBB67AE85u;
+  }
+  return ctr;
+}
+// Uniform in (0, 1]: never exactly 0 so -log(-log(u)) is finite.
+DEV float u01(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+
+}  // namespace dsse

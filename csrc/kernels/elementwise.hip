@@ -1,0 +1,201 @@
+// Memory-bound helper kernels of the decode/prefill step (K1, K2, K4, K11 of SURVEY.md §2.4).
+// All bf16 traffic is vectorised to 8-16 bytes per lane (guide Guideline 13).
+#include <algorithm>
+#include "api.h"
+
+namespace dsse {
+
+constexpr int kPageTok = 32;
+
+DEV int vperm_tok(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4 + (off & 3); }
+
+// ---- K1 + K2: (embedding gather | residual add) + RMSNorm ------------------------------------
+// MODE 0: y = rmsnorm(resid)            MODE 1: resid += delta; y = rmsnorm(resid)
+// MODE 2: resid = embed[ids[m]]; y = rmsnorm(resid)
+// The residual stream is fp32 [M, H]; y is the bf16 input of the next GEMM.
+// One 256-thread workgroup per row; each thread keeps its H/256 values in registers.
+template <int MODE>
+__global__ void __launch_bounds__(256)
+rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
+               const bf16* __restrict__ embed, const int* __restrict__ ids,
+               const bf16* __restrict__ w, bf16* __restrict__ y, float eps) {
+  const int m = blockIdx.x, tid = threadIdx.x;
+  float* rrow = resid + (size_t)m * H;
+  constexpr int kMaxIt = 8;  // H <= 8192
+  float4 v[kMaxIt];
+  const int nit = H / 1024;
+  float ss = 0.f;
+#pragma unroll
+  for (int it = 0; it < kMaxIt; ++it) {
+    if (it < nit) {
+      const int i = it * 1024 + tid * 4;
+      float4 x;
+      if constexpr (MODE == 2) {
+        const bf16x4 e = *reinterpret_cast<const bf16x4*>(embed + (size_t)ids[m] * H + i);
+        x = make_float4(bf2f(e[0]), bf2f(e[1]), bf2f(e[2]), bf2f(e[3]));
+      } else {
+        x = *reinterpret_cast<const float4*>(rrow + i);
+        if constexpr (MODE == 1) {
+          const bf16x4 d = *reinterpret_cast<const bf16x4*>(delta + (size_t)m * H + i);
+          x.x += bf2f(d[0]); x.y += bf2f(d[1]); x.z += bf2f(d[2]); x.w += bf2f(d[3]);
+        }
+      }
+      if constexpr (MODE != 0) *reinterpret_cast<float4*>(rrow + i) = x;
+      v[it] = x;
+      ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+    }
+  }
+  ss = wave_sum(ss);
+  __shared__ float red[4];
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = rsqrtf(tot / (float)H + eps);
+#pragma unroll
+  for (int it = 0; it < kMaxIt; ++it) {
+    if (it < nit) {
+      const int i = it * 1024 + tid * 4;
+      const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + i);
+      bf16x4 o;
+      o[0] = f2bf(v[it].x * inv * bf2f(wv[0]));
+      o[1] = f2bf(v[it].y * inv * bf2f(wv[1]));
+      o[2] = f2bf(v[it].z * inv * bf2f(wv[2]));
+      o[3] = f2bf(v[it].w * inv * bf2f(wv[3]));
+      *reinterpret_cast<bf16x4*>(y + (size_t)m * H + i) = o;
+    }
+  }
+}
+
+// ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
+// qkv: [T, (hq + 2 hkv) * 128] bf16 in the engine's permuted column order (inside each 16-column
+// tile j of a head: columns 0..7 = dims 8j..8j+7, columns 8..15 = dims 64+8j..64+8j+7).
+// One workgroup per token, one thread per (unit, pair) for rotary units and per column for V.
+__global__ void __launch_bounds__(256)
+rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* __restrict__ positions,
+                     const int* __restrict__ slots, const float2* __restrict__ rope,
+                     bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache) {
+  const int t = blockIdx.x;
+  const int ncols = (hq + 2 * hkv) * 128;
+  const bf16* row = qkv + (size_t)t * ncols;
+  const int pos = positions[t], slot = slots[t];
+  const int blk = slot >= 0 ? slot / kPageTok : 0, off = slot >= 0 ? slot % kPageTok : 0;
+  // rotary part: (hq + hkv) units × 64 pairs
+  for (int idx = threadIdx.x; idx < (hq + hkv) * 64; idx += blockDim.x) {
+    const int u = idx >> 6, pr = idx & 63;  // pr = rotary pair index = dim of the first half
+    const int j = pr >> 3, rr = pr & 7;
+    const float x1 = bf2f(row[u * 128 + 16 * j + rr]);
+    const float x2 = bf2f(row[u * 128 + 16 * j + 8 + rr]);
+    const float2 cs = rope[(size_t)pos * 64 + pr];
+    const float o1 = x1 * cs.x - x2 * cs.y, o2 = x2 * cs.x + x1 * cs.y;
+    if (u < hq) {
+      bf16* qp = q_out + ((size_t)t * hq + u) * 128;
+      qp[pr] = f2bf(o1);
+      qp[64 + pr] = f2bf(o2);
+    } else if (slot >= 0) {
+      bf16* kp = k_cache + (((size_t)blk * hkv + (u - hq)) * kPageTok + off) * 128;
+      kp[pr] = f2bf(o1);
+      kp[64 + pr] = f2bf(o2);
+    }
+  }
+  if (slot < 0) return;
+  for (int idx = threadIdx.x; idx < hkv * 128; idx += blockDim.x) {
+    const int h = idx >> 7, c = idx & 127;
+    const int j = c >> 4, rr = c & 15;
+    const int d = rr < 8 ? 8 * j + rr : 64 + 8 * j + (rr - 8);
+    v_cache[(((size_t)blk * hkv + h) * 128 + d) * kPageTok + vperm_tok(off)] =
+        row[(hq + hkv + h) * 128 + c];
+  }
+}
+
+// ---- SiLU·mul over the interleaved gate/up output of a library GEMM (prefill) ---------------
+// gu: [T, 2F] with 16-column tiles (0..7 gate[8t..8t+7], 8..15 up[8t..8t+7]) -> h: [T, F]
+__global__ void __launch_bounds__(256)
+silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ h, int F, int T) {
+  const size_t n = (size_t)T * (F / 8);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = i / (F / 8), tile = i % (F / 8);
+    const bf16x8 gv = *reinterpret_cast<const bf16x8*>(gu + t * 2 * F + tile * 16);
+    const bf16x8 uv = *reinterpret_cast<const bf16x8*>(gu + t * 2 * F + tile * 16 + 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(silu(bf2f(gv[j])) * bf2f(uv[j]));
+    *reinterpret_cast<bf16x8*>(h + t * F + tile * 8) = o;
+  }
+}
+
+// ---- decode-step metadata (runs first inside the captured graph) -----------------------------
+// For slot b: live sequences process the token at positions[b]; dead slots write nothing.
+__global__ void decode_prep_kernel(int B, const int* __restrict__ active, const int* __restrict__ positions,
+                                   const int* __restrict__ block_tables, int max_blocks,
+                                   int* __restrict__ slots, int* __restrict__ ctx_len,
+                                   int* __restrict__ q_len) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if (active[b]) {
+    const int pos = positions[b];
+    slots[b] = block_tables[(size_t)b * max_blocks + pos / kPageTok] * kPageTok + pos % kPageTok;
+    ctx_len[b] = pos + 1;
+    q_len[b] = 1;
+  } else {
+    slots[b] = -1;
+    ctx_len[b] = 0;
+    q_len[b] = 0;
+  }
+}
+
+// Token-ring head advance (one thread), the last node of a step.
+__global__ void ring_advance_kernel(int* counter) { counter[0] += 1; }
+
+}  // namespace dsse
+
+using namespace dsse;
+
+extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta,
+                                   const void* embed, const int* ids, const void* w, void* y,
+                                   float eps, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  const bf16* d = reinterpret_cast<const bf16*>(delta);
+  const bf16* e = reinterpret_cast<const bf16*>(embed);
+  const bf16* wp = reinterpret_cast<const bf16*>(w);
+  bf16* yp = reinterpret_cast<bf16*>(y);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
+    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
+    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
+                                         const int* slots, const float2* rope, void* q_out,
+                                         void* k_cache, void* v_cache, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rope_kv_write_kernel, dim3(T), dim3(256), 0, st,
+                     reinterpret_cast<const bf16*>(qkv), hq, hkv, positions, slots, rope,
+                     reinterpret_cast<bf16*>(q_out), reinterpret_cast<bf16*>(k_cache),
+                     reinterpret_cast<bf16*>(v_cache));
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st) {
+  if (T <= 0) return hipSuccess;
+  const size_t n = (size_t)T * (F / 8);
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, st,
+                     reinterpret_cast<const bf16*>(gu), reinterpret_cast<bf16*>(h), F, T);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsse_decode_prep(int B, const int* active, const int* positions,
+                                       const int* block_tables, int max_blocks, int* slots,
+                                       int* ctx_len, int* q_len, hipStream_t st) {
+  hipLaunchKernelGGL(decode_prep_kernel, dim3((B + 255) / 256), dim3(256), 0, st, B, active,
+                     positions, block_tables, max_blocks, slots, ctx_len, q_len);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsse_ring_advance(int* counter, hipStream_t st) {
+  hipLaunchKernelGGL(ring_advance_kernel, dim3(1), dim3(1), 0, st, counter);
+  return hipGetLastError();
+}

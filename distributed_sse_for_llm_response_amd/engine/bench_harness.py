@@ -1,0 +1,148 @@
+"""Decode-throughput harness behind bench.py (one engine replica per rank)."""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from ..models.mistral import TINY, get_config
+from ..parallel.comm import TPComm
+from .kv_cache import PAGE, KVCache, blocks_needed
+from .model_runner import RING_SIZE, ModelRunner, PrefillSeq
+from .weights import random_engine_weights
+
+
+class _Drain:
+    """Side-stream device->host copy of one token-ring row per step into pinned memory."""
+
+    def __init__(self, runner: ModelRunner):
+        self.r = runner
+        self.cuda = runner.device.type == "cuda"
+        B = runner.max_batch
+        if self.cuda:
+            self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32).pin_memory()
+            self.stream = torch.cuda.Stream(runner.device)
+            self.done = [torch.cuda.Event() for _ in range(RING_SIZE)]
+        else:
+            self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32)
+
+    def issue(self, row: int, B: int):
+        if not self.cuda:
+            self.host[row, :B] = self.r.ring[row, :B]
+            return
+        main = torch.cuda.current_stream(self.r.device)
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            self.host[row, :B].copy_(self.r.ring[row, :B], non_blocking=True)
+            self.done[row].record(self.stream)
+
+    def wait(self, row: int):
+        if self.cuda:
+            self.done[row].synchronize()
+        return self.host[row]
+
+
+def _build_runner(model: str, device, streams: int, prompt_len: int, total_steps: int, tp: int, use_graphs: bool,
+                  rank: int, world: int):
+    cfg = get_config(model) if device.type == "cuda" else TINY
+    comm = TPComm()
+    if tp > 1:
+        import torch.distributed as dist
+
+        from ..parallel.comm import make_groups
+
+        grp, _ = make_groups(world, tp)
+        comm = TPComm(rank=rank % tp, size=tp, group=grp)
+    w = random_engine_weights(cfg, tp_rank=comm.rank, tp_size=comm.size, device=device, seed=1234)
+    max_len = prompt_len + total_steps + 2 * PAGE
+    nblk = streams * (blocks_needed(max_len) + 1) + 4
+    runner = ModelRunner(w, num_blocks=nblk, max_batch=streams, max_model_len=max_len, device=device, comm=comm,
+                         use_graphs=use_graphs)
+    return cfg, runner
+
+
+def run_decode_bench(model="mistral-7b-v0.3", device=None, streams=64, prompt_len=512, steps=64, warmup=8, tp=1,
+                     delivery="frame", use_graphs=True, rank=0, world=1, seed=0):
+    device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    total = steps + warmup
+    cfg, r = _build_runner(model, device, streams, prompt_len, total, tp, use_graphs, rank, world)
+    gen = torch.Generator().manual_seed(seed + rank)
+    V = cfg.vocab_size
+    # ---- admit `streams` sequences: block tables, sampling params (vLLM defaults: T=1, top_p=1) ----
+    per = blocks_needed(prompt_len + total + 1)
+    bt = torch.zeros(streams, r.max_blocks, dtype=torch.int32)
+    seqs = []
+    for s in range(streams):
+        blocks = list(range(s * per, (s + 1) * per))
+        bt[s, :per] = torch.tensor(blocks, dtype=torch.int32)
+        toks = torch.randint(3, V, (prompt_len,), generator=gen).tolist()
+        seqs.append(PrefillSeq(slot=s, tokens=toks, start_pos=0, block_table=blocks, last_chunk=True))
+    r.block_tables.copy_(bt.to(device))
+    r.temperature.fill_(1.0)
+    r.top_p.fill_(1.0)
+    r.top_k.fill_(0)
+    r.seeds.copy_(torch.randint(0, 2**31 - 1, (streams, 2), generator=gen, dtype=torch.int32).to(device))
+    # ---- prefill in packed chunks of <= max_prefill_tokens ----
+    chunk = max(1, r.max_prefill_tokens // max(1, prompt_len))
+    for i in range(0, streams, chunk):
+        r.prefill(seqs[i:i + chunk], ring_row=0)
+    r.active.fill_(1)
+    if use_graphs and device.type == "cuda":
+        r.capture([streams])
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    head = int(r.ring_counter.item())
+    drain = _Drain(r)
+    conv_ids = [f"bench-{rank}-{s}" for s in range(streams)]
+    seq_no = [0] * streams
+    frames_bytes = 0
+    deliver_ts = []
+
+    def deliver(row):
+        nonlocal frames_bytes
+        toks = drain.wait(row)[:streams].tolist()
+        now = time.time_ns()
+        if delivery != "none":
+            for s, t in enumerate(toks):
+                seq_no[s] += 1
+                body = ('{"conversation_id":"%s","token":"%s","sequence":%d,"done":false,"timestamp":%d}'
+                        % (conv_ids[s], "t%d" % t, seq_no[s], now))
+                frame = "event: token\nid: %d\ndata: %s\n\n" % (seq_no[s], body)
+                frames_bytes += len(frame)
+        deliver_ts.append(time.perf_counter())
+
+    def run(n):
+        nonlocal head
+        prev = None
+        for _ in range(n):
+            r.decode(streams)
+            row = head % RING_SIZE
+            head += 1
+            drain.issue(row, streams)
+            if prev is not None:
+                deliver(prev)
+            prev = row
+        if prev is not None:
+            deliver(prev)
+
+    run(warmup)
+    deliver_ts.clear()
+    _sync(device, world)
+    t0 = time.perf_counter()
+    run(steps)
+    _sync(device, world)
+    elapsed = time.perf_counter() - t0
+    itl = np.diff(np.array(deliver_ts)) * 1000.0 if len(deliver_ts) > 1 else np.array([elapsed * 1000.0])
+    return {"elapsed_s": elapsed, "p50_itl_ms": float(np.percentile(itl, 50)),
+            "p99_itl_ms": float(np.percentile(itl, 99)), "frames_bytes": frames_bytes, "model": cfg.name}
+
+
+def _sync(device, world):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()

@@ -1,0 +1,318 @@
+"""Mistral forward passes on the engine's kernels: hipGraph-captured decode step + chunked prefill.
+
+Decode step for a batch bucket of B slots (all device-resident, no host round trip):
+
+    decode_prep          slots / ctx_len / q_len from positions + block tables
+    embed+rmsnorm        resid = E[ids]; x = norm(resid)
+    per layer:
+      gemm_qkv_rope      x·Wqkvᵀ, RoPE, K/V written into the paged cache, q for attention
+      paged_attention    flash-decoding over the pages (+ partition combine)
+      gemm_resid         resid += attn·Woᵀ          (TP>1: gemm_out + RCCL all-reduce + add)
+      rmsnorm            x = norm(resid)
+      gemm_silu          h = silu(x·Wgᵀ)·(x·Wuᵀ)
+      gemm_resid         resid += h·Wdᵀ             (TP>1: gemm_out + all-reduce + add)
+      rmsnorm            x = norm(resid) with the next layer's (or the final) weight
+    gemm_out (fp32)      logits = x·Wlmᵀ (vocab shard)
+    sample               Gumbel-max / greedy; ids[b] <- token, ring[head][b] <- token, positions += 1
+    ring_advance         head += 1
+
+The sampled token becomes the next step's input in place, so consecutive steps need no host sync;
+the host drains the token ring asynchronously (engine.py).  The whole step is captured once per
+batch bucket into a torch.cuda.CUDAGraph (a hipGraph on ROCm).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..ops.reference import rope_table
+from ..parallel.comm import TPComm
+from .kv_cache import PAGE, KVCache
+from .weights import EngineWeights
+
+RING_SIZE = 64
+
+
+def batch_buckets(max_batch: int):
+    out, b = [], 1
+    while b < max_batch:
+        out.append(b)
+        b *= 2
+    out.append(max_batch)
+    return sorted(set(out))
+
+
+def decode_partitioning(B: int, nkv: int, max_ctx: int, target_wgs: int = 1024, max_parts: int = 32):
+    """(part, nparts) for flash-decoding so that B·Hkv·nparts workgroups fill the chip."""
+    want = max(1, min(max_parts, math.ceil(target_wgs / max(1, B * nkv))))
+    part = max(128, math.ceil(max_ctx / want / 128) * 128)
+    nparts = math.ceil(max_ctx / part)
+    return part, nparts
+
+
+@dataclass
+class PrefillSeq:
+    slot: int               # decode slot the sequence occupies
+    tokens: list            # token ids of this chunk
+    start_pos: int          # absolute position of tokens[0]
+    block_table: list       # the sequence's full block table
+    last_chunk: bool        # sample a token after this chunk
+
+
+class ModelRunner:
+    def __init__(self, w: EngineWeights, num_blocks: int, max_batch: int = 64, max_model_len: int = 4096,
+                 max_prefill_tokens: int = 8192, device="cuda", comm: TPComm | None = None, use_graphs=None):
+        self.w, self.cfg = w, w.cfg
+        self.device = torch.device(device)
+        self.comm = comm or TPComm()
+        self.max_batch = max_batch
+        self.max_model_len = max_model_len
+        self.max_blocks = math.ceil(max_model_len / PAGE) + 1
+        self.max_prefill_tokens = max_prefill_tokens
+        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
+        cfg, dev = self.cfg, self.device
+        H = cfg.hidden_size
+        nh, nkv, F, V = w.nh, w.nkv, w.ffn, w.vocab_local
+        self.kv = KVCache(cfg.num_layers, num_blocks, nkv, dev)
+        self.rope = rope_table(max(cfg.max_position, max_model_len + 1), cfg.rope_theta, dev)
+        Bm = max_batch
+        i32 = dict(device=dev, dtype=torch.int32)
+        # ---- decode state (slot-indexed, device resident) ----
+        self.ids = torch.zeros(Bm, **i32)
+        self.positions = torch.zeros(Bm, **i32)
+        self.active = torch.zeros(Bm, **i32)
+        self.block_tables = torch.zeros(Bm, self.max_blocks, **i32)
+        self.slots = torch.full((Bm,), -1, **i32)
+        self.ctx_len = torch.zeros(Bm, **i32)
+        self.q_len = torch.zeros(Bm, **i32)
+        self.q_start = torch.arange(Bm, **i32)
+        self.work_seq = torch.arange(Bm, **i32)
+        self.work_tile = torch.zeros(Bm, **i32)
+        self.temperature = torch.zeros(Bm, device=dev, dtype=torch.float32)
+        self.top_k = torch.zeros(Bm, **i32)
+        self.top_p = torch.ones(Bm, device=dev, dtype=torch.float32)
+        self.seeds = torch.zeros(Bm, 2, **i32)
+        self.ring = torch.zeros(RING_SIZE, Bm, **i32)
+        self.ring_counter = torch.zeros(1, **i32)
+        # ---- decode activations ----
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        self.resid = torch.zeros(Bm, H, device=dev, dtype=torch.float32)
+        self.x = torch.zeros(Bm, H, **bf)
+        self.q = torch.zeros(Bm, nh * 128, **bf)
+        self.attn = torch.zeros(Bm, nh * 128, **bf)
+        self.h = torch.zeros(Bm, F, **bf)
+        self.tmp = torch.zeros(Bm, H, **bf)
+        self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
+        self.cand = torch.zeros(Bm, 2, device=dev, dtype=torch.float32)
+        self._cand_bufs = {}
+        part, nparts = decode_partitioning(1, nkv, max_model_len)
+        ws = max(decode_partitioning(b, nkv, max_model_len)[1] * b for b in batch_buckets(Bm))
+        self.part_o = torch.zeros(max(1, ws) * nkv * 16 * 128, device=dev, dtype=torch.float32)
+        self.part_ml = torch.zeros(max(1, ws) * nkv * 16 * 2, device=dev, dtype=torch.float32)
+        self.graphs = {}
+        self.graph_pool = None
+
+    # ------------------------------------------------------------------ decode
+    def decode_forward(self, B: int) -> None:
+        """One decode step over slots [0, B) (graph-capturable: fixed shapes, no host sync)."""
+        w, cfg, comm = self.w, self.cfg, self.comm
+        nh, nkv = w.nh, w.nkv
+        r = slice(0, B)
+        eps = cfg.rms_eps
+        ops.decode_prep(self.active[r], self.positions[r], self.block_tables[r], self.slots[r], self.ctx_len[r],
+                        self.q_len[r])
+        resid, x = self.resid[r], self.x[r]
+        ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=self.ids[r])
+        part, nparts = decode_partitioning(B, nkv, self.max_model_len)
+        q3 = self.q[r].view(B, nh, 128)
+        a3 = self.attn[r].view(B, nh, 128)
+        nl = len(w.layers)
+        for li, L in enumerate(w.layers):
+            ops.gemm_qkv_rope(x, L.wqkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+                              self.kv.v[li], nh, nkv)
+            ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
+                                self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
+                                self.part_ml, part, nparts)
+            if comm.size == 1:
+                ops.gemm_resid(self.attn[r], L.wo, resid)
+                ops.rmsnorm(resid, L.ffn_norm, x, eps)
+            else:
+                ops.gemm_out(self.attn[r], L.wo, self.tmp[r])
+                comm.all_reduce(self.tmp[r])
+                ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=self.tmp[r])
+            ops.gemm_silu(x, L.wgu, self.h[r])
+            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+            if comm.size == 1:
+                ops.gemm_resid(self.h[r], L.wd, resid)
+                ops.rmsnorm(resid, w_next, x, eps)
+            else:
+                ops.gemm_out(self.h[r], L.wd, self.tmp[r])
+                comm.all_reduce(self.tmp[r])
+                ops.rmsnorm(resid, w_next, x, eps, delta=self.tmp[r])
+        ops.gemm_out(x, w.lm_head, self.logits[r])
+        self._sample_commit(B)
+        ops.ring_advance(self.ring_counter)
+
+    def _sample_commit(self, B: int) -> None:
+        r = slice(0, B)
+        args = (self.temperature[r], self.top_k[r], self.top_p[r], self.seeds[r], self.positions[r], self.active[r])
+        if self.comm.size == 1:
+            ops.sample(self.logits[r], *args, self.ids[r], self.ring, self.ring_counter, self.positions[r], None, 0)
+        else:
+            # vocab-parallel: each rank proposes its Gumbel-max candidate, 8 bytes per sequence cross the link
+            ops.sample(self.logits[r], *args, self.ids[r], None, None, None, self.cand[r], self.w.vocab_offset)
+            flat = self._cand_bufs.get(B)
+            if flat is None:
+                flat = self._cand_bufs[B] = torch.zeros(self.comm.size * B * 2, device=self.device,
+                                                        dtype=torch.float32)
+            self.comm.all_gather_into(flat, self.cand[r].contiguous().view(-1))
+            ops.sample_pick(flat, self.comm.size, *args, self.ids[r], self.ring, self.ring_counter,
+                            self.positions[r])
+
+    def bucket_for(self, n_active_max_slot: int) -> int:
+        for b in batch_buckets(self.max_batch):
+            if b >= n_active_max_slot:
+                return b
+        return self.max_batch
+
+    def capture(self, buckets=None) -> None:
+        """Capture the decode step of each batch bucket into its own graph (shared memory pool)."""
+        if not self.use_graphs:
+            return
+        buckets = buckets or batch_buckets(self.max_batch)
+        # Warm up on a side stream (allocator + library init) before capture.
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        saved = self._snapshot_state()
+        with torch.cuda.stream(s):
+            for B in buckets:
+                self.decode_forward(B)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for B in sorted(buckets, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self.decode_forward(B)
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.graphs[B] = g
+        torch.cuda.synchronize(self.device)
+        self._restore_state(saved)
+
+    def _snapshot_state(self):
+        return [t.clone() for t in (self.ids, self.positions, self.ring, self.ring_counter)]
+
+    def _restore_state(self, saved):
+        for t, s in zip((self.ids, self.positions, self.ring, self.ring_counter), saved):
+            t.copy_(s)
+
+    def decode(self, B: int) -> None:
+        g = self.graphs.get(B)
+        if g is not None:
+            g.replay()
+        else:
+            self.decode_forward(B)
+
+    # ------------------------------------------------------------------ prefill
+    def prefill(self, seqs: list, ring_row: int) -> None:
+        """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
+        first token into ids[slot] and ring[ring_row, slot] and get positions[slot] set on device."""
+        if not seqs:
+            return
+        w, cfg, comm, dev = self.w, self.cfg, self.comm, self.device
+        nh, nkv, F = w.nh, w.nkv, w.ffn
+        H, eps = cfg.hidden_size, cfg.rms_eps
+        n = len(seqs)
+        ids, pos, slots = [], [], []
+        q_start, q_len, ctx_len, work_seq, work_tile = [], [], [], [], []
+        bt = torch.zeros(n, self.max_blocks, dtype=torch.int32)
+        for i, s in enumerate(seqs):
+            q_start.append(len(ids))
+            for j, t in enumerate(s.tokens):
+                p = s.start_pos + j
+                ids.append(t)
+                pos.append(p)
+                slots.append(s.block_table[p // PAGE] * PAGE + p % PAGE)
+            q_len.append(len(s.tokens))
+            ctx_len.append(s.start_pos + len(s.tokens))
+            bt[i, : len(s.block_table)] = torch.tensor(s.block_table, dtype=torch.int32)
+            for tile in range(math.ceil(len(s.tokens) / 16)):
+                work_seq.append(i)
+                work_tile.append(tile)
+        T = len(ids)
+        meta = torch.tensor(ids + pos + slots + q_start + q_len + ctx_len + work_seq + work_tile, dtype=torch.int32)
+        if dev.type == "cuda":
+            meta = meta.pin_memory().to(dev, non_blocking=True)
+            bt = bt.pin_memory().to(dev, non_blocking=True)
+        o = 0
+        d_ids, o = meta[o:o + T], o + T
+        d_pos, o = meta[o:o + T], o + T
+        d_slots, o = meta[o:o + T], o + T
+        d_qs, o = meta[o:o + n], o + n
+        d_ql, o = meta[o:o + n], o + n
+        d_ctx, o = meta[o:o + n], o + n
+        nw = len(work_seq)
+        d_ws, o = meta[o:o + nw], o + nw
+        d_wt, o = meta[o:o + nw], o + nw
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        resid = torch.empty(T, H, **f32)
+        x = torch.empty(T, H, **bf)
+        q = torch.empty(T, nh, 128, **bf)
+        attn = torch.empty(T, nh, 128, **bf)
+        h = torch.empty(T, F, **bf)
+        max_ctx = max(ctx_len)
+        part = math.ceil(max_ctx / 32) * 32
+        ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d_ids)
+        nl = len(w.layers)
+        for li, L in enumerate(w.layers):
+            qkv = x @ L.wqkv.t()
+            ops.rope_kv_write(qkv, d_pos, d_slots, self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
+            del qkv
+            ops.paged_attention(1, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
+                                self.part_o, self.part_ml, part, 1)
+            o_proj = attn.view(T, nh * 128) @ L.wo.t()
+            comm.all_reduce(o_proj)
+            ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=o_proj)
+            gu = x @ L.wgu.t()
+            ops.silu_mul(gu, h)
+            del gu
+            down = h @ L.wd.t()
+            comm.all_reduce(down)
+            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+            ops.rmsnorm(resid, w_next, x, eps, delta=down)
+        last = [i for i, s in enumerate(seqs) if s.last_chunk]
+        if not last:
+            return
+        rows = torch.tensor([q_start[i] + q_len[i] - 1 for i in last], dtype=torch.long, device=dev)
+        xl = x.index_select(0, rows)
+        logits = (xl.float() @ w.lm_head.float().t()) if dev.type == "cpu" else None
+        if logits is None:
+            logits = torch.empty(len(last), w.vocab_local, **f32)
+            if len(last) <= 64:
+                ops.gemm_out(xl, w.lm_head, logits)
+            else:
+                logits = (xl @ w.lm_head.t()).float()
+        slot_idx = torch.tensor([seqs[i].slot for i in last], dtype=torch.long, device=dev)
+        last_pos = torch.tensor([seqs[i].start_pos + len(seqs[i].tokens) - 1 for i in last], dtype=torch.int32,
+                                device=dev)
+        nL = len(last)
+        new_ids = torch.zeros(nL, dtype=torch.int32, device=dev)
+        temp = self.temperature.index_select(0, slot_idx)
+        tk = self.top_k.index_select(0, slot_idx)
+        tp = self.top_p.index_select(0, slot_idx)
+        sd = self.seeds.index_select(0, slot_idx).contiguous()
+        if comm.size == 1:
+            ops.sample(logits, temp, tk, tp, sd, last_pos, None, new_ids)
+        else:
+            cand = torch.zeros(nL, 2, **f32)
+            ops.sample(logits, temp, tk, tp, sd, last_pos, None, new_ids, None, None, None, cand, w.vocab_offset)
+            cand_all = torch.zeros(comm.size * nL * 2, **f32)
+            comm.all_gather_into(cand_all, cand.view(-1))
+            ops.sample_pick(cand_all, comm.size, temp, tk, tp, sd, last_pos, None, new_ids)
+        self.ids.index_copy_(0, slot_idx, new_ids)
+        self.ring[ring_row].index_copy_(0, slot_idx, new_ids)
+        self.positions.index_copy_(0, slot_idx, last_pos + 1)

@@ -1,0 +1,157 @@
+"""Engine ops: gfx950 HIP kernels on GPU tensors, fp32 PyTorch references on CPU tensors.
+
+The HIP library (``_lib/libdsse_kernels.so``, built by ``_build.build_kernels``) registers the
+operators under ``torch.ops.dsse``.  Dispatch is by tensor device only:
+
+* GPU tensor  -> the HIP kernel, always.  If the library is missing or failed to load, the call
+  raises: there is no eager-PyTorch fallback on the GPU path.
+* CPU tensor  -> the reference implementation in ``ops/reference.py`` (plumbing tests in the
+  GPU-less build container).
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import torch
+
+from . import reference as ref
+
+_LIB = Path(__file__).resolve().parent.parent / "_lib" / "libdsse_kernels.so"
+_loaded = False
+_load_error: str | None = None
+
+
+def load_library(required: bool = False) -> bool:
+    """Load the HIP kernel library once.  Returns True when torch.ops.dsse is available."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    if not _LIB.exists() and os.environ.get("DSSE_AUTOBUILD", "1") == "1":
+        try:
+            from .._build import build_kernels
+
+            build_kernels()
+        except Exception as e:  # noqa: BLE001 - reported below
+            _load_error = f"build failed: {e}"
+    if _LIB.exists():
+        try:
+            torch.ops.load_library(str(_LIB))
+            _loaded = True
+        except Exception as e:  # noqa: BLE001
+            _load_error = f"load failed: {e}"
+    elif _load_error is None:
+        _load_error = f"{_LIB} not built"
+    if required and not _loaded:
+        raise RuntimeError(f"dsse HIP kernels unavailable ({_load_error}); run `python -m "
+                           "distributed_sse_for_llm_response_amd._build kernels`")
+    return _loaded
+
+
+def library_path() -> Path:
+    return _LIB
+
+
+def _hip(t: torch.Tensor) -> bool:
+    if t.is_cuda:
+        load_library(required=True)
+        return True
+    return False
+
+
+def gemm_out(x, w, out):
+    """out[M, N] = x[M, K] · w[N, K]ᵀ (bf16 or fp32 out)."""
+    if _hip(x):
+        torch.ops.dsse.gemm_out(x, w, out)
+    else:
+        ref.gemm_out(x, w, out)
+
+
+def gemm_resid(x, w, resid):
+    """resid[M, N] (fp32) += x · wᵀ."""
+    if _hip(x):
+        torch.ops.dsse.gemm_resid(x, w, resid)
+    else:
+        ref.gemm_resid(x, w, resid)
+
+
+def gemm_silu(x, w, out):
+    """out[M, N/2] = silu(gate) * up with the interleaved gate/up weight rows."""
+    if _hip(x):
+        torch.ops.dsse.gemm_silu(x, w, out)
+    else:
+        ref.gemm_silu(x, w, out)
+
+
+def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
+    """Fused QKV projection + RoPE + paged KV write (decode)."""
+    if _hip(x):
+        torch.ops.dsse.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+    else:
+        ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+
+
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None):
+    if _hip(resid):
+        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids)
+    else:
+        ref.rmsnorm(resid, w, y, eps, delta, embed, ids)
+
+
+def rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
+    if _hip(qkv):
+        torch.ops.dsse.rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+    else:
+        ref.rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+
+
+def silu_mul(gu, h):
+    if _hip(gu):
+        torch.ops.dsse.silu_mul(gu, h)
+    else:
+        ref.silu_mul(gu, h)
+
+
+def decode_prep(active, positions, block_tables, slots, ctx_len, q_len):
+    if _hip(active):
+        torch.ops.dsse.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
+    else:
+        ref.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
+
+
+def ring_advance(counter):
+    if _hip(counter):
+        torch.ops.dsse.ring_advance(counter)
+    else:
+        ref.ring_advance(counter)
+
+
+def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, out,
+                    part_o, part_ml, part, nparts):
+    """mode 0 = decode (flash-decoding partitions), mode 1 = prefill (causal, one partition)."""
+    if _hip(q):
+        torch.ops.dsse.paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
+                                       work_tile, out, part_o, part_ml, part, nparts)
+    else:
+        ref.paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile,
+                            out, part_o, part_ml, part, nparts)
+
+
+def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
+           positions_inc=None, cand=None, vocab_offset=0):
+    if _hip(logits):
+        torch.ops.dsse.sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring,
+                              ring_counter, positions_inc, cand, vocab_offset)
+    else:
+        ref.sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring, ring_counter,
+                   positions_inc, cand, vocab_offset)
+
+
+def sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None,
+                ring_counter=None, positions_inc=None):
+    if _hip(cand_all):
+        torch.ops.dsse.sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids,
+                                   ring, ring_counter, positions_inc)
+    else:
+        ref.sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids, ring,
+                        ring_counter, positions_inc)

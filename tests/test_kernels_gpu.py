@@ -1,0 +1,286 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference of the same op."""
+import math
+import os
+
+import pytest
+import torch
+
+from distributed_sse_for_llm_response_amd import ops
+from distributed_sse_for_llm_response_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, dev, scale=1.0, dtype=torch.bfloat16, gen=None):
+    return (torch.randn(*shape, generator=gen) * scale).to(dtype).to(dev)
+
+
+def _close(a, b, atol, rtol, what=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad} / {a.numel()} elements off; max err {err.max().item():.4g}"
+
+
+@pytest.fixture(params=[(0, 0), (1, 4), (1, 8), (2, 4), (2, 8)], ids=lambda p: f"nt{p[0]}kw{p[1]}")
+def tiles(request, monkeypatch):
+    nt, kw = request.param
+    if nt:
+        monkeypatch.setenv("DSSE_GEMM_NT", str(nt))
+        monkeypatch.setenv("DSSE_GEMM_KW", str(kw))
+    return request.param
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 17, 40, 64])
+def test_gemm_out_bf16_f32(gpu, tiles, M):
+    g = torch.Generator().manual_seed(M)
+    x = _rand(M, 1024, dev=gpu, gen=g)
+    w = _rand(512, 1024, dev=gpu, scale=1 / 32, gen=g)
+    for dt in (torch.bfloat16, torch.float32):
+        out = torch.zeros(M, 512, device=gpu, dtype=dt)
+        ref = torch.zeros(M, 512, dtype=dt)
+        ops.gemm_out(x, w, out)
+        R.gemm_out(x.cpu(), w.cpu(), ref)
+        _close(out, ref, 2e-2 if dt == torch.bfloat16 else 1e-3, 1e-2, f"gemm_out {dt}")
+
+
+@pytest.mark.parametrize("M,K", [(3, 4096), (64, 1536), (33, 14336)])
+def test_gemm_resid(gpu, tiles, M, K):
+    g = torch.Generator().manual_seed(K)
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = _rand(256, K, dev=gpu, scale=1 / math.sqrt(K), gen=g)
+    r0 = torch.randn(M, 256, generator=g)
+    r = r0.clone().to(gpu)
+    ops.gemm_resid(x, w, r)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    _close(r, r0, 1e-3, 1e-3, "gemm_resid")
+
+
+@pytest.mark.parametrize("M", [1, 20, 64])
+def test_gemm_silu(gpu, tiles, M):
+    g = torch.Generator().manual_seed(M + 100)
+    x = _rand(M, 2048, dev=gpu, gen=g)
+    w = _rand(2 * 704, 2048, dev=gpu, scale=1 / 45, gen=g)
+    out = torch.zeros(M, 704, device=gpu, dtype=torch.bfloat16)
+    ref = torch.zeros(M, 704, dtype=torch.bfloat16)
+    ops.gemm_silu(x, w, out)
+    R.gemm_silu(x.cpu(), w.cpu(), ref)
+    _close(out, ref, 2e-2, 2e-2, "gemm_silu")
+
+
+@pytest.mark.parametrize("M", [1, 9, 64])
+def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
+    nh, nkv, H = 8, 2, 1024
+    g = torch.Generator().manual_seed(M + 7)
+    x = _rand(M, H, dev=gpu, gen=g)
+    w = _rand((nh + 2 * nkv) * 128, H, dev=gpu, scale=1 / 32, gen=g)
+    rope = R.rope_table(4096, 1e6, gpu)
+    positions = torch.randint(0, 4000, (M,), generator=g, dtype=torch.int32)
+    slots = torch.randperm(8 * 32, generator=g)[:M].to(torch.int32)
+    slots[0] = -1  # a padding row must not write the cache
+    q = torch.zeros(M, nh * 128, device=gpu, dtype=torch.bfloat16)
+    kc = torch.zeros(8, nkv, 32, 128, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros(8, nkv, 128, 32, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_qkv_rope(x, w, positions.to(gpu), slots.to(gpu), rope, q, kc, vc, nh, nkv)
+    qr, kr, vr = torch.zeros(M, nh * 128, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    R.gemm_qkv_rope(x.cpu(), w.cpu(), positions, slots, rope.cpu(), qr, kr, vr, nh, nkv)
+    _close(q, qr, 3e-2, 2e-2, "q")
+    _close(kc, kr, 3e-2, 2e-2, "k cache")
+    _close(vc, vr, 3e-2, 2e-2, "v cache")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("M,H", [(1, 4096), (37, 4096), (5, 1024), (3, 8192)])
+def test_rmsnorm(gpu, mode, M, H):
+    g = torch.Generator().manual_seed(M * 3 + mode)
+    resid0 = torch.randn(M, H, generator=g)
+    w = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16()
+    delta = torch.randn(M, H, generator=g).bfloat16() if mode == 1 else None
+    embed = torch.randn(64, H, generator=g).bfloat16() if mode == 2 else None
+    ids = torch.randint(0, 64, (M,), generator=g, dtype=torch.int32) if mode == 2 else None
+    r_gpu = resid0.clone().to(gpu)
+    y = torch.zeros(M, H, device=gpu, dtype=torch.bfloat16)
+    yr = torch.zeros(M, H, dtype=torch.bfloat16)
+    to = (lambda t: None if t is None else t.to(gpu))
+    ops.rmsnorm(r_gpu, w.to(gpu), y, 1e-5, to(delta), to(embed), to(ids))
+    R.rmsnorm(resid0, w, yr, 1e-5, delta, embed, ids)
+    _close(r_gpu, resid0, 1e-5, 1e-5, "resid")
+    _close(y, yr, 2e-2, 1e-2, "y")
+
+
+def test_rope_kv_write_and_silu_mul(gpu):
+    nh, nkv, T = 8, 2, 45
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(T, (nh + 2 * nkv) * 128, generator=g).bfloat16()
+    positions = torch.arange(100, 100 + T, dtype=torch.int32)
+    slots = torch.randperm(4 * 32, generator=g)[:T].to(torch.int32)
+    rope = R.rope_table(1024, 1e6)
+    q, kc, vc = (torch.zeros(T, nh, 128, dtype=torch.bfloat16), torch.zeros(4, nkv, 32, 128, dtype=torch.bfloat16),
+                 torch.zeros(4, nkv, 128, 32, dtype=torch.bfloat16))
+    qg, kg, vg = q.to(gpu), kc.to(gpu), vc.to(gpu)
+    ops.rope_kv_write(qkv.to(gpu), positions.to(gpu), slots.to(gpu), rope.to(gpu), qg, kg, vg, nh, nkv)
+    R.rope_kv_write(qkv, positions, slots, rope, q, kc, vc, nh, nkv)
+    _close(qg, q, 2e-2, 1e-2, "q")
+    _close(kg, kc, 2e-2, 1e-2, "k")
+    _close(vg, vc, 0, 0, "v")
+    gu = torch.randn(T, 2 * 1408, generator=g).bfloat16()
+    h, hr = torch.zeros(T, 1408, device=gpu, dtype=torch.bfloat16), torch.zeros(T, 1408, dtype=torch.bfloat16)
+    ops.silu_mul(gu.to(gpu), h)
+    R.silu_mul(gu, hr)
+    _close(h, hr, 1e-2, 1e-2, "silu_mul")
+
+
+def _attn_setup(ctxs, qlens, hq=32, hkv=8, gen=None, blocks=None):
+    B = len(ctxs)
+    nblk_seq = [math.ceil(c / 32) for c in ctxs]
+    total = sum(nblk_seq) + 2
+    perm = torch.randperm(total, generator=gen).tolist()
+    kc = torch.randn(total, hkv, 32, 128, generator=gen).bfloat16()
+    vc = torch.randn(total, hkv, 128, 32, generator=gen).bfloat16()
+    maxb = max(nblk_seq) + 1
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    o = 0
+    for b in range(B):
+        bt[b, : nblk_seq[b]] = torch.tensor(perm[o:o + nblk_seq[b]], dtype=torch.int32)
+        o += nblk_seq[b]
+    T = sum(qlens)
+    q = torch.randn(T, hq, 128, generator=gen).bfloat16()
+    q_start = torch.tensor([sum(qlens[:b]) for b in range(B)], dtype=torch.int32)
+    return kc, vc, bt, q, q_start
+
+
+@pytest.mark.parametrize("ctxs", [[1, 31, 32, 33, 300], [2000, 4096, 77], [1, 1, 1]])
+@pytest.mark.parametrize("part", [128, 512, 8192])
+def test_paged_attention_decode(gpu, ctxs, part):
+    g = torch.Generator().manual_seed(sum(ctxs) + part)
+    B = len(ctxs)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, [1] * B, gen=g)
+    qlen = torch.ones(B, dtype=torch.int32)
+    qlen[-1] = 0 if B > 3 else 1  # an inactive slot
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    ws, wt = torch.arange(B, dtype=torch.int32), torch.zeros(B, dtype=torch.int32)
+    nparts = math.ceil(max(ctxs) / part)
+    out = torch.zeros_like(q)
+    out_g = torch.zeros_like(q).to(gpu)
+    po = torch.zeros(B * 8 * nparts * 16 * 128, device=gpu)
+    pml = torch.zeros(B * 8 * nparts * 16 * 2, device=gpu)
+    ops.paged_attention(0, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
+                        ws.to(gpu), wt.to(gpu), out_g, po, pml, part, nparts)
+    R.paged_attention(0, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
+    live = qlen.bool()
+    _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention")
+
+
+@pytest.mark.parametrize("case", [([45], [45]), ([300, 17], [300, 17]), ([700, 64], [100, 64]), ([4096], [1000])])
+def test_paged_attention_prefill(gpu, case):
+    ctxs, qlens = case
+    g = torch.Generator().manual_seed(sum(ctxs))
+    B = len(ctxs)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, qlens, gen=g)
+    qlen, ctx = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
+    ws, wt = [], []
+    for b in range(B):
+        for t in range(math.ceil(qlens[b] / 16)):
+            ws.append(b)
+            wt.append(t)
+    ws, wt = torch.tensor(ws, dtype=torch.int32), torch.tensor(wt, dtype=torch.int32)
+    part = math.ceil(max(ctxs) / 32) * 32
+    out = torch.zeros_like(q)
+    out_g = torch.zeros_like(q).to(gpu)
+    dummy = torch.zeros(1, device=gpu)
+    ops.paged_attention(1, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
+                        ws.to(gpu), wt.to(gpu), out_g, dummy, dummy, part, 1)
+    R.paged_attention(1, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
+    _close(out_g, out, 1e-2, 2e-2, "prefill attention")
+
+
+def _sampler_inputs(B, V, gen, temps, topk, topp):
+    logits = torch.randn(B, V, generator=gen) * 3
+    t = torch.tensor(temps, dtype=torch.float32)
+    k = torch.tensor(topk, dtype=torch.int32)
+    p = torch.tensor(topp, dtype=torch.float32)
+    seeds = torch.randint(0, 2**31 - 1, (B, 2), generator=gen, dtype=torch.int32)
+    pos = torch.randint(0, 5000, (B,), generator=gen, dtype=torch.int32)
+    return logits, t, k, p, seeds, pos
+
+
+@pytest.mark.parametrize("V", [32768, 4096, 1000])
+def test_sampler_matches_reference(gpu, V):
+    g = torch.Generator().manual_seed(V)
+    temps = [0.0, 1.0, 0.7, 1.3, 1.0, 0.5, 1.0, 2.0]
+    topk = [0, 0, 0, 50, 1, 0, 20, 0]
+    topp = [1.0, 1.0, 1.0, 1.0, 1.0, 0.9, 0.5, 0.95]
+    B = len(temps)
+    logits, t, k, p, seeds, pos = _sampler_inputs(B, V, g, temps, topk, topp)
+    ids_g = torch.zeros(B, dtype=torch.int32, device=gpu)
+    ring = torch.zeros(4, B, dtype=torch.int32, device=gpu)
+    ctr = torch.tensor([2], dtype=torch.int32, device=gpu)
+    pos_g = pos.clone().to(gpu)
+    ops.sample(logits.to(gpu), t.to(gpu), k.to(gpu), p.to(gpu), seeds.to(gpu), pos.to(gpu), None, ids_g, ring, ctr,
+               pos_g)
+    ids_r = torch.zeros(B, dtype=torch.int32)
+    R.sample(logits, t, k, p, seeds, pos, None, ids_r)
+    assert torch.equal(ids_g.cpu(), ids_r), (ids_g.cpu(), ids_r)
+    assert torch.equal(ring[2].cpu(), ids_r)
+    assert torch.equal(pos_g.cpu(), pos + 1)
+
+
+def test_sampler_distribution(gpu):
+    """Gumbel-max draws follow softmax(logits / T) (chi-square style check on a small vocab)."""
+    V, N = 16, 4096
+    logits = torch.linspace(-2, 2, V)
+    lg = logits.repeat(N, 1).to(gpu)
+    t = torch.full((N,), 0.8, device=gpu)
+    k = torch.zeros(N, dtype=torch.int32, device=gpu)
+    p = torch.ones(N, device=gpu)
+    seeds = torch.stack([torch.arange(N, dtype=torch.int32), torch.full((N,), 7, dtype=torch.int32)], 1).to(gpu)
+    pos = torch.zeros(N, dtype=torch.int32, device=gpu)
+    ids = torch.zeros(N, dtype=torch.int32, device=gpu)
+    ops.sample(lg, t, k, p, seeds, pos, None, ids)
+    counts = torch.bincount(ids.cpu().long(), minlength=V).float()
+    expect = torch.softmax(logits / 0.8, 0) * N
+    assert ((counts - expect).abs() <= 5 * expect.sqrt() + 5).all(), (counts, expect)
+
+
+def test_sampler_tp_candidates(gpu):
+    """Per-shard candidates merged by sample_pick equal the unsharded draw (TP invariance)."""
+    g = torch.Generator().manual_seed(11)
+    B, V, world = 6, 32768, 4
+    logits, t, k, p, seeds, pos = _sampler_inputs(B, V, g, [0.0, 1.0, 0.6, 1.0, 1.2, 0.9], [0] * 6, [1.0] * 6)
+    args = [x.to(gpu) for x in (t, k, p, seeds, pos)]
+    full = torch.zeros(B, dtype=torch.int32, device=gpu)
+    ops.sample(logits.to(gpu), *args, None, full)
+    cands = []
+    for r in range(world):
+        c = torch.zeros(B, 2, device=gpu)
+        sh = logits[:, r * V // world:(r + 1) * V // world].contiguous().to(gpu)
+        ops.sample(sh, *args, None, torch.zeros(B, dtype=torch.int32, device=gpu), None, None, None, c, r * V // world)
+        cands.append(c)
+    picked = torch.zeros(B, dtype=torch.int32, device=gpu)
+    ops.sample_pick(torch.stack(cands).contiguous().view(-1), world, *args, None, picked)
+    assert torch.equal(picked.cpu(), full.cpu())
+
+
+def test_decode_prep_and_ring(gpu):
+    B = 5
+    active = torch.tensor([1, 0, 1, 1, 0], dtype=torch.int32)
+    positions = torch.tensor([0, 5, 31, 32, 9], dtype=torch.int32)
+    bt = torch.arange(B * 4, dtype=torch.int32).view(B, 4)
+    outs = [torch.zeros(B, dtype=torch.int32) for _ in range(3)]
+    outs_g = [o.clone().to(gpu) for o in outs]
+    ops.decode_prep(active.to(gpu), positions.to(gpu), bt.to(gpu), *outs_g)
+    R.decode_prep(active, positions, bt, *outs)
+    for a, b in zip(outs_g, outs):
+        assert torch.equal(a.cpu(), b)
+    c = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.ring_advance(c)
+    ops.ring_advance(c)
+    assert int(c) == 2
+
+
+def test_gpu_path_has_no_fallback(gpu):
+    """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
+    assert ops.load_library(required=True)
+    assert os.path.exists(ops.library_path())
+    assert torch.ops.dsse.kernels_abi_version() == 1

@@ -1,0 +1,64 @@
+"""The engine's forward (paged KV, fused epilogues, prefill + decode) against the fp32 reference model."""
+import pytest
+import torch
+
+from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
+from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights, reference_forward
+
+
+def _run(device, use_graphs, steps=6, chunked=False):
+    cfg = TINY
+    std = init_standard_weights(cfg, seed=1)
+    w = convert_standard(cfg, std, device=device)
+    r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device=device, use_graphs=use_graphs)
+    prompts = [[5, 17, 99, 3, 8, 1000, 42], list(range(100, 170)), [7] * 33]
+    bts = [[0, 1, 2], [10, 4, 5, 6], [20, 21, 22]]
+    for i, bt in enumerate(bts):
+        r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    if chunked:
+        # prompt 1 in two chunks across two prefill calls, the other two in the first call
+        r.prefill([PrefillSeq(0, prompts[0], 0, bts[0], True), PrefillSeq(1, prompts[1][:40], 0, bts[1], False),
+                   PrefillSeq(2, prompts[2], 0, bts[2], True)], ring_row=0)
+        r.prefill([PrefillSeq(1, prompts[1][40:], 40, bts[1], True)], ring_row=0)
+    else:
+        r.prefill([PrefillSeq(i, p, 0, bts[i], True) for i, p in enumerate(prompts)], ring_row=0)
+    r.active[:3] = 1
+    if use_graphs:
+        r.capture([4])
+    gen = [[int(r.ids[i])] for i in range(3)]
+    for step in range(steps):
+        r.decode(4)
+        ids = r.ids.cpu()
+        for i in range(3):
+            gen[i].append(int(ids[i]))
+    ring = r.ring.cpu()
+    for step in range(steps):
+        assert [int(ring[step, i]) for i in range(3)] == [gen[i][step + 1] for i in range(3)]
+    worst = 0.0
+    for i in range(3):
+        logits, _ = reference_forward(cfg, std, torch.tensor(prompts[i] + gen[i]))
+        L = len(prompts[i])
+        for j, g in enumerate(gen[i]):
+            row = logits[L - 1 + j]
+            worst = max(worst, float(row.max() - row[g]))
+    return worst
+
+
+def test_engine_matches_reference_cpu():
+    assert _run("cpu", False) < 0.05
+
+
+def test_engine_chunked_prefill_cpu():
+    assert _run("cpu", False, steps=3, chunked=True) < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_engine_matches_reference_gpu(gpu, graphs):
+    assert _run(gpu, graphs) < 0.1
+
+
+@pytest.mark.gpu
+def test_engine_chunked_prefill_gpu(gpu):
+    assert _run(gpu, False, steps=3, chunked=True) < 0.1
