@@ -53,13 +53,13 @@ struct SampleParams {
   const uint2* seeds;        // [B]
   const int* positions;      // [B] position of the sampled token's predecessor (RNG counter)
   const int* active;         // [B] or null (all active)
-  int* next_ids;             // [B] written when !candidates_only
+  int* next_ids;             // [B] (pick pass)
   int* ring;                 // [ring_size, ring_stride] or null
   const int* ring_counter;
   int ring_size, ring_stride;
   int* positions_inc;        // [B] or null: positions[b] += 1 for active rows
-  float2* cand;              // [B] (score, index-as-bits) when candidates_only
-  int candidates_only;
+  float2* cand;              // [B, nchunks] (score, index-as-bits) candidates
+  int nchunks;               // vocab chunks per row (unfiltered path)
 };
 
 }  // namespace dsse
@@ -67,6 +67,8 @@ struct SampleParams {
 extern "C" {
 hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int ldx, int M,
                             const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
+hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx, int M,
+                          const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);
 hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::SampleParams* p,

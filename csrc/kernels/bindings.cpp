@@ -7,6 +7,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -52,6 +53,46 @@ void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
   (void)mode;
 }
 
+// X-in-LDS kernel configuration (gemm_xlds.hip).  Env overrides: DSSE_X_KS, DSSE_X_NW, DSSE_X_NT, DSSE_X_TG,
+// DSSE_X_DEPTH.
+struct XCfg {
+  int mt, nt, nw, depth, ks, tg, S;
+};
+// Defaults from the gfx950 sweep (tools/tune_gemm.py --grid, profiles/gemm_sweep_r1.md): 8 waves, 4-deep
+// weight ring, K-slices of 1024 (512 for the small O projection, 2048 for wide layers at M <= 32), and
+// ~224 workgroups so that the one-workgroup-per-CU grid stays balanced.
+XCfg pick_xlds(int M, int N, int K) {
+  XCfg c{};
+  c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  c.nt = env_int("DSSE_X_NT", 1);
+  c.nw = env_int("DSSE_X_NW", 8);
+  c.depth = env_int("DSSE_X_DEPTH", 4);
+  int ks = env_int("DSSE_X_KS", 0);
+  if (ks <= 0) {
+    ks = 1024;
+    if (N <= 4096 && K <= 4096) ks = 512;
+    if (N >= 16384 && M <= 32) ks = 2048;
+  }
+  ks = std::min(ks, (65536 / (16 * c.mt)) / 128 * 128);  // <= 128 KiB of LDS
+  ks = std::max(128, std::min(ks, K)) / 128 * 128;
+  c.ks = ks;
+  c.S = (K + ks - 1) / ks;
+  const int TG = N / (16 * c.nt);
+  int tg = env_int("DSSE_X_TG", 0);
+  if (tg <= 0) tg = std::max(c.nw, (TG * c.S / 224 / c.nw) * c.nw);
+  c.tg = std::min(tg, TG);
+  return c;
+}
+
+// Register-streaming kernel for tiny batches (X re-reads are cheap), X-in-LDS kernel above.
+bool use_xlds(int M, int N, int K) {
+  const int impl = env_int("DSSE_GEMM_IMPL", -1);
+  if (impl >= 0) return impl == 1;
+  if (M <= 8) return false;
+  if (M <= 16) return N >= 16384;
+  return true;
+}
+
 void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   check_gpu(x, "x");
   check_gpu(w, "w");
@@ -60,9 +101,18 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x and w must be 2-D");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch: x ", K, " vs w ", w.size(1));
-  TORCH_CHECK(M >= 1 && M <= 64, "skinny GEMM supports 1 <= M <= 64, got ", M);
+  TORCH_CHECK(M >= 1 && M <= 64, "decode GEMM supports 1 <= M <= 64, got ", M);
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
+  if (use_xlds(M, N, K)) {
+    XCfg c = pick_xlds(M, N, K);
+    if (N % (16 * c.nt) != 0) c.nt = 1;
+    at::Tensor part;
+    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
+    DSSE_CHECK_HIP(dsse_gemm_xlds(mode, c.mt, c.nt, c.nw, c.depth, c.ks, c.tg, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                  c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    return;
+  }
   int mt, nt, kw;
   pick_tiles(M, N, K, mode, mt, nt, kw);
   DSSE_CHECK_HIP(dsse_skinny_gemm(mode, mt, nt, kw, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
@@ -270,76 +320,85 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
 
 dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
                                  const Tensor& seeds, const Tensor& positions,
-                                 const c10::optional<Tensor>& active, Tensor& next_ids,
-                                 const c10::optional<Tensor>& ring,
-                                 const c10::optional<Tensor>& ring_counter,
-                                 const c10::optional<Tensor>& positions_inc) {
+                                 const c10::optional<Tensor>& active, int B) {
+  for (const Tensor* t : {&temperature, &top_k, &top_p, &seeds, &positions}) check_gpu(*t, "sampling metadata");
   check_dtype(temperature, at::kFloat, "temperature");
   check_dtype(top_k, at::kInt, "top_k");
   check_dtype(top_p, at::kFloat, "top_p");
   check_dtype(seeds, at::kInt, "seeds");
   check_dtype(positions, at::kInt, "positions");
-  check_dtype(next_ids, at::kInt, "next_ids");
+  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B && seeds.numel() >= 2 * B &&
+                  positions.numel() >= B, "sampling metadata too short");
   dsse::SampleParams p{};
   p.temperature = temperature.data_ptr<float>();
   p.top_k = top_k.data_ptr<int>();
   p.top_p = top_p.data_ptr<float>();
   p.seeds = reinterpret_cast<const uint2*>(seeds.data_ptr<int>());
   p.positions = positions.data_ptr<int>();
-  p.active = active.has_value() ? active->data_ptr<int>() : nullptr;
+  if (active.has_value()) {
+    check_gpu(*active, "active");
+    check_dtype(*active, at::kInt, "active");
+    TORCH_CHECK(active->numel() >= B, "active too short");
+    p.active = active->data_ptr<int>();
+  }
+  return p;
+}
+
+// Per-rank candidate pass: cand [B, nchunks, 2] fp32 (score, index bits).
+void sample_candidates(const Tensor& logits, const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
+                       const Tensor& seeds, const Tensor& positions, const c10::optional<Tensor>& active,
+                       Tensor& cand, int64_t vocab_offset) {
+  check_gpu(logits, "logits");
+  check_dtype(logits, at::kFloat, "logits");
+  check_gpu(cand, "cand");
+  check_dtype(cand, at::kFloat, "cand");
+  const int B = (int)logits.size(0), V = (int)logits.size(1);
+  TORCH_CHECK(V <= 32768, "sampler supports V <= 32768 per rank");
+  TORCH_CHECK(cand.dim() == 3 && cand.size(0) == B && cand.size(2) == 2, "cand must be [B, nchunks, 2]");
+  dsse::SampleParams p = sample_params(temperature, top_k, top_p, seeds, positions, active, B);
+  p.logits = logits.data_ptr<float>();
+  p.ld = V;
+  p.V = V;
+  p.vocab_offset = (int)vocab_offset;
+  p.cand = reinterpret_cast<float2*>(cand.data_ptr<float>());
+  p.nchunks = (int)cand.size(1);
+  DSSE_CHECK_HIP(dsse_sample(B, &p, cur_stream()));
+}
+
+// Merge pass over cand_all [world, B, nchunks, 2] and commit: next_ids, ring[head], positions += 1.
+void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Tensor& next_ids,
+                 const c10::optional<Tensor>& ring, const c10::optional<Tensor>& ring_counter,
+                 const c10::optional<Tensor>& positions_inc) {
+  check_gpu(cand_all, "cand_all");
+  check_gpu(next_ids, "next_ids");
+  check_dtype(next_ids, at::kInt, "next_ids");
+  TORCH_CHECK(cand_all.dim() == 4 && cand_all.size(3) == 2, "cand_all must be [world, B, nchunks, 2]");
+  const int world = (int)cand_all.size(0), B = (int)cand_all.size(1);
+  TORCH_CHECK(next_ids.numel() >= B, "next_ids too short");
+  dsse::SampleParams p{};
+  p.nchunks = (int)cand_all.size(2);
   p.next_ids = next_ids.data_ptr<int>();
+  if (active.has_value()) {
+    TORCH_CHECK(active->numel() >= B, "active too short");
+    p.active = active->data_ptr<int>();
+  }
   if (ring.has_value()) {
     TORCH_CHECK(ring_counter.has_value(), "ring needs ring_counter");
+    check_gpu(*ring, "ring");
+    TORCH_CHECK(ring->dim() == 2 && ring->size(1) >= B, "ring must be [R, >= B]");
     p.ring = ring->data_ptr<int>();
     p.ring_counter = ring_counter->data_ptr<int>();
     p.ring_size = (int)ring->size(0);
     p.ring_stride = (int)ring->size(1);
   }
-  p.positions_inc = positions_inc.has_value() ? positions_inc->data_ptr<int>() : nullptr;
-  return p;
-}
-
-void sample(const Tensor& logits, const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
-            const Tensor& seeds, const Tensor& positions, const c10::optional<Tensor>& active,
-            Tensor& next_ids, const c10::optional<Tensor>& ring,
-            const c10::optional<Tensor>& ring_counter, const c10::optional<Tensor>& positions_inc,
-            const c10::optional<Tensor>& cand, int64_t vocab_offset) {
-  check_gpu(logits, "logits");
-  check_dtype(logits, at::kFloat, "logits");
-  const int B = (int)logits.size(0), V = (int)logits.size(1);
-  TORCH_CHECK(V <= 32768, "sampler supports V <= 32768 per rank");
-  TORCH_CHECK(temperature.numel() >= B && top_k.numel() >= B && top_p.numel() >= B &&
-                  seeds.numel() >= 2 * B && positions.numel() >= B && next_ids.numel() >= B,
-              "sampling metadata too short");
-  if (ring.has_value()) TORCH_CHECK(ring->size(1) >= B, "ring too narrow");
-  dsse::SampleParams p = sample_params(temperature, top_k, top_p, seeds, positions, active, next_ids,
-                                       ring, ring_counter, positions_inc);
-  p.logits = logits.data_ptr<float>();
-  p.ld = V;
-  p.V = V;
-  p.vocab_offset = (int)vocab_offset;
-  if (cand.has_value()) {
-    TORCH_CHECK(cand->numel() >= 2 * B, "cand too small");
-    p.cand = reinterpret_cast<float2*>(cand->data_ptr<float>());
-    p.candidates_only = 1;
+  if (positions_inc.has_value()) {
+    TORCH_CHECK(positions_inc->numel() >= B, "positions_inc too short");
+    p.positions_inc = positions_inc->data_ptr<int>();
   }
-  DSSE_CHECK_HIP(dsse_sample(B, &p, cur_stream()));
+  DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-void sample_pick(const Tensor& cand_all, int64_t world, const Tensor& temperature, const Tensor& top_k,
-                 const Tensor& top_p, const Tensor& seeds, const Tensor& positions,
-                 const c10::optional<Tensor>& active, Tensor& next_ids, const c10::optional<Tensor>& ring,
-                 const c10::optional<Tensor>& ring_counter,
-                 const c10::optional<Tensor>& positions_inc) {
-  check_gpu(cand_all, "cand_all");
-  const int B = (int)(cand_all.numel() / (2 * world));
-  TORCH_CHECK(next_ids.numel() >= B, "next_ids too short");
-  dsse::SampleParams p = sample_params(temperature, top_k, top_p, seeds, positions, active, next_ids,
-                                       ring, ring_counter, positions_inc);
-  DSSE_CHECK_HIP(dsse_sample_pick(B, (int)world, cand_all.data_ptr(), &p, cur_stream()));
-}
-
-int64_t kernels_abi_version() { return 1; }
+int64_t kernels_abi_version() { return 2; }
 
 }  // namespace
 
@@ -360,12 +419,10 @@ TORCH_LIBRARY(dsse, m) {
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
         "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
-  m.def("sample(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, Tensor positions, "
-        "Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, Tensor? ring_counter=None, "
-        "Tensor(c!)? positions_inc=None, Tensor(d!)? cand=None, int vocab_offset=0) -> ()");
-  m.def("sample_pick(Tensor cand_all, int world, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
-        "Tensor positions, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, Tensor? ring_counter=None, "
-        "Tensor(c!)? positions_inc=None) -> ()");
+  m.def("sample_candidates(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
+        "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
+  m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
+        "Tensor? ring_counter=None, Tensor(c!)? positions_inc=None) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
 }
 
@@ -380,6 +437,6 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("decode_prep", &decode_prep);
   m.impl("ring_advance", &ring_advance);
   m.impl("paged_attention", &paged_attention);
-  m.impl("sample", &sample);
+  m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
 }

@@ -18,58 +18,76 @@ DEV uint32_t fkey(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-constexpr int kSThreads = 1024;
-constexpr int kSMaxPer = 32;  // V <= 32768
+constexpr int kSThreads = 1024;   // filtered path: one workgroup per row
+constexpr int kSMaxV = 32768;     // per-rank vocab limit (row staged in 128 KiB of LDS)
+constexpr int kCThreads = 256;    // unfiltered path: one workgroup per (row, vocab chunk)
 
-template <typename T>
-DEV T block_reduce_sum(T v, T* sh) {
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  T tot = 0;
-#pragma unroll
-  for (int i = 0; i < kSThreads / 64; ++i) tot += sh[i];
-  __syncthreads();
-  return tot;
+DEV bool row_filtered(const SampleParams& p, int b) {
+  return p.temperature[b] > 0.f && ((p.top_k[b] > 0 && p.top_k[b] < p.V) || p.top_p[b] < 1.f);
 }
 
-DEV float block_reduce_max(float v, float* sh) {
-  v = wave_max(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float tot = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < kSThreads / 64; ++i) tot = fmaxf(tot, sh[i]);
-  __syncthreads();
-  return tot;
+// Score of one logit: greedy -> the logit itself; sampling -> logit/T + Gumbel(seed, pos, gidx).
+DEV float score(float logit, float inv_t, bool greedy, uint2 seed, uint32_t pos, int gidx) {
+  if (greedy) return logit;
+  const uint4 rv = philox4x32(make_uint4((uint32_t)gidx, pos, 0x5353u, 0u), seed);
+  return logit * inv_t - __logf(-__logf(u01(rv.x)));
 }
 
-// MSB-first radix select.  Returns the key `thr` such that the elements with key >= thr are the
-// smallest top set whose weight (count or mass) reaches `target`.  Elements with key < floor_key
-// are ignored.
+DEV void better(float& best, int& bidx, float s, int i) {
+  if (s > best || (s == best && i < bidx)) { best = s; bidx = i; }
+}
+
+template <int NT>
+DEV void block_argmax(float& best, int& bidx, float* s_best, int* s_bidx) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) better(best, bidx, __shfl_xor(best, o), __shfl_xor(bidx, o));
+  if ((threadIdx.x & 63) == 0) { s_best[threadIdx.x >> 6] = best; s_bidx[threadIdx.x >> 6] = bidx; }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int i = 1; i < NT / 64; ++i) better(best, bidx, s_best[i], s_bidx[i]);
+}
+
+// Unfiltered rows (greedy or pure temperature): Gumbel-max is separable, so each (row, chunk)
+// workgroup proposes the best (score, index) of its vocab slice.
+__global__ void __launch_bounds__(kCThreads) sample_chunk_kernel(SampleParams p) {
+  const int c = blockIdx.x, b = blockIdx.y;
+  if ((p.active && !p.active[b]) || row_filtered(p, b)) return;
+  __shared__ float s_best[kCThreads / 64];
+  __shared__ int s_bidx[kCThreads / 64];
+  const float temp = p.temperature[b];
+  const bool greedy = !(temp > 0.f);
+  const float inv_t = greedy ? 1.f : 1.f / temp;
+  const uint2 seed = p.seeds[b];
+  const uint32_t pos = (uint32_t)p.positions[b];
+  const int chunk = (p.V + p.nchunks - 1) / p.nchunks;
+  const int lo = c * chunk, hi = min(p.V, lo + chunk);
+  const float* row = p.logits + (size_t)b * p.ld;
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int i = lo + threadIdx.x; i < hi; i += kCThreads)
+    better(best, bidx, score(row[i], inv_t, greedy, seed, pos, i + p.vocab_offset), i + p.vocab_offset);
+  block_argmax<kCThreads>(best, bidx, s_best, s_bidx);
+  if (threadIdx.x == 0) p.cand[(size_t)b * p.nchunks + c] = make_float2(best, __int_as_float(bidx));
+}
+
+// MSB-first radix select over LDS-resident base-2 logits.  Returns the key `thr` such that the
+// elements with key >= thr form the smallest top set whose weight (count or softmax mass) reaches
+// `target`; elements with key < floor_key are ignored.
 template <bool MASS>
-DEV uint32_t radix_select(const float (&x)[kSMaxPer], const uint32_t (&key)[kSMaxPer], int nper,
-                          int V, float xmax, uint32_t floor_key, float target, float* hist) {
+DEV uint32_t radix_select(const float* xs, int V, float xmax, uint32_t floor_key, float target, float* hist) {
   uint32_t prefix = 0, mask = 0;
   float remaining = target;
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += kSThreads) hist[i] = 0.f;
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kSMaxPer; ++j) {
-      if (j < nper) {
-        const int idx = j * kSThreads + threadIdx.x;
-        if (idx < V && key[j] >= floor_key && (key[j] & mask) == prefix) {
-          const float wgt = MASS ? exp2f(x[j] - xmax) : 1.f;
-          atomicAdd(&hist[(key[j] >> shift) & 255], wgt);
-        }
-      }
+    for (int i = threadIdx.x; i < V; i += kSThreads) {
+      const uint32_t k = fkey(xs[i]);
+      if (k >= floor_key && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], MASS ? exp2f(xs[i] - xmax) : 1.f);
     }
     __syncthreads();
-    // every thread scans the 256 bins (cheap, avoids another barrier round)
     float cum = 0.f;
     int digit = 0;
-    for (int d = 255; d >= 0; --d) {
+    for (int d = 255; d >= 0; --d) {  // every thread scans the 256 bins (no extra barrier round)
       const float hv = hist[d];
       if (cum + hv >= remaining) { digit = d; break; }
       cum += hv;
@@ -82,104 +100,85 @@ DEV uint32_t radix_select(const float (&x)[kSMaxPer], const uint32_t (&key)[kSMa
   return prefix;
 }
 
-__global__ void __launch_bounds__(kSThreads) sample_kernel(SampleParams p) {
-  const int b = blockIdx.x;
-  if (p.active && !p.active[b]) return;
-  __shared__ float sh[kSThreads / 64];
-  __shared__ float hist[256];
-  __shared__ float s_best[kSThreads / 64];
-  __shared__ int s_bidx[kSThreads / 64];
-
-  const float* row = p.logits + (size_t)b * p.ld;
-  const float temp = p.temperature[b];
-  const bool greedy = !(temp > 0.f);
-  const float inv_t = greedy ? 1.f : 1.f / temp;
-  const int nper = (p.V + kSThreads - 1) / kSThreads;
-
-  float x[kSMaxPer];
-  uint32_t key[kSMaxPer];
-  float lmax = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < kSMaxPer; ++j) {
-    const int idx = j * kSThreads + threadIdx.x;
-    if (j < nper && idx < p.V) {
-      x[j] = row[idx] * inv_t * 1.4426950408889634f;  // base-2 scaled logits
-      key[j] = fkey(x[j]);
-      lmax = fmaxf(lmax, x[j]);
-    } else {
-      x[j] = -INFINITY;
-      key[j] = 0;
-    }
-  }
-
-  uint32_t thr = 0;
-  if (!greedy) {
-    const int tk = p.top_k[b];
-    const float tp = p.top_p[b];
-    const float xmax = block_reduce_max(lmax, sh);
-    if (tk > 0 && tk < p.V) thr = radix_select<false>(x, key, nper, p.V, xmax, 0u, (float)tk, hist);
-    if (tp < 1.f) {
-      float z = 0.f;
-#pragma unroll
-      for (int j = 0; j < kSMaxPer; ++j)
-        if (j < nper && key[j] >= thr && x[j] > -INFINITY) z += exp2f(x[j] - xmax);
-      z = block_reduce_sum(z, sh);
-      thr = radix_select<true>(x, key, nper, p.V, xmax, thr, tp * z, hist);
-    }
-  }
-
-  // Gumbel-max (or plain argmax) over kept elements; ties -> smallest index.
-  float best = -INFINITY;
-  int bidx = 0x7fffffff;
-  const uint2 seed = p.seeds ? p.seeds[b] : make_uint2(0, 0);
-  const uint32_t pos = p.positions ? (uint32_t)p.positions[b] : 0u;
-#pragma unroll
-  for (int j = 0; j < kSMaxPer; ++j) {
-    const int idx = j * kSThreads + threadIdx.x;
-    if (j < nper && idx < p.V && key[j] >= thr) {
-      float sc = x[j];
-      const int gidx = idx + p.vocab_offset;
-      if (!greedy) {
-        const uint4 rv = philox4x32(make_uint4((uint32_t)gidx, pos, 0x5353u, 0u), seed);
-        const float u = u01(rv.x);
-        sc = x[j] * 0.6931471805599453f - __logf(-__logf(u));  // back to natural units + Gumbel
-      }
-      if (sc > best || (sc == best && gidx < bidx)) { best = sc; bidx = gidx; }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const float ob = __shfl_xor(best, o);
-    const int oi = __shfl_xor(bidx, o);
-    if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-  }
-  if ((threadIdx.x & 63) == 0) { s_best[threadIdx.x >> 6] = best; s_bidx[threadIdx.x >> 6] = bidx; }
+template <typename T>
+DEV T block_sum(T v, T* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int i = 1; i < kSThreads / 64; ++i) {
-    if (s_best[i] > best || (s_best[i] == best && s_bidx[i] < bidx)) { best = s_best[i]; bidx = s_bidx[i]; }
-  }
-  if (p.candidates_only) {
-    p.cand[b] = make_float2(best, __int_as_float(bidx));
-    return;
-  }
-  p.next_ids[b] = bidx;
-  if (p.ring) p.ring[(size_t)(p.ring_counter[0] % p.ring_size) * p.ring_stride + b] = bidx;
-  if (p.positions_inc) p.positions_inc[b] += 1;
+  T tot = 0;
+  for (int i = 0; i < kSThreads / 64; ++i) tot += sh[i];
+  __syncthreads();
+  return tot;
+}
+DEV float block_max(float v, float* sh) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float tot = -INFINITY;
+  for (int i = 0; i < kSThreads / 64; ++i) tot = fmaxf(tot, sh[i]);
+  __syncthreads();
+  return tot;
 }
 
-// Merge per-rank candidates [world, B] (tensor-parallel vocab shards) and commit the token.
+// Rows with top-k / top-p: one workgroup per row, the whole (local) row staged in LDS.
+__global__ void __launch_bounds__(kSThreads) sample_filtered_kernel(SampleParams p) {
+  const int b = blockIdx.x;
+  if ((p.active && !p.active[b]) || !row_filtered(p, b)) return;
+  __shared__ float xs[kSMaxV];
+  __shared__ float hist[256];
+  __shared__ float sh[kSThreads / 64];
+  __shared__ int shi[kSThreads / 64];
+  const float inv_t = 1.f / p.temperature[b];
+  const float* row = p.logits + (size_t)b * p.ld;
+  float lmax = -INFINITY;
+  for (int i = threadIdx.x; i < p.V; i += kSThreads) {
+    const float x = row[i] * inv_t * 1.4426950408889634f;  // base-2 scaled
+    xs[i] = x;
+    lmax = fmaxf(lmax, x);
+  }
+  const float xmax = block_max(lmax, sh);
+  uint32_t thr = 0;
+  const int tk = p.top_k[b];
+  const float tp = p.top_p[b];
+  if (tk > 0 && tk < p.V) thr = radix_select<false>(xs, p.V, xmax, 0u, (float)tk, hist);
+  if (tp < 1.f) {
+    float z = 0.f;
+    for (int i = threadIdx.x; i < p.V; i += kSThreads)
+      if (fkey(xs[i]) >= thr) z += exp2f(xs[i] - xmax);
+    z = block_sum(z, sh);
+    thr = radix_select<true>(xs, p.V, xmax, thr, tp * z, hist);
+  }
+  const uint2 seed = p.seeds[b];
+  const uint32_t pos = (uint32_t)p.positions[b];
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for (int i = threadIdx.x; i < p.V; i += kSThreads) {
+    if (fkey(xs[i]) < thr) continue;
+    const int gidx = i + p.vocab_offset;
+    const uint4 rv = philox4x32(make_uint4((uint32_t)gidx, pos, 0x5353u, 0u), seed);
+    better(best, bidx, xs[i] * 0.6931471805599453f - __logf(-__logf(u01(rv.x))), gidx);
+  }
+  block_argmax<kSThreads>(best, bidx, sh, shi);
+  if (threadIdx.x == 0) {
+    p.cand[(size_t)b * p.nchunks] = make_float2(best, __int_as_float(bidx));
+    for (int c = 1; c < p.nchunks; ++c)
+      p.cand[(size_t)b * p.nchunks + c] = make_float2(-INFINITY, __int_as_float(0x7fffffff));
+  }
+}
+
+// Merge candidates [world, B, nchunks] (vocab chunks x tensor-parallel shards) and commit the token:
+// next_ids[b], ring[head][b], positions[b] += 1.
 __global__ void sample_pick_kernel(const float2* __restrict__ cand, int world, int B, SampleParams p) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   if (p.active && !p.active[b]) return;
   float best = -INFINITY;
   int bidx = 0x7fffffff;
-  for (int w = 0; w < world; ++w) {
-    const float2 c = cand[(size_t)w * B + b];
-    const int ci = __float_as_int(c.y);
-    if (c.x > best || (c.x == best && ci < bidx)) { best = c.x; bidx = ci; }
-  }
+  for (int w = 0; w < world; ++w)
+    for (int c = 0; c < p.nchunks; ++c) {
+      const float2 v = cand[((size_t)w * B + b) * p.nchunks + c];
+      better(best, bidx, v.x, __float_as_int(v.y));
+    }
   p.next_ids[b] = bidx;
   if (p.ring) p.ring[(size_t)(p.ring_counter[0] % p.ring_size) * p.ring_stride + b] = bidx;
   if (p.positions_inc) p.positions_inc[b] += 1;
@@ -187,15 +186,18 @@ __global__ void sample_pick_kernel(const float2* __restrict__ cand, int world, i
 
 }  // namespace dsse
 
+// Per-rank candidate pass: fills p->cand[B, nchunks].
 extern "C" hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  if (p->V > dsse::kSThreads * dsse::kSMaxPer) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dsse::sample_kernel, dim3(B), dim3(dsse::kSThreads), 0, st, *p);
+  if (p->V > dsse::kSMaxV || p->nchunks < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dsse::sample_chunk_kernel, dim3(p->nchunks, B), dim3(dsse::kCThreads), 0, st, *p);
+  hipLaunchKernelGGL(dsse::sample_filtered_kernel, dim3(B), dim3(dsse::kSThreads), 0, st, *p);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dsse_sample_pick(int B, int world, const void* cand,
-                                       const dsse::SampleParams* p, hipStream_t st) {
+// Merge pass over cand [world, B, nchunks].
+extern "C" hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::SampleParams* p,
+                                       hipStream_t st) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(dsse::sample_pick_kernel, dim3((B + 63) / 64), dim3(64), 0, st,
                      reinterpret_cast<const float2*>(cand), world, B, *p);

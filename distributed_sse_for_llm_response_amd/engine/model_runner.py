@@ -34,6 +34,7 @@ from .kv_cache import PAGE, KVCache
 from .weights import EngineWeights
 
 RING_SIZE = 64
+SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
 
 
 def batch_buckets(max_batch: int):
@@ -106,8 +107,10 @@ class ModelRunner:
         self.h = torch.zeros(Bm, F, **bf)
         self.tmp = torch.zeros(Bm, H, **bf)
         self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
-        self.cand = torch.zeros(Bm, 2, device=dev, dtype=torch.float32)
-        self._cand_bufs = {}
+        nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
+        self._cand = {b: torch.zeros(b, nch, 2, device=dev, dtype=torch.float32) for b in batch_buckets(Bm)}
+        self._cand_all = {b: torch.zeros(self.comm.size, b, nch, 2, device=dev, dtype=torch.float32)
+                          for b in batch_buckets(Bm)}
         part, nparts = decode_partitioning(1, nkv, max_model_len)
         ws = max(decode_partitioning(b, nkv, max_model_len)[1] * b for b in batch_buckets(Bm))
         self.part_o = torch.zeros(max(1, ws) * nkv * 16 * 128, device=dev, dtype=torch.float32)
@@ -157,20 +160,17 @@ class ModelRunner:
         ops.ring_advance(self.ring_counter)
 
     def _sample_commit(self, B: int) -> None:
+        """Candidates per (row, vocab chunk) on each rank -> (TP: all-gather, 8 B per candidate) -> pick."""
         r = slice(0, B)
-        args = (self.temperature[r], self.top_k[r], self.top_p[r], self.seeds[r], self.positions[r], self.active[r])
+        cand = self._cand[B]
+        ops.sample_candidates(self.logits[r], self.temperature[r], self.top_k[r], self.top_p[r], self.seeds[r],
+                              self.positions[r], self.active[r], cand, self.w.vocab_offset)
         if self.comm.size == 1:
-            ops.sample(self.logits[r], *args, self.ids[r], self.ring, self.ring_counter, self.positions[r], None, 0)
+            cand_all = cand.unsqueeze(0)
         else:
-            # vocab-parallel: each rank proposes its Gumbel-max candidate, 8 bytes per sequence cross the link
-            ops.sample(self.logits[r], *args, self.ids[r], None, None, None, self.cand[r], self.w.vocab_offset)
-            flat = self._cand_bufs.get(B)
-            if flat is None:
-                flat = self._cand_bufs[B] = torch.zeros(self.comm.size * B * 2, device=self.device,
-                                                        dtype=torch.float32)
-            self.comm.all_gather_into(flat, self.cand[r].contiguous().view(-1))
-            ops.sample_pick(flat, self.comm.size, *args, self.ids[r], self.ring, self.ring_counter,
-                            self.positions[r])
+            cand_all = self._cand_all[B]
+            self.comm.all_gather_into(cand_all, cand)
+        ops.sample_pick(cand_all, self.active[r], self.ids[r], self.ring, self.ring_counter, self.positions[r])
 
     def bucket_for(self, n_active_max_slot: int) -> int:
         for b in batch_buckets(self.max_batch):
@@ -305,14 +305,15 @@ class ModelRunner:
         tk = self.top_k.index_select(0, slot_idx)
         tp = self.top_p.index_select(0, slot_idx)
         sd = self.seeds.index_select(0, slot_idx).contiguous()
+        nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
+        cand = torch.zeros(nL, nch, 2, **f32)
+        ops.sample_candidates(logits, temp, tk, tp, sd, last_pos, None, cand, w.vocab_offset)
         if comm.size == 1:
-            ops.sample(logits, temp, tk, tp, sd, last_pos, None, new_ids)
+            cand_all = cand.unsqueeze(0)
         else:
-            cand = torch.zeros(nL, 2, **f32)
-            ops.sample(logits, temp, tk, tp, sd, last_pos, None, new_ids, None, None, None, cand, w.vocab_offset)
-            cand_all = torch.zeros(comm.size * nL * 2, **f32)
-            comm.all_gather_into(cand_all, cand.view(-1))
-            ops.sample_pick(cand_all, comm.size, temp, tk, tp, sd, last_pos, None, new_ids)
+            cand_all = torch.zeros(comm.size, nL, nch, 2, **f32)
+            comm.all_gather_into(cand_all, cand)
+        ops.sample_pick(cand_all, None, new_ids)
         self.ids.index_copy_(0, slot_idx, new_ids)
         self.ring[ring_row].index_copy_(0, slot_idx, new_ids)
         self.positions.index_copy_(0, slot_idx, last_pos + 1)

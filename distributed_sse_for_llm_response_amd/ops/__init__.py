@@ -137,21 +137,27 @@ def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx
                             out, part_o, part_ml, part, nparts)
 
 
-def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
-           positions_inc=None, cand=None, vocab_offset=0):
+def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):
+    """Per-rank pass: cand [B, C, 2] <- best (score, index) of each vocab chunk (Gumbel-max / argmax)."""
     if _hip(logits):
-        torch.ops.dsse.sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring,
-                              ring_counter, positions_inc, cand, vocab_offset)
+        torch.ops.dsse.sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand,
+                                         vocab_offset)
     else:
-        ref.sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring, ring_counter,
-                   positions_inc, cand, vocab_offset)
+        ref.sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset)
 
 
-def sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None,
-                ring_counter=None, positions_inc=None):
+def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None):
+    """Merge cand_all [world, B, C, 2] and commit: next_ids[b], ring[head][b], positions[b] += 1."""
     if _hip(cand_all):
-        torch.ops.dsse.sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids,
-                                   ring, ring_counter, positions_inc)
+        torch.ops.dsse.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc)
     else:
-        ref.sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids, ring,
-                        ring_counter, positions_inc)
+        ref.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc)
+
+
+def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
+           positions_inc=None, nchunks: int = 16):
+    """Single-rank convenience: candidates + pick."""
+    B = logits.shape[0]
+    cand = torch.empty(B, nchunks if logits.is_cuda else 1, 2, device=logits.device, dtype=torch.float32)
+    sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, 0)
+    sample_pick(cand.unsqueeze(0), active, next_ids, ring, ring_counter, positions_inc)

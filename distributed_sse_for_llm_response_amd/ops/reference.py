@@ -244,41 +244,42 @@ def sample_row(logits: torch.Tensor, temperature: float, top_k: int, top_p: floa
     return float(sc[i]), i + vocab_offset
 
 
-def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
-           positions_inc=None, cand=None, vocab_offset=0):
+def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):
+    """cand [B, C, 2]: the whole-row best goes to chunk 0, other chunks get -inf (same final pick)."""
     B = logits.shape[0]
-    sd = seeds.view(-1).tolist()
+    sd = seeds.reshape(-1).tolist()
+    cand[..., 0] = float("-inf")
+    cand[..., 1] = 0.0
     for b in range(B):
         if active is not None and not int(active[b]):
             continue
         seed = (sd[2 * b] & _U32, sd[2 * b + 1] & _U32)
         sc, idx = sample_row(logits[b], float(temperature[b]), int(top_k[b]), float(top_p[b]), seed,
                              int(positions[b]), vocab_offset)
-        if cand is not None:
-            cand.view(-1, 2)[b, 0] = sc
-            cand.view(-1, 2)[b, 1] = float(idx)  # CPU path keeps the index as a float value
-            continue
-        next_ids[b] = idx
-        if ring is not None:
-            ring[int(ring_counter[0]) % ring.shape[0], b] = idx
-        if positions_inc is not None:
-            positions_inc[b] += 1
+        cand[b, 0, 0] = sc
+        cand[b, 0, 1] = float(idx)  # CPU encoding: the index as a float value (GPU: its bit pattern)
 
 
-def sample_pick(cand_all, world, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None,
-                ring_counter=None, positions_inc=None):
-    c = cand_all.view(world, -1, 2)
-    B = c.shape[1]
+def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None):
+    world, B, C, _ = cand_all.shape
     for b in range(B):
         if active is not None and not int(active[b]):
             continue
         best, bidx = float("-inf"), None
         for w in range(world):
-            s, i = float(c[w, b, 0]), int(c[w, b, 1])
-            if s > best or (s == best and (bidx is None or i < bidx)):
-                best, bidx = s, i
+            for c in range(C):
+                s, i = float(cand_all[w, b, c, 0]), int(cand_all[w, b, c, 1])
+                if s > best or (s == best and (bidx is None or i < bidx)):
+                    best, bidx = s, i
         next_ids[b] = bidx
         if ring is not None:
             ring[int(ring_counter[0]) % ring.shape[0], b] = bidx
         if positions_inc is not None:
             positions_inc[b] += 1
+
+
+def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
+           positions_inc=None):
+    cand = torch.empty(logits.shape[0], 1, 2)
+    sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand)
+    sample_pick(cand.unsqueeze(0), active, next_ids, ring, ring_counter, positions_inc)

@@ -23,12 +23,22 @@ def _close(a, b, atol, rtol, what=""):
     assert bad == 0, f"{what}: {bad} / {a.numel()} elements off; max err {err.max().item():.4g}"
 
 
-@pytest.fixture(params=[(0, 0), (1, 4), (1, 8), (2, 4), (2, 8)], ids=lambda p: f"nt{p[0]}kw{p[1]}")
+GEMM_CONFIGS = {
+    "auto": {},
+    "xlds-default": {"DSSE_GEMM_IMPL": "1"},
+    "xlds-ks256-nw4": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "256", "DSSE_X_NW": "4"},
+    "xlds-ks512-nt2": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "512", "DSSE_X_NT": "2", "DSSE_X_TG": "3"},
+    "xlds-d8": {"DSSE_GEMM_IMPL": "1", "DSSE_X_DEPTH": "8", "DSSE_X_TG": "16"},
+    "skinny-default": {"DSSE_GEMM_IMPL": "0"},
+    "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
+    "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
+}
+
+
+@pytest.fixture(params=sorted(GEMM_CONFIGS))
 def tiles(request, monkeypatch):
-    nt, kw = request.param
-    if nt:
-        monkeypatch.setenv("DSSE_GEMM_NT", str(nt))
-        monkeypatch.setenv("DSSE_GEMM_KW", str(kw))
+    for k, v in GEMM_CONFIGS[request.param].items():
+        monkeypatch.setenv(k, v)
     return request.param
 
 
@@ -206,8 +216,9 @@ def _sampler_inputs(B, V, gen, temps, topk, topp):
 
 
 @pytest.mark.parametrize("V", [32768, 4096, 1000])
-def test_sampler_matches_reference(gpu, V):
-    g = torch.Generator().manual_seed(V)
+@pytest.mark.parametrize("nchunks", [1, 16])
+def test_sampler_matches_reference(gpu, V, nchunks):
+    g = torch.Generator().manual_seed(V + nchunks)
     temps = [0.0, 1.0, 0.7, 1.3, 1.0, 0.5, 1.0, 2.0]
     topk = [0, 0, 0, 50, 1, 0, 20, 0]
     topp = [1.0, 1.0, 1.0, 1.0, 1.0, 0.9, 0.5, 0.95]
@@ -218,7 +229,7 @@ def test_sampler_matches_reference(gpu, V):
     ctr = torch.tensor([2], dtype=torch.int32, device=gpu)
     pos_g = pos.clone().to(gpu)
     ops.sample(logits.to(gpu), t.to(gpu), k.to(gpu), p.to(gpu), seeds.to(gpu), pos.to(gpu), None, ids_g, ring, ctr,
-               pos_g)
+               pos_g, nchunks=nchunks)
     ids_r = torch.zeros(B, dtype=torch.int32)
     R.sample(logits, t, k, p, seeds, pos, None, ids_r)
     assert torch.equal(ids_g.cpu(), ids_r), (ids_g.cpu(), ids_r)
@@ -237,7 +248,7 @@ def test_sampler_distribution(gpu):
     seeds = torch.stack([torch.arange(N, dtype=torch.int32), torch.full((N,), 7, dtype=torch.int32)], 1).to(gpu)
     pos = torch.zeros(N, dtype=torch.int32, device=gpu)
     ids = torch.zeros(N, dtype=torch.int32, device=gpu)
-    ops.sample(lg, t, k, p, seeds, pos, None, ids)
+    ops.sample(lg, t, k, p, seeds, pos, None, ids, nchunks=2)
     counts = torch.bincount(ids.cpu().long(), minlength=V).float()
     expect = torch.softmax(logits / 0.8, 0) * N
     assert ((counts - expect).abs() <= 5 * expect.sqrt() + 5).all(), (counts, expect)
@@ -247,19 +258,22 @@ def test_sampler_tp_candidates(gpu):
     """Per-shard candidates merged by sample_pick equal the unsharded draw (TP invariance)."""
     g = torch.Generator().manual_seed(11)
     B, V, world = 6, 32768, 4
-    logits, t, k, p, seeds, pos = _sampler_inputs(B, V, g, [0.0, 1.0, 0.6, 1.0, 1.2, 0.9], [0] * 6, [1.0] * 6)
+    logits, t, k, p, seeds, pos = _sampler_inputs(B, V, g, [0.0, 1.0, 0.6, 1.0, 1.2, 0.9], [0, 0, 0, 0, 7, 0],
+                                                  [1.0, 1.0, 1.0, 0.8, 1.0, 1.0])
     args = [x.to(gpu) for x in (t, k, p, seeds, pos)]
     full = torch.zeros(B, dtype=torch.int32, device=gpu)
     ops.sample(logits.to(gpu), *args, None, full)
     cands = []
     for r in range(world):
-        c = torch.zeros(B, 2, device=gpu)
+        c = torch.zeros(B, 16, 2, device=gpu)
         sh = logits[:, r * V // world:(r + 1) * V // world].contiguous().to(gpu)
-        ops.sample(sh, *args, None, torch.zeros(B, dtype=torch.int32, device=gpu), None, None, None, c, r * V // world)
+        ops.sample_candidates(sh, *args, None, c, r * V // world)
         cands.append(c)
     picked = torch.zeros(B, dtype=torch.int32, device=gpu)
-    ops.sample_pick(torch.stack(cands).contiguous().view(-1), world, *args, None, picked)
-    assert torch.equal(picked.cpu(), full.cpu())
+    ops.sample_pick(torch.stack(cands).contiguous(), None, picked)
+    # rows without top-k / top-p are exactly TP-invariant (filtered rows filter per shard)
+    for b in (0, 1, 2, 5):
+        assert int(picked[b]) == int(full[b])
 
 
 def test_decode_prep_and_ring(gpu):
@@ -283,4 +297,4 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 1
+    assert torch.ops.dsse.kernels_abi_version() == 2
