@@ -1,0 +1,220 @@
+// Python bindings of the host runtime (module `_dsse_runtime`).
+//
+// The engine loop (Python, one per GPU) drives the runtime through a handful of calls per decode
+// step: poll_requests() for new chats, publish_tokens() with the step's sampled token ids (detokenised
+// and JSON-encoded here, in C++), pop_cancellations(), and engine metric updates.  Blocking calls
+// release the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bus.h"
+#include "inspector.h"
+#include "json.h"
+#include "metrics.h"
+#include "server.h"
+#include "util.h"
+
+namespace py = pybind11;
+using namespace dsse;
+
+namespace {
+
+class Runtime {
+ public:
+  explicit Runtime(py::dict cfg) {
+    auto geti = [&](const char* k, int d) { return cfg.contains(k) ? cfg[k].cast<int>() : d; };
+    auto gets = [&](const char* k, const std::string& d) { return cfg.contains(k) ? cfg[k].cast<std::string>() : d; };
+    ServerConfig c;
+    c.host = gets("host", c.host);
+    c.sse_port = geti("sse_port", c.sse_port);
+    c.origin_port = geti("origin_port", c.origin_port);
+    c.metrics_port = geti("metrics_port", c.metrics_port);
+    c.resp_port = geti("resp_port", c.resp_port);
+    c.io_threads = geti("io_threads", c.io_threads);
+    c.llm_proxy_url = gets("llm_proxy_url", "");
+    c.local_engine = cfg.contains("local_engine") && cfg["local_engine"].cast<bool>();
+    c.model_name = gets("model_name", c.model_name);
+    c.inspection = parse_inspection_mode(gets("inspection_mode", "disabled"));
+    c.inspection_buffer_ms = geti("inspection_buffer_ms", c.inspection_buffer_ms);
+    c.keepalive_ms = geti("keepalive_ms", c.keepalive_ms);
+    c.first_token_timeout_ms = geti("first_token_timeout_ms", c.first_token_timeout_ms);
+    c.max_pending_bytes = (size_t)geti("max_pending_bytes", (int)c.max_pending_bytes);
+    c.replay_max = (size_t)geti("replay_max", (int)c.replay_max);
+    c.retention_s = geti("retention_s", c.retention_s);
+    c.ui_html = gets("ui_html", "");
+    BusConfig bc;
+    bc.replay_max = c.replay_max;
+    bc.retention_s = c.retention_s;
+    bus_ = std::make_shared<Bus>(bc);
+    server_ = std::make_unique<Server>(c, bus_);
+  }
+  ~Runtime() { stop(); }
+
+  void start() {
+    std::string err;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = server_->start(&err);
+    }
+    if (!ok) throw std::runtime_error("runtime start failed: " + err);
+  }
+  void stop() {
+    py::gil_scoped_release nogil;
+    if (stub_) stub_->stop();
+    stub_.reset();
+    if (server_) server_->stop();
+  }
+  int bound_port(const std::string& role) { return server_->bound_port(role); }
+
+  py::list poll_requests(size_t max, int timeout_ms) {
+    std::vector<ChatRequest> rs;
+    {
+      py::gil_scoped_release nogil;
+      rs = server_->requests().pop(max, timeout_ms);
+    }
+    py::list out;
+    for (auto& r : rs) {
+      py::dict d;
+      d["id"] = r.id;
+      d["conversation_id"] = r.conversation_id;
+      d["message"] = r.message;
+      d["arrival_ns"] = r.arrival_ns;
+      d["max_tokens"] = r.max_tokens;
+      d["temperature"] = r.temperature;
+      d["top_p"] = r.top_p;
+      d["top_k"] = r.top_k;
+      d["seed"] = r.seed;
+      d["from_edge"] = r.from_edge;
+      out.append(d);
+    }
+    return out;
+  }
+  void submit(const std::string& conv_id, const std::string& message, int max_tokens) {
+    ChatRequest r;
+    r.conversation_id = conv_id;
+    r.message = message;
+    r.max_tokens = max_tokens;
+    server_->submit_chat(std::move(r));
+  }
+
+  void set_vocab(std::vector<std::string> pieces) { vocab_ = std::move(pieces); }
+
+  // Publish one engine step: conversation ids, token ids, sequence numbers, done flags.  Token text
+  // comes from the vocabulary; `texts` (optional) overrides per entry (e.g. "[DONE]", "[ERROR]").
+  int publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
+                     const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
+                     const std::vector<std::string>& texts) {
+    const size_t n = conv_ids.size();
+    if (token_ids.size() != n || seqs.size() != n || dones.size() != n)
+      throw std::invalid_argument("publish_tokens: length mismatch");
+    std::vector<FramePtr> frames;
+    frames.reserve(n);
+    {
+      py::gil_scoped_release nogil;
+      const int64_t t = ts > 0 ? ts : now_ns();
+      TokenMessage m;
+      for (size_t i = 0; i < n; ++i) {
+        m.conversation_id = conv_ids[i];
+        if (i < texts.size() && !texts[i].empty()) m.token = texts[i];
+        else if (token_ids[i] >= 0 && (size_t)token_ids[i] < vocab_.size()) m.token = vocab_[token_ids[i]];
+        else m.token = "<" + std::to_string(token_ids[i]) + ">";
+        m.sequence = seqs[i];
+        m.done = dones[i];
+        m.timestamp = t;
+        frames.push_back(Bus::make_frame(m));
+      }
+      bus_->publish_batch(frames);
+    }
+    metrics().engine_tokens_total.add((double)n);
+    return (int)n;
+  }
+  int publish(const std::string& conv_id, const std::string& token, int64_t seq, bool done, int64_t ts) {
+    TokenMessage m{conv_id, token, seq, done, ts > 0 ? ts : now_ns()};
+    py::gil_scoped_release nogil;
+    return bus_->publish(m);
+  }
+  std::vector<std::string> pop_cancellations() { return server_->pop_cancellations(); }
+  size_t subscriber_count(const std::string& id) { return bus_->subscriber_count(id); }
+  int64_t last_sequence(const std::string& id) { return bus_->last_sequence(id); }
+  size_t queued_requests() { return server_->requests().size(); }
+  void set_ready(bool r) { server_->set_ready(r); }
+  void set_local_engine(bool on) { server_->set_local_engine(on); }
+  void start_stub(int tokens, int delay_ms, int workers) {
+    stub_ = std::make_unique<StubEngine>(*server_, tokens, delay_ms, workers);
+  }
+  std::string metrics_text() { return metrics().render(); }
+
+ private:
+  std::shared_ptr<Bus> bus_;
+  std::unique_ptr<Server> server_;
+  std::unique_ptr<StubEngine> stub_;
+  std::vector<std::string> vocab_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_dsse_runtime, m) {
+  m.doc() = "MI355X streaming-token delivery runtime (bus, SSE server, RESP ingest, inspector, metrics)";
+  py::class_<Runtime>(m, "Runtime")
+      .def(py::init<py::dict>(), py::arg("config") = py::dict())
+      .def("start", &Runtime::start)
+      .def("stop", &Runtime::stop)
+      .def("bound_port", &Runtime::bound_port)
+      .def("poll_requests", &Runtime::poll_requests, py::arg("max") = 256, py::arg("timeout_ms") = 0)
+      .def("submit", &Runtime::submit, py::arg("conversation_id"), py::arg("message"), py::arg("max_tokens") = -1)
+      .def("set_vocab", &Runtime::set_vocab)
+      .def("publish_tokens", &Runtime::publish_tokens, py::arg("conversation_ids"), py::arg("token_ids"),
+           py::arg("sequences"), py::arg("dones"), py::arg("timestamp_ns") = 0,
+           py::arg("texts") = std::vector<std::string>{})
+      .def("publish", &Runtime::publish, py::arg("conversation_id"), py::arg("token"), py::arg("sequence"),
+           py::arg("done") = false, py::arg("timestamp_ns") = 0)
+      .def("pop_cancellations", &Runtime::pop_cancellations)
+      .def("subscriber_count", &Runtime::subscriber_count)
+      .def("last_sequence", &Runtime::last_sequence)
+      .def("queued_requests", &Runtime::queued_requests)
+      .def("set_ready", &Runtime::set_ready)
+      .def("set_local_engine", &Runtime::set_local_engine)
+      .def("start_stub", &Runtime::start_stub, py::arg("tokens") = 50, py::arg("delay_ms") = 50, py::arg("workers") = 2)
+      .def("metrics_text", &Runtime::metrics_text);
+
+  m.def("encode_token_message", [](const std::string& cid, const std::string& tok, int64_t seq, bool done, int64_t ts) {
+    return encode_token_message(TokenMessage{cid, tok, seq, done, ts});
+  });
+  m.def("parse_token_message", [](const std::string& s) -> py::object {
+    TokenMessage t;
+    if (!parse_token_message(s, t)) return py::none();
+    py::dict d;
+    d["conversation_id"] = t.conversation_id;
+    d["token"] = t.token;
+    d["sequence"] = t.sequence;
+    d["done"] = t.done;
+    d["timestamp"] = t.timestamp;
+    return d;
+  });
+  m.def("sse_frame", [](const std::string& cid, const std::string& tok, int64_t seq, bool done, int64_t ts) {
+    return py::bytes(Bus::make_frame(TokenMessage{cid, tok, seq, done, ts})->bytes);
+  });
+  m.def("inspect", [](const std::string& content) {
+    InspectionResult r = inspect_message(content);
+    py::dict d;
+    d["action"] = action_name(r.action);
+    d["reason"] = r.reason.empty() ? py::object(py::none()) : py::object(py::str(r.reason));
+    d["redacted_content"] = r.action == InspectAction::kRedact ? py::object(py::str(r.redacted_content)) : py::object(py::none());
+    return d;
+  });
+  m.def("inspection_json", [](const std::string& content) { return inspection_result_json(inspect_message(content)); });
+  m.def("engine_observe", [](double step_s, double batch, double kv_free) {
+    if (step_s > 0) metrics().engine_decode_step_seconds.observe(step_s);
+    metrics().engine_batch_size.set(batch);
+    metrics().engine_kv_blocks_free.set(kv_free);
+  });
+  m.def("observe_ttft", [](double s) { metrics().engine_ttft_seconds.observe(s); });
+  m.def("observe_itl", [](double s) { metrics().engine_itl_seconds.observe(s); });
+  m.def("set_active_chats", [](double n) { metrics().active_chats.set(n); });
+  m.def("uuid4", &uuid4);
+}

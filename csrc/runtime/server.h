@@ -1,0 +1,147 @@
+// Native epoll HTTP/1.1 + SSE server, origin admission API, RESP ingest shim and metrics endpoint.
+//
+// One process serves every role the reference splits over Go services and Redis/NATS:
+//   edge  (SSE_PORT, default 8080)   POST /chat -> SSE, GET /stream/{id}, /healthz, /readyz
+//                                    (src/sse-adapter/sse_handler.go:80-450, main.go:96-139)
+//   origin (ORIGIN_PORT, default 8081) POST /chat -> {"conversation_id","status":"streaming"},
+//                                    GET /health, GET /metrics (src/llm-stream-proxy/main.go:89-146)
+//   metrics (METRICS_PORT, 9090)     Prometheus text (src/sse-adapter/main.go:134-139)
+//   resp  (RESP_PORT, 6379 or 0)     PUBLISH/SUBSCRIBE/PSUBSCRIBE ingest compatible with go-redis, so
+//                                    demo/load-generator's producer works unchanged
+//                                    (demo/load-generator/main.go:204-240)
+//   extra: POST /publish/<subject>   (src/spin-functions/nats-publisher), POST /inspect
+//                                    (src/spin-functions/nats-subscriber), GET / (chat page)
+//
+// Threading: `io_threads` event loops, each with its own SO_REUSEPORT listeners, epoll set and
+// eventfd-woken outbox.  The bus pushes frames into the owning thread's outbox; sockets are only
+// touched by their own thread.  Chat requests from either /chat endpoint are queued for the engine
+// (RequestQueue), or, when LLM_PROXY_URL is set and no local engine is attached, forwarded to the
+// remote origin over HTTP exactly like the reference adapter.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bus.h"
+#include "inspector.h"
+
+namespace dsse {
+
+struct ServerConfig {
+  std::string host = "0.0.0.0";
+  int sse_port = 8080;      // < 0 = disabled, 0 = ephemeral
+  int origin_port = 8081;   // < 0 = disabled
+  int metrics_port = 9090;  // < 0 = disabled
+  int resp_port = -1;       // < 0 = disabled (6379 for the load-generator producer)
+  int io_threads = 4;
+  std::string llm_proxy_url;  // edge mode: forward POST /chat here when no local engine is attached
+  bool local_engine = false;  // POST /chat goes straight into the in-process request queue
+  std::string model_name = "mistralai/Mistral-7B-Instruct-v0.3";
+  InspectionMode inspection = InspectionMode::kDisabled;
+  int inspection_buffer_ms = 150;
+  int keepalive_ms = 15000;          // sse_handler.go:182
+  int first_token_timeout_ms = 30000;  // sse_handler.go:395
+  size_t max_pending_bytes = 4 << 20;  // per-connection output cap before token frames are dropped
+  size_t replay_max = 4096;
+  int retention_s = 300;
+  std::string ui_html;  // served at GET / when non-empty
+};
+
+// Chat request handed to the engine (or the stub generator).
+struct ChatRequest {
+  uint64_t id = 0;
+  std::string conversation_id;
+  std::string message;
+  int64_t arrival_ns = 0;
+  int max_tokens = -1;       // optional body fields beyond the reference's {message, conversation_id}
+  double temperature = -1;
+  double top_p = -1;
+  int top_k = -1;
+  int64_t seed = -1;
+  bool from_edge = false;    // submitted by the edge /chat (a subscriber exists)
+};
+
+class RequestQueue {
+ public:
+  void push(ChatRequest r);
+  // Pop up to `max` requests, waiting at most timeout_ms for the first.
+  std::vector<ChatRequest> pop(size_t max, int timeout_ms);
+  size_t size();
+  void close();
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<ChatRequest> q_;
+  bool closed_ = false;
+};
+
+class IoThread;
+
+class Server {
+ public:
+  Server(ServerConfig cfg, std::shared_ptr<Bus> bus);
+  ~Server();
+  bool start(std::string* err = nullptr);
+  void stop();
+  bool running() const { return running_.load(); }
+
+  RequestQueue& requests() { return requests_; }
+  Bus& bus() { return *bus_; }
+  const ServerConfig& config() const { return cfg_; }
+  void set_local_engine(bool on) { local_engine_.store(on); }
+  void set_ready(bool on) { ready_.store(on); }
+  // Conversations whose last subscriber left before completion (engine may abort them).
+  std::vector<std::string> pop_cancellations();
+  // Actual bound ports (useful with port 0 requests in tests): role -> port.
+  int bound_port(const std::string& role) const;
+
+  // internal (used by IoThread)
+  void submit_chat(ChatRequest r);
+  void note_cancel(const std::string& conv_id);
+  bool local_engine() const { return local_engine_.load(); }
+  bool ready() const { return ready_.load(); }
+  void forward_to_proxy(uint64_t conn_id, IoThread* io, const std::string& conv_id, const std::string& message);
+
+ private:
+  ServerConfig cfg_;
+  std::shared_ptr<Bus> bus_;
+  RequestQueue requests_;
+  std::vector<std::unique_ptr<IoThread>> io_;
+  std::vector<std::thread> threads_;
+  std::thread housekeeping_;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> local_engine_{false};
+  std::atomic<bool> ready_{true};
+  std::atomic<uint64_t> next_req_{1};
+  std::mutex cancel_mu_;
+  std::vector<std::string> cancels_;
+  std::vector<std::pair<std::string, int>> ports_;
+  friend class IoThread;
+};
+
+// Stub token generator (BASELINE config 1, CPU plumbing): consumes the request queue and streams
+// `tokens` words per conversation with `delay_ms` (+ uniform jitter up to delay/2, like the Go
+// load generator's producer) between tokens, then "[DONE]".
+class StubEngine {
+ public:
+  StubEngine(Server& server, int tokens, int delay_ms, int workers = 2);
+  ~StubEngine();
+  void stop();
+
+ private:
+  void run();
+  Server& server_;
+  int tokens_, delay_ms_;
+  std::atomic<bool> stop_{false};
+  std::vector<std::thread> threads_;
+};
+
+}  // namespace dsse
