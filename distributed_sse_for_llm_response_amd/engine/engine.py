@@ -1,0 +1,356 @@
+"""Continuous-batching LLM engine: scheduler + pipelined decode + asynchronous token-ring drain.
+
+Replaces vLLM's scheduler/worker loop behind the reference's proxy (reference
+``src/llm-stream-proxy/main.go:148-228`` consumed vLLM's OpenAI SSE stream; here the engine emits
+token events directly).  One engine per GPU (DP replica) or per TP group.
+
+Per ``step()`` (host, a few hundred microseconds of Python):
+
+1. admit waiting requests into free decode slots (lowest index first so live slots stay packed and
+   the smallest captured batch bucket applies), allocating KV pages for prompt + max_tokens;
+2. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
+   non-blocking copies on the compute stream;
+3. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
+   streams keep their inter-token latency while new prompts are absorbed);
+4. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
+   next step; token ring row ``t`` receives every token produced in step ``t``);
+5. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
+   earlier steps: sequence numbers, EOS / max_tokens stops, TTFT / ITL accounting.
+
+The GPU is never idle waiting for the host: step ``t+1`` is enqueued before row ``t`` is read.  Stops
+discovered late (EOS) cost at most one wasted decode step for that slot, and the slot's pages are
+only reused by work enqueued after the stop, so stream order makes reuse safe.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import time
+from collections import deque
+from dataclasses import dataclass, field
+
+import torch
+
+from .kv_cache import BlockAllocator, blocks_needed
+from .model_runner import RING_SIZE, ModelRunner, PrefillSeq, batch_buckets
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 1.0   # vLLM OpenAI-server defaults (the proxy sets none: main.go:155-163)
+    top_p: float = 1.0
+    top_k: int = 0
+    max_tokens: int = 256
+    seed: int | None = None
+    ignore_eos: bool = False
+
+
+@dataclass
+class TokenEvent:
+    conversation_id: str
+    token_id: int
+    sequence: int
+    done: bool
+    text: str = ""          # overrides the vocabulary piece ("[DONE]", "[ERROR]")
+    timestamp_ns: int = 0
+
+
+@dataclass
+class Sequence:
+    rid: int
+    conversation_id: str
+    prompt: list
+    params: SamplingParams
+    arrival_ns: int = 0
+    slot: int = -1
+    blocks: list = field(default_factory=list)
+    prefilled: int = 0
+    state: str = "waiting"      # waiting | prefill | decode | finished
+    decode_enqueued: int = 0    # decode steps enqueued (tokens 2..n)
+    produced: int = 0           # tokens drained and published
+    first_token_ns: int = 0
+    last_token_ns: int = 0
+    aborted: bool = False
+    stop_after_enqueue: bool = False
+
+
+class _Drain:
+    def __init__(self, runner: ModelRunner):
+        self.r = runner
+        self.cuda = runner.device.type == "cuda"
+        B = runner.max_batch
+        if self.cuda:
+            self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32).pin_memory()
+            self.stream = torch.cuda.Stream(runner.device)
+            self.events = [torch.cuda.Event() for _ in range(RING_SIZE)]
+        else:
+            self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32)
+
+    def issue(self, row: int, width: int):
+        if not self.cuda:
+            self.host[row, :width] = self.r.ring[row, :width]
+            return
+        self.stream.wait_stream(torch.cuda.current_stream(self.r.device))
+        with torch.cuda.stream(self.stream):
+            self.host[row, :width].copy_(self.r.ring[row, :width], non_blocking=True)
+            self.events[row].record(self.stream)
+
+    def ready(self, row: int) -> bool:
+        return (not self.cuda) or self.events[row].query()
+
+    def wait(self, row: int):
+        if self.cuda:
+            self.events[row].synchronize()
+        return self.host[row]
+
+
+class LLMEngine:
+    def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 2048,
+                 idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
+                 pipeline_depth: int = 1):
+        self.r = runner
+        self.eos_id = eos_id
+        self.alloc = BlockAllocator(runner.kv.num_blocks)
+        self.prefill_budget = prefill_budget
+        self.idle_prefill_budget = idle_prefill_budget or runner.max_prefill_tokens
+        self.default_params = default_params or SamplingParams()
+        self.depth = pipeline_depth
+        self.waiting: deque = deque()
+        self.slots: list = [None] * runner.max_batch
+        self.by_conv: dict = {}
+        self.step_no = 0
+        self.inflight: deque = deque()  # (step, ring_row, producers [(slot, seq)], t_enqueue)
+        self.drain = _Drain(runner)
+        self._rid = itertools.count(1)
+        self._dirty_slots: set = set()
+        self.ring_head = int(runner.ring_counter.item()) if runner.device.type == "cuda" else int(runner.ring_counter[0])
+        self.stats = {"steps": 0, "decode_steps": 0, "prefill_tokens": 0, "tokens": 0, "last_step_s": 0.0}
+        self.on_ttft = None
+        self.on_itl = None
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, conversation_id: str, prompt: list, params: SamplingParams | None = None,
+                    arrival_ns: int | None = None) -> Sequence:
+        p = params or self.default_params
+        max_prompt = self.r.max_model_len - 1
+        if len(prompt) > max_prompt:
+            prompt = prompt[-max_prompt:]  # keep the tail (most recent context)
+        s = Sequence(rid=next(self._rid), conversation_id=conversation_id, prompt=list(prompt), params=p,
+                     arrival_ns=arrival_ns or time.time_ns())
+        self.waiting.append(s)
+        self.by_conv[conversation_id] = s
+        return s
+
+    def abort(self, conversation_id: str) -> bool:
+        s = self.by_conv.get(conversation_id)
+        if s is None or s.state == "finished":
+            return False
+        s.aborted = True
+        if s.state == "waiting":
+            self.waiting.remove(s)
+            self._finish(s, [], reason="abort")
+        return True
+
+    def has_work(self) -> bool:
+        return bool(self.waiting) or any(s is not None for s in self.slots) or bool(self.inflight)
+
+    def num_running(self) -> int:
+        return sum(1 for s in self.slots if s is not None)
+
+    # ------------------------------------------------------------------ helpers
+    def _upload(self):
+        """Push host-side slot metadata changes to the device (pinned, non-blocking)."""
+        if not self._dirty_slots:
+            return
+        r = self.r
+        Bm = r.max_batch
+        active = torch.zeros(Bm, dtype=torch.int32)
+        temp = torch.zeros(Bm, dtype=torch.float32)
+        topk = torch.zeros(Bm, dtype=torch.int32)
+        topp = torch.ones(Bm, dtype=torch.float32)
+        seeds = torch.zeros(Bm, 2, dtype=torch.int32)
+        for i, s in enumerate(self.slots):
+            if s is None:
+                continue
+            if s.state == "decode" and not s.aborted and not s.stop_after_enqueue:
+                active[i] = 1
+            temp[i] = s.params.temperature
+            topk[i] = s.params.top_k
+            topp[i] = s.params.top_p
+            sd = s.params.seed if s.params.seed is not None else (s.rid * 2654435761) & 0x7FFFFFFF
+            seeds[i, 0] = sd & 0x7FFFFFFF
+            seeds[i, 1] = (sd >> 31) & 0x7FFFFFFF
+        bt_rows = {}
+        for i in self._dirty_slots:
+            s = self.slots[i]
+            if s is not None and s.blocks:
+                row = torch.zeros(r.max_blocks, dtype=torch.int32)
+                row[: len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+                bt_rows[i] = row
+        cuda = r.device.type == "cuda"
+
+        def put(dst, src):
+            if cuda:
+                dst.copy_(src.pin_memory(), non_blocking=True)
+            else:
+                dst.copy_(src)
+
+        put(r.active, active)
+        put(r.temperature, temp)
+        put(r.top_k, topk)
+        put(r.top_p, topp)
+        put(r.seeds, seeds)
+        for i, row in bt_rows.items():
+            put(r.block_tables[i], row)
+        self._dirty_slots.clear()
+
+    def _admit(self):
+        r = self.r
+        while self.waiting:
+            s = self.waiting[0]
+            free = [i for i, x in enumerate(self.slots) if x is None]
+            if not free:
+                return
+            max_new = max(1, min(s.params.max_tokens, r.max_model_len - len(s.prompt)))
+            s.params = SamplingParams(**{**s.params.__dict__, "max_tokens": max_new})
+            need = blocks_needed(len(s.prompt) + max_new + 1)
+            if not self.alloc.can_allocate(need):
+                return
+            self.waiting.popleft()
+            s.blocks = self.alloc.allocate(need)
+            s.slot = free[0]
+            s.state = "prefill"
+            self.slots[s.slot] = s
+            self._dirty_slots.add(s.slot)
+
+    def _schedule_prefill(self, t: int):
+        running_decode = any(s is not None and s.state == "decode" for s in self.slots)
+        budget = self.prefill_budget if running_decode else self.idle_prefill_budget
+        chunks, finished = [], []
+        for s in self.slots:
+            if s is None or s.state != "prefill" or s.aborted or budget <= 0:
+                continue
+            n = min(len(s.prompt) - s.prefilled, budget)
+            last = s.prefilled + n == len(s.prompt)
+            chunks.append(PrefillSeq(slot=s.slot, tokens=s.prompt[s.prefilled:s.prefilled + n], start_pos=s.prefilled,
+                                     block_table=s.blocks, last_chunk=last))
+            s.prefilled += n
+            budget -= n
+            if last:
+                finished.append(s)
+        return chunks, finished
+
+    def _finish(self, s: Sequence, events: list, reason: str = "stop", text: str = "[DONE]"):
+        if s.state == "finished":
+            return
+        s.state = "finished"
+        now = time.time_ns()
+        events.append(TokenEvent(s.conversation_id, -1, s.produced + 1, True, text=text, timestamp_ns=now))
+        if s.slot >= 0 and self.slots[s.slot] is s:
+            self.slots[s.slot] = None
+            self._dirty_slots.add(s.slot)
+        if s.blocks:
+            self.alloc.free(s.blocks)
+            s.blocks = []
+        if self.by_conv.get(s.conversation_id) is s:
+            del self.by_conv[s.conversation_id]
+
+    # ------------------------------------------------------------------ step
+    def step(self, block: bool = True) -> list:
+        """Enqueue one engine step and return the token events of completed earlier steps."""
+        t0 = time.perf_counter()
+        events: list = []
+        r = self.r
+        # sequences whose max_tokens budget is fully enqueued stop decoding now
+        for s in self.slots:
+            if s is not None and s.state == "decode" and s.decode_enqueued + 1 >= s.params.max_tokens:
+                if not s.stop_after_enqueue:
+                    s.stop_after_enqueue = True
+                    self._dirty_slots.add(s.slot)
+            if s is not None and s.aborted and s.state != "finished":
+                self._dirty_slots.add(s.slot)
+        self._admit()
+        row = self.ring_head % RING_SIZE
+        chunks, prefill_done = self._schedule_prefill(self.step_no)
+        self._upload()
+        producers = []
+        ran = False
+        if chunks:
+            r.prefill(chunks, ring_row=row)
+            self.stats["prefill_tokens"] += sum(len(c.tokens) for c in chunks)
+            producers += [(s.slot, s) for s in prefill_done]
+            ran = True
+        dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
+               and not s.stop_after_enqueue]
+        if dec:
+            hi = max(s.slot for s in dec) + 1
+            B = next(b for b in batch_buckets(r.max_batch) if b >= hi)
+            r.decode(B)
+            for s in dec:
+                s.decode_enqueued += 1
+                producers.append((s.slot, s))
+            self.stats["decode_steps"] += 1
+            ran = True
+        elif ran:
+            from .. import ops
+            ops.ring_advance(r.ring_counter)
+        for s in prefill_done:
+            s.state = "decode"
+            self._dirty_slots.add(s.slot)
+        if ran:
+            width = max(sl for sl, _ in producers) + 1 if producers else 1
+            self.drain.issue(row, width)
+            self.inflight.append((self.step_no, row, producers, t0))
+            self.ring_head += 1
+            self.step_no += 1
+        # ---- consume drained steps: keep `depth` steps in flight, process everything that is ready
+        while self.inflight:
+            st, rrow, prods, tq = self.inflight[0]
+            must = len(self.inflight) > self.depth or not ran
+            if not must and not self.drain.ready(rrow):
+                break
+            if not must and not block:
+                break
+            toks = self.drain.wait(rrow)
+            self.inflight.popleft()
+            self._consume(toks, prods, events)
+        # aborted sequences leave at this boundary
+        for s in list(self.slots):
+            if s is not None and s.aborted and s.state != "finished" and not any(
+                    s is p for _, _, prods, _ in self.inflight for _, p in prods):
+                self._finish(s, events, reason="abort")
+        self.stats["steps"] += 1
+        self.stats["last_step_s"] = time.perf_counter() - t0
+        return events
+
+    def _consume(self, toks, prods, events):
+        now = time.time_ns()
+        tl = toks.tolist()
+        for slot, s in prods:
+            if s.state == "finished" or s.aborted:
+                continue
+            tok = int(tl[slot])
+            s.produced += 1
+            if s.produced == 1:
+                s.first_token_ns = now
+                if self.on_ttft:
+                    self.on_ttft((now - s.arrival_ns) / 1e9)
+            elif self.on_itl and s.last_token_ns:
+                self.on_itl((now - s.last_token_ns) / 1e9)
+            s.last_token_ns = now
+            is_eos = tok == self.eos_id and not s.params.ignore_eos
+            if not is_eos:
+                events.append(TokenEvent(s.conversation_id, tok, s.produced, False, timestamp_ns=now))
+                self.stats["tokens"] += 1
+            else:
+                s.produced -= 1
+            if is_eos or s.produced >= s.params.max_tokens or len(s.prompt) + s.produced >= self.r.max_model_len:
+                self._finish(s, events)
+
+    def run_until_idle(self, max_steps: int = 100000) -> list:
+        out = []
+        for _ in range(max_steps):
+            if not self.has_work():
+                break
+            out += self.step()
+        return out

@@ -1,0 +1,155 @@
+"""The serving process: native runtime (HTTP/SSE/bus) + one engine loop per GPU replica.
+
+Data path of one token (compare reference README.md:59-68, six network hops and four JSON
+round trips): sampled on the GPU into the HBM token ring -> side-stream copy into pinned host memory
+-> engine loop publishes the step's tokens in one call -> C++ bus formats one SSE frame per token
+and fans it out to the subscribed connections' I/O threads -> epoll writer.  No network hop inside
+the node.
+
+Engine kinds:
+* ``gpu``  Mistral on the gfx950 kernels (TP group of this process, captured hipGraphs);
+* ``cpu``  the same engine on the fp32 reference ops with a tiny model (plumbing tests, no GPU);
+* ``stub`` the C++ stub token generator (BASELINE config 1: delivery plumbing only).
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import torch
+
+from .. import runtime as rt_mod
+from ..engine.engine import LLMEngine, SamplingParams
+from ..engine.kv_cache import KVCache
+from ..engine.model_runner import ModelRunner
+from ..models.mistral import TINY, get_config, init_standard_weights
+from ..models.tokenizer import get_tokenizer
+from .config import ServeConfig
+
+
+def build_engine(cfg: ServeConfig, device=None, comm=None):
+    """Weights + KV cache + runner + engine for this process (one DP replica / TP rank)."""
+    from ..engine.weights import convert_standard, load_safetensors, random_engine_weights
+
+    if cfg.engine == "cpu":
+        mcfg = TINY if cfg.model.startswith("mistral-7b") else get_config(cfg.model)
+        w = convert_standard(mcfg, init_standard_weights(mcfg, seed=cfg.seed))
+        runner = ModelRunner(w, num_blocks=256, max_batch=min(cfg.max_batch, 8),
+                             max_model_len=min(cfg.max_model_len, 1024), device="cpu", use_graphs=False)
+    else:
+        device = device or torch.device("cuda", torch.cuda.current_device())
+        mcfg = get_config(cfg.model)
+        tp_rank, tp = (comm.rank, comm.size) if comm is not None else (0, 1)
+        if cfg.weights_path:
+            w = load_safetensors(mcfg, cfg.weights_path, tp_rank, tp, device)
+        else:
+            w = random_engine_weights(mcfg, tp_rank=tp_rank, tp_size=tp, device=device, seed=cfg.seed)
+        free, total = torch.cuda.mem_get_info(device)
+        budget = int(total * cfg.gpu_memory_utilization) - (total - free) - (2 << 30)
+        nkv = mcfg.num_kv_heads // tp
+        nblk = max(64, min(KVCache.blocks_for_budget(budget, mcfg.num_layers, nkv),
+                           cfg.max_batch * (cfg.max_model_len // 32 + 2) * 4))
+        runner = ModelRunner(w, num_blocks=nblk, max_batch=cfg.max_batch, max_model_len=cfg.max_model_len,
+                             device=device, comm=comm)
+        runner.capture()
+    tok = get_tokenizer(mcfg.vocab_size, cfg.tokenizer_path or None)
+    engine = LLMEngine(runner, eos_id=tok.eos_id, prefill_budget=cfg.prefill_budget,
+                       default_params=SamplingParams(temperature=cfg.temperature, max_tokens=cfg.max_tokens))
+    return engine, tok
+
+
+class EngineLoop(threading.Thread):
+    """Pulls chat requests from the runtime, steps the engine, publishes token events."""
+
+    def __init__(self, runtime, engine: LLMEngine, tokenizer, cfg: ServeConfig):
+        super().__init__(daemon=True, name="engine-loop")
+        self.rt, self.engine, self.tok, self.cfg = runtime, engine, tokenizer, cfg
+        self.stop_flag = threading.Event()
+        self.error = None
+        rt = rt_mod.load()
+        engine.on_ttft = rt.observe_ttft
+        engine.on_itl = rt.observe_itl
+        self._rt = rt
+
+    def _params(self, req) -> SamplingParams:
+        d = self.engine.default_params
+        return SamplingParams(
+            temperature=req["temperature"] if req["temperature"] >= 0 else d.temperature,
+            top_p=req["top_p"] if 0 < req["top_p"] <= 1 else d.top_p,
+            top_k=req["top_k"] if req["top_k"] > 0 else d.top_k,
+            max_tokens=req["max_tokens"] if req["max_tokens"] > 0 else d.max_tokens,
+            seed=req["seed"] if req["seed"] >= 0 else None)
+
+    def publish(self, events):
+        if not events:
+            return
+        self.rt.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
+                               [e.sequence for e in events], [e.done for e in events], 0,
+                               [e.text for e in events])
+
+    def run(self):
+        try:
+            while not self.stop_flag.is_set():
+                busy = self.engine.has_work()
+                for req in self.rt.poll_requests(256, 0 if busy else 20):
+                    self.engine.add_request(req["conversation_id"], self.tok.chat_prompt(req["message"]),
+                                            self._params(req), arrival_ns=req["arrival_ns"])
+                for conv in self.rt.pop_cancellations():
+                    self.engine.abort(conv)
+                if not self.engine.has_work():
+                    continue
+                events = self.engine.step()
+                self.publish(events)
+                self._rt.engine_observe(self.engine.stats["last_step_s"], float(self.engine.num_running()),
+                                        float(self.engine.alloc.num_free))
+                self._rt.set_active_chats(float(self.engine.num_running() + len(self.engine.waiting)))
+        except Exception as e:  # noqa: BLE001 - surfaced to the operator, readiness drops
+            self.error = e
+            self.rt.set_ready(False)
+            raise
+
+
+class ServingApp:
+    def __init__(self, cfg: ServeConfig, device=None, comm=None):
+        self.cfg = cfg
+        mod = rt_mod.load()
+        rd = cfg.runtime_dict()
+        rd["local_engine"] = cfg.engine in ("gpu", "cpu", "stub")
+        self.rt = mod.Runtime(rd)
+        self.loop = None
+        self.engine = None
+        self.tok = None
+        if cfg.engine in ("gpu", "cpu"):
+            self.rt.set_ready(False)
+            self.engine, self.tok = build_engine(cfg, device=device, comm=comm)
+            self.rt.set_vocab(self.tok.pieces())
+
+    def start(self):
+        self.rt.start()
+        if self.cfg.engine == "stub":
+            self.rt.start_stub(self.cfg.stub_tokens, self.cfg.stub_token_delay_ms, 2)
+        elif self.engine is not None:
+            self.loop = EngineLoop(self.rt, self.engine, self.tok, self.cfg)
+            self.loop.start()
+            self.rt.set_ready(True)
+        return self
+
+    def port(self, role: str) -> int:
+        return self.rt.bound_port(role)
+
+    def stop(self):
+        if self.loop is not None:
+            self.loop.stop_flag.set()
+            self.loop.join(timeout=10)
+        self.rt.stop()
+
+    def serve_forever(self):
+        try:
+            while True:
+                time.sleep(0.5)
+                if self.loop is not None and not self.loop.is_alive():
+                    raise RuntimeError(f"engine loop died: {self.loop.error!r}")
+        except KeyboardInterrupt:
+            pass
+        finally:
+            self.stop()

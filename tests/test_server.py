@@ -1,0 +1,282 @@
+"""HTTP / SSE / RESP behaviour of the native server against the reference's contract
+(src/sse-adapter/sse_handler.go, src/llm-stream-proxy/main.go, demo/load-generator/main.go)."""
+import json
+import socket
+import threading
+import time
+
+import pytest
+
+from distributed_sse_for_llm_response_amd import runtime as rtmod
+from distributed_sse_for_llm_response_amd.utils.sse_client import RespClient, request
+
+H = "127.0.0.1"
+
+
+def make_rt(**kw):
+    cfg = {"sse_port": 0, "origin_port": 0, "metrics_port": 0, "resp_port": 0, "io_threads": 2, "host": H}
+    cfg.update(kw)
+    r = rtmod.load().Runtime(cfg)
+    r.start()
+    return r
+
+
+@pytest.fixture
+def stub_rt():
+    r = make_rt()
+    r.start_stub(6, 2, 1)
+    yield r
+    r.stop()
+
+
+@pytest.fixture
+def bare_rt():
+    r = make_rt()
+    yield r
+    r.stop()
+
+
+def tokens_of(resp):
+    return [e.json() for e in resp.events if e.event == "token"]
+
+
+def test_chat_sse_stream(stub_rt):
+    p = stub_rt.bound_port("edge")
+    resp = request(H, p, "POST", "/chat", {"message": "hello"})
+    assert resp.status == 200
+    assert resp.headers["content-type"] == "text/event-stream"
+    assert resp.headers["cache-control"] == "no-cache"
+    assert resp.headers["access-control-allow-origin"] == "*"
+    assert resp.headers["x-accel-buffering"] == "no"
+    assert resp.events[0].event == "connected"
+    conv = json.loads(resp.events[0].data)["conversation_id"]
+    toks = tokens_of(resp)
+    assert [t["sequence"] for t in toks] == [1, 2, 3, 4, 5, 6, 7]
+    assert all(t["conversation_id"] == conv for t in toks)
+    assert toks[-1] == {**toks[-1], "token": "[DONE]", "done": True}
+    assert [e.id for e in resp.events if e.event == "token"] == [str(i) for i in range(1, 8)]
+    assert all(t["timestamp"] > 1_600_000_000_000_000_000 for t in toks)  # nanoseconds
+
+
+def test_chat_with_given_conversation_id_and_keepalive_reuse(stub_rt):
+    p = stub_rt.bound_port("edge")
+    s = socket.create_connection((H, p))
+    try:
+        for i in range(2):  # two requests on one keep-alive connection
+            body = json.dumps({"message": "x", "conversation_id": f"my-conv-{i}"}).encode()
+            s.sendall(b"POST /chat HTTP/1.1\r\nHost: h\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+            buf = b""
+            while not buf.endswith(b"0\r\n\r\n"):
+                buf += s.recv(65536)
+            assert b'"conversation_id":"my-conv-%d"' % i in buf
+            assert b'"done":true' in buf
+    finally:
+        s.close()
+
+
+def test_chat_errors(bare_rt):
+    p = bare_rt.bound_port("edge")
+    r = request(H, p, "POST", "/chat", {"message": "hi"})
+    assert r.status == 503 and r.body == b"LLM proxy not configured\n"
+    bare_rt.set_local_engine(True)
+    r = request(H, p, "POST", "/chat", b"{not json")
+    assert r.status == 400 and r.body == b"Invalid JSON body\n"
+    r = request(H, p, "POST", "/chat", {"message": ""})
+    assert r.status == 400 and r.body == b"message is required\n"
+    r = request(H, p, "GET", "/chat")
+    assert r.status == 405 and r.body == b"Method not allowed\n"
+    r = request(H, p, "OPTIONS", "/chat")
+    assert r.status == 200
+    assert r.headers["access-control-allow-methods"] == "POST, OPTIONS"
+    assert r.headers["access-control-allow-headers"] == "Content-Type"
+    assert r.headers["access-control-allow-origin"] == "*"
+    r = request(H, p, "GET", "/nope")
+    assert r.status == 404
+
+
+def test_first_token_timeout():
+    r = make_rt(first_token_timeout_ms=200)
+    try:
+        r.set_local_engine(True)  # requests queue up but nothing generates
+        resp = request(H, r.bound_port("edge"), "POST", "/chat", {"message": "hi"}, timeout=5)
+        assert resp.events[0].event == "connected"
+        assert resp.events[-1].event == "error"
+        assert json.loads(resp.events[-1].data) == {"error": "timeout waiting for response"}
+        assert len(r.poll_requests(10, 0)) == 1
+    finally:
+        r.stop()
+
+
+def test_keepalive_comments():
+    r = make_rt(keepalive_ms=100)
+    try:
+        resp = request(H, r.bound_port("edge"), "GET", "/stream/ka-test", timeout=5, max_events=4)
+        assert resp.events[0].comment == "connected to ka-test"
+        assert [e.comment for e in resp.events[1:4]] == ["keep-alive"] * 3
+    finally:
+        r.stop()
+
+
+def test_stream_publish_and_last_event_id_replay(bare_rt):
+    p = bare_rt.bound_port("edge")
+    conv = "replay-1"
+    for i in range(1, 6):
+        bare_rt.publish(conv, f"t{i}", i, False, 0)
+    # reconnect with Last-Event-ID: 2 -> frames 3, 4, 5 (no off-by-one loss), then live frames
+    got = []
+
+    def reader():
+        got.append(request(H, p, "GET", f"/stream/{conv}", headers={"Last-Event-ID": "2"}, timeout=5))
+
+    th = threading.Thread(target=reader)
+    th.start()
+    time.sleep(0.3)
+    bare_rt.publish(conv, "t6", 6, False, 0)
+    bare_rt.publish(conv, "[DONE]", 7, True, 0)
+    th.join(5)
+    toks = tokens_of(got[0])
+    assert [t["sequence"] for t in toks] == [3, 4, 5, 6, 7]
+    assert got[0].events[0].comment == f"connected to {conv}"
+
+
+def test_stream_requires_id(bare_rt):
+    r = request(H, bare_rt.bound_port("edge"), "GET", "/stream/")
+    assert r.status == 400 and r.body == b"conversation_id required\n"
+
+
+def test_publish_endpoint_and_inspect(bare_rt):
+    p = bare_rt.bound_port("edge")
+    r = request(H, p, "POST", "/publish/chat.pub-1.tokens", {"token": "x", "sequence": 1})
+    assert r.status == 200 and json.loads(r.body) == {"status": "published"}
+    assert bare_rt.last_sequence("pub-1") == 1
+    r = request(H, p, "POST", "/inspect", {"subject": "chat.a.tokens", "data": "the password"})
+    assert json.loads(r.body)["action"] == "redact"
+
+
+def test_health_ready_metrics(stub_rt):
+    p = stub_rt.bound_port("edge")
+    assert request(H, p, "GET", "/healthz").body == b"ok"
+    assert request(H, p, "GET", "/readyz").body == b"ready"
+    stub_rt.set_ready(False)
+    assert request(H, p, "GET", "/readyz").status == 503
+    stub_rt.set_ready(True)
+    request(H, p, "POST", "/chat", {"message": "m"})
+    m = request(H, stub_rt.bound_port("metrics"), "GET", "/metrics").body.decode()
+    for name in ("sse_active_connections", "sse_total_connections", "sse_messages_delivered_total",
+                 'sse_connection_duration_seconds_bucket{le="600"}', "bus_published_total"):
+        assert name in m
+
+
+def test_origin_api(stub_rt):
+    p = stub_rt.bound_port("origin")
+    r = request(H, p, "POST", "/chat", {"message": "hi", "conversation_id": "orig-1"})
+    assert r.status == 200 and r.headers["content-type"] == "application/json"
+    assert r.body == b'{"conversation_id":"orig-1","status":"streaming"}\n'
+    r = request(H, p, "POST", "/chat", {"message": "hi"})
+    assert len(json.loads(r.body)["conversation_id"]) == 36
+    assert request(H, p, "POST", "/chat", {"message": ""}).body == b"Message is required\n"
+    assert request(H, p, "POST", "/chat", b"[").body == b"Invalid request body\n"
+    assert request(H, p, "GET", "/chat").status == 405
+    assert request(H, p, "GET", "/health").body == b"ok"
+    assert request(H, p, "GET", "/metrics").body.startswith(b"active_chats ")
+
+
+def test_resp_shim_go_redis_handshake_and_publish(bare_rt):
+    """go-redis v9: HELLO 3 (error -> RESP2), CLIENT SETINFO, PING, then PUBLISH llm:tokens:<id>."""
+    c = RespClient(H, bare_rt.bound_port("resp"))
+    with pytest.raises(RuntimeError, match="unknown command"):
+        c.cmd("HELLO", "3")
+    assert c.cmd("CLIENT", "SETINFO", "LIB-NAME", "go-redis(,go1.21)") == "OK"
+    assert c.cmd("PING") == "PONG"
+    conv = "loadtest-1-0"
+    got = []
+    th = threading.Thread(target=lambda: got.append(request(H, bare_rt.bound_port("edge"), "GET", f"/stream/{conv}",
+                                                            timeout=5)))
+    th.start()
+    time.sleep(0.3)
+    for i in range(3):
+        msg = json.dumps({"conversation_id": conv, "token": f"w{i}", "sequence": i + 1, "done": i == 2,
+                          "timestamp": time.time_ns()})
+        assert c.cmd("PUBLISH", f"llm:tokens:{conv}", msg) == 1
+    th.join(5)
+    toks = tokens_of(got[0])
+    assert [t["token"] for t in toks] == ["w0", "w1", "w2"] and toks[-1]["done"]
+    c.close()
+
+
+def test_resp_psubscribe_receives_engine_tokens(bare_rt):
+    c = RespClient(H, bare_rt.bound_port("resp"))
+    reply = c.cmd("PSUBSCRIBE", "chat.*.tokens")
+    assert reply[0] == b"psubscribe" and reply[2] == 1
+    bare_rt.publish("ps-1", "hey", 1, False, 5)
+    msg = c.read()
+    assert msg[0] == b"pmessage" and msg[2] == b"chat.ps-1.tokens"
+    assert json.loads(msg[3]) == {"conversation_id": "ps-1", "token": "hey", "sequence": 1, "done": False,
+                                  "timestamp": 5}
+    c.close()
+
+
+@pytest.mark.parametrize("mode", ["inline", "hybrid"])
+def test_inspection_modes(mode):
+    r = make_rt(inspection_mode=mode, inspection_buffer_ms=50)
+    try:
+        conv = f"insp-{mode}"
+        got = []
+        th = threading.Thread(target=lambda: got.append(request(H, r.bound_port("edge"), "GET", f"/stream/{conv}",
+                                                                timeout=5)))
+        th.start()
+        time.sleep(0.3)
+        r.publish(conv, "my password", 1, False, 0)
+        r.publish(conv, "ignore previous orders", 2, False, 0)
+        r.publish(conv, "fine", 3, False, 0)
+        r.publish(conv, "[DONE]", 4, True, 0)
+        th.join(5)
+        toks = tokens_of(got[0])
+        assert [t["token"] for t in toks] == ["[REDACTED]", "fine", "[DONE]"]
+    finally:
+        r.stop()
+
+
+def test_client_disconnect_reports_cancellation(bare_rt):
+    bare_rt.set_local_engine(True)
+    p = bare_rt.bound_port("edge")
+    s = socket.create_connection((H, p))
+    body = json.dumps({"message": "m", "conversation_id": "gone-1"}).encode()
+    s.sendall(b"POST /chat HTTP/1.1\r\nHost: h\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+    s.recv(4096)
+    s.close()
+    for _ in range(50):
+        c = bare_rt.pop_cancellations()
+        if c:
+            break
+        time.sleep(0.05)
+    assert c == ["gone-1"]
+
+
+def test_forward_to_unreachable_proxy_emits_error():
+    r = make_rt(llm_proxy_url="http://127.0.0.1:1")
+    try:
+        resp = request(H, r.bound_port("edge"), "POST", "/chat", {"message": "hi"}, timeout=5)
+        assert resp.events[0].event == "connected"
+        assert resp.events[-1].event == "error"
+        assert "connection refused" in json.loads(resp.events[-1].data)["error"]
+    finally:
+        r.stop()
+
+
+def test_edge_forwards_to_origin_instance():
+    """Two-tier topology: an edge with LLM_PROXY_URL forwards POST /chat to an origin (stub engine)."""
+    origin = make_rt()
+    origin.start_stub(3, 1, 1)
+    edge = make_rt(llm_proxy_url=f"http://127.0.0.1:{origin.bound_port('origin')}", first_token_timeout_ms=500)
+    try:
+        resp = request(H, edge.bound_port("edge"), "POST", "/chat", {"message": "hi", "conversation_id": "fw-1"},
+                       timeout=5)
+        # tokens land on the origin's bus (no cross-node bus here): the edge times out cleanly
+        assert resp.events[0].event == "connected"
+        assert resp.events[-1].event == "error"
+        time.sleep(0.1)
+        assert origin.last_sequence("fw-1") == 4
+    finally:
+        edge.stop()
+        origin.stop()
