@@ -45,10 +45,14 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     args = ap.parse_args()
 
+    from distributed_sse_for_llm_response_amd.engine import bench_harness
+
+    # the SSE client process must be started before this process initialises the GPU
+    client = bench_harness.spawn_client() if args.delivery == "sse" else None
+
     import torch
     import torch.distributed as dist
 
-    from distributed_sse_for_llm_response_amd.engine.bench_harness import run_decode_bench
     from distributed_sse_for_llm_response_amd.parallel.comm import init_distributed
 
     rank, local, world = init_distributed()
@@ -59,9 +63,15 @@ def main():
     if device.type == "cuda":
         torch.cuda.set_device(device)
 
-    res = run_decode_bench(model=args.model, device=device, streams=args.streams, prompt_len=args.prompt_len,
-                           steps=args.steps, warmup=args.warmup, tp=args.tp, delivery=args.delivery,
-                           use_graphs=not args.no_graph, rank=rank, world=world)
+    if client is not None:
+        res = bench_harness.run_serving_bench(client, model=args.model, device=device, streams=args.streams,
+                                              prompt_len=args.prompt_len, steps=args.steps, warmup=args.warmup,
+                                              tp=args.tp, use_graphs=not args.no_graph, rank=rank, world=world)
+    else:
+        res = bench_harness.run_decode_bench(model=args.model, device=device, streams=args.streams,
+                                             prompt_len=args.prompt_len, steps=args.steps, warmup=args.warmup,
+                                             tp=args.tp, delivery=args.delivery, use_graphs=not args.no_graph,
+                                             rank=rank, world=world)
     elapsed = res["elapsed_s"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)

@@ -89,6 +89,7 @@ class Runtime {
       d["top_p"] = r.top_p;
       d["top_k"] = r.top_k;
       d["seed"] = r.seed;
+      d["ignore_eos"] = r.ignore_eos;
       d["from_edge"] = r.from_edge;
       out.append(d);
     }

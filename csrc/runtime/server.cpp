@@ -769,6 +769,10 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
       r.top_p = num("top_p", -1);
       r.top_k = (int)num("top_k", -1);
       r.seed = (int64_t)num("seed", -1);
+      {
+        auto ie = o.find("ignore_eos");
+        r.ignore_eos = ie != o.end() && ie->second.kind == JsonValue::kBool && ie->second.b;
+      }
       srv_.submit_chat(std::move(r));
       write_raw(c, simple_response(200, "{\"conversation_id\":" + json_quote(conv) + ",\"status\":\"streaming\"}\n",
                                    "application/json", ka));
@@ -840,6 +844,10 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
       r.top_p = num("top_p", -1);
       r.top_k = (int)num("top_k", -1);
       r.seed = (int64_t)num("seed", -1);
+      {
+        auto ie = o.find("ignore_eos");
+        r.ignore_eos = ie != o.end() && ie->second.kind == JsonValue::kBool && ie->second.b;
+      }
       r.from_edge = true;
       srv_.submit_chat(std::move(r));
     } else {

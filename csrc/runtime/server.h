@@ -65,6 +65,7 @@ struct ChatRequest {
   double top_p = -1;
   int top_k = -1;
   int64_t seed = -1;
+  bool ignore_eos = false;
   bool from_edge = false;    // submitted by the edge /chat (a subscriber exists)
 };
 

@@ -139,6 +139,97 @@ def run_decode_bench(model="mistral-7b-v0.3", device=None, streams=64, prompt_le
             "p99_itl_ms": float(np.percentile(itl, 99)), "frames_bytes": frames_bytes, "model": cfg.name}
 
 
+def spawn_client():
+    """Start the SSE client process (call BEFORE the GPU is initialised in this process)."""
+    import subprocess
+    import sys
+
+    return subprocess.Popen([sys.executable, "-m", "distributed_sse_for_llm_response_amd.engine.bench_client"],
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+
+
+def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, prompt_len=512, steps=64, warmup=8,
+                      tp=1, use_graphs=True, rank=0, world=1, seed=0):
+    """Full serving path: `streams` real POST /chat SSE connections (client process) -> native runtime
+    -> LLMEngine (scheduler, hipGraph decode, token-ring drain) -> bus -> epoll writers -> sockets.
+
+    Timed: exactly `steps` engine steps once every stream is decoding.  The p50 inter-token latency is
+    measured by the client (socket receive times of consecutive tokens of a stream) inside the timed
+    window."""
+    import json as _json
+
+    from .. import runtime as rt_mod
+    from ..models.tokenizer import SyntheticTokenizer
+    from .engine import LLMEngine, SamplingParams
+
+    device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    total = steps + warmup
+    cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
+    if use_graphs and device.type == "cuda":
+        r.capture()
+    tok = SyntheticTokenizer(cfg.vocab_size)
+    engine = LLMEngine(r, eos_id=tok.eos_id, prefill_budget=r.max_prefill_tokens,
+                       default_params=SamplingParams(temperature=1.0, top_p=1.0, max_tokens=total + 2))
+    mod = rt_mod.load()
+    runtime = mod.Runtime({"host": "127.0.0.1", "sse_port": 0, "origin_port": -1, "metrics_port": -1, "resp_port": -1,
+                           "io_threads": 4, "local_engine": True})
+    runtime.set_vocab(tok.pieces())
+    runtime.start()
+    words = [f"w{i % 997}" for i in range(max(1, prompt_len - 8))]
+    client.stdin.write(_json.dumps({"host": "127.0.0.1", "port": runtime.bound_port("edge"), "streams": streams,
+                                    "message": " ".join(words), "max_tokens": total + 2, "rank": rank}) + "\n")
+    client.stdin.flush()
+
+    def publish(events):
+        if events:
+            runtime.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
+                                   [e.sequence for e in events], [e.done for e in events], 0,
+                                   [e.text for e in events])
+
+    def pump(block_ms=0):
+        for req in runtime.poll_requests(1024, block_ms):
+            p = SamplingParams(temperature=1.0, top_p=1.0, max_tokens=req["max_tokens"], ignore_eos=True)
+            engine.add_request(req["conversation_id"], tok.chat_prompt(req["message"]), p,
+                               arrival_ns=req["arrival_ns"])
+
+    # admission + prefill until every stream is decoding
+    t_admit = time.time()
+    while sum(1 for s in engine.slots if s is not None and s.state == "decode") < streams:
+        pump(20 if not engine.has_work() else 0)
+        if engine.has_work():
+            publish(engine.step())
+        if time.time() - t_admit > 600:
+            raise RuntimeError("bench: streams did not all start decoding")
+    for _ in range(warmup):
+        publish(engine.step())
+    _sync(device, world)
+    t0_ns = time.time_ns()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        publish(engine.step())
+    _sync(device, world)
+    elapsed = time.perf_counter() - t0
+    t1_ns = time.time_ns()
+    while engine.has_work():
+        publish(engine.step())
+    out = client.stdout.readline()
+    client.wait(timeout=120)
+    runtime.stop()
+    res = _json.loads(out) if out.strip() else {"arrivals": [], "errors": ["client produced no output"]}
+    by_stream = {}
+    for s, seq, t_ns, _ts in res["arrivals"]:
+        by_stream.setdefault(s, []).append(t_ns)
+    gaps = []
+    for ts in by_stream.values():
+        ts.sort()
+        gaps += [(b - a) / 1e6 for a, b in zip(ts, ts[1:]) if t0_ns <= a and b <= t1_ns]
+    delivered = sum(1 for _s, _q, t_ns, _ in res["arrivals"] if t0_ns <= t_ns <= t1_ns)
+    itl = np.array(gaps) if gaps else np.array([elapsed * 1000.0 / max(1, steps)])
+    return {"elapsed_s": elapsed, "p50_itl_ms": float(np.percentile(itl, 50)),
+            "p99_itl_ms": float(np.percentile(itl, 99)), "delivered_in_window": delivered,
+            "client_errors": res["errors"][:5], "model": cfg.name}
+
+
 def _sync(device, world):
     if device.type == "cuda":
         torch.cuda.synchronize(device)

@@ -78,7 +78,7 @@ class EngineLoop(threading.Thread):
             top_p=req["top_p"] if 0 < req["top_p"] <= 1 else d.top_p,
             top_k=req["top_k"] if req["top_k"] > 0 else d.top_k,
             max_tokens=req["max_tokens"] if req["max_tokens"] > 0 else d.max_tokens,
-            seed=req["seed"] if req["seed"] >= 0 else None)
+            seed=req["seed"] if req["seed"] >= 0 else None, ignore_eos=bool(req.get("ignore_eos", False)))
 
     def publish(self, events):
         if not events:
