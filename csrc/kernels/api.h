@@ -9,6 +9,12 @@ constexpr int kBS = 32;  // KV-cache page size in tokens (fixed for every kernel
 
 enum GemmMode { kStoreBf16 = 0, kStoreF32 = 1, kResidAdd = 2, kSiluMul = 3, kQkvRope = 4 };
 
+// Decode-GEMM weight layout ("tiled"): W[N, K] is stored as blocks of (16-row tile T, 128-column
+// K-chunk c), block-major (T, c), each block [s = 0..3][lane = 0..63][j = 0..7] where lane l = r + 16g
+// holds W[16T + r][128c + 32g + 8s + j] — exactly the MFMA B-operand fragment of k-step s.  A wave
+// therefore loads every block as four fully contiguous 1 KiB runs (see ops/reference.py tile_weight).
+constexpr int kTileChunk = 16 * 128;  // elements per (tile, chunk) block
+
 struct GemmEpi {
   void* out;          // bf16 / f32 output (modes 0, 1, 3)
   int ldo;
@@ -69,12 +75,17 @@ hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int
                             const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
 hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx, int M,
                           const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
+hipError_t dsse_gemm_xlds_partial(int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx, int M,
+                                  const void* W, int K, int N, float* part, hipStream_t st);
+hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int S, int partial_only, const void* X, int ldx, int M,
+                            const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);
 hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::SampleParams* p,
                             hipStream_t st);
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
-                        const int* ids, const void* w, void* y, float eps, hipStream_t st);
+                        const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
+                        hipStream_t st);
 hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                               const int* slots, const float2* rope, void* q_out, void* k_cache,
                               void* v_cache, hipStream_t st);

@@ -79,18 +79,53 @@ XCfg pick_xlds(int M, int N, int K) {
   c.S = (K + ks - 1) / ks;
   const int TG = N / (16 * c.nt);
   int tg = env_int("DSSE_X_TG", 0);
+  if (tg == -1) tg = (TG * c.S + 255) / 256;  // exactly one workgroup per CU
   if (tg <= 0) tg = std::max(c.nw, (TG * c.S / 224 / c.nw) * c.nw);
   c.tg = std::min(tg, TG);
   return c;
 }
 
-// Register-streaming kernel for tiny batches (X re-reads are cheap), X-in-LDS kernel above.
-bool use_xlds(int M, int N, int K) {
+// X-streaming kernel configuration (gemm_stream.hip).  Env overrides: DSSE_S_NT, DSSE_S_NW, DSSE_S_SPLIT.
+struct SCfg {
+  int mt, nt, nw, S;
+  bool ok;
+};
+SCfg pick_stream(int M, int N, int K) {
+  SCfg c{};
+  c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  c.nt = env_int("DSSE_S_NT", 1);
+  c.nw = env_int("DSSE_S_NW", 8);
+  if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
+  c.ok = K % 512 == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
+  if (!c.ok) return c;
+  const int wgs = N / (16 * c.nt) / c.nw, slices = K / 512;
+  int S = env_int("DSSE_S_SPLIT", 0);
+  if (S <= 0 || slices % S != 0) {
+    // smallest split that gives ~one workgroup per CU (256 CUs), never more than 320 workgroups
+    S = 1;
+    for (int d = 1; d <= slices; ++d) {
+      if (slices % d) continue;
+      if (wgs * d > 320) break;
+      S = d;
+      if (wgs * d >= 192) break;
+    }
+  }
+  c.S = S;
+  return c;
+}
+
+// 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
+// whole K-slice staged (gemm_xlds.hip), 2 = X streamed through LDS slices (gemm_stream.hip).
+// DSSE_GEMM_IMPL forces one.
+int gemm_impl(int M, int N, int K) {
   const int impl = env_int("DSSE_GEMM_IMPL", -1);
-  if (impl >= 0) return impl == 1;
-  if (M <= 8) return false;
-  if (M <= 16) return N >= 16384;
-  return true;
+  if (impl >= 0) {
+    if (impl == 2 && !pick_stream(M, N, K).ok) return 1;
+    return impl;
+  }
+  if (M <= 8) return 0;
+  if (M <= 16 && N < 16384) return 0;
+  return pick_stream(M, N, K).ok ? 2 : 1;
 }
 
 void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
@@ -104,7 +139,16 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(M >= 1 && M <= 64, "decode GEMM supports 1 <= M <= 64, got ", M);
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
-  if (use_xlds(M, N, K)) {
+  const int impl = gemm_impl(M, N, K);
+  if (impl == 2) {
+    const SCfg c = pick_stream(M, N, K);
+    at::Tensor part;
+    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
+    DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                    c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    return;
+  }
+  if (impl == 1) {
     XCfg c = pick_xlds(M, N, K);
     if (N % (16 * c.nt) != 0) c.nt = 1;
     at::Tensor part;
@@ -142,6 +186,42 @@ void gemm_resid(const Tensor& x, const Tensor& w, Tensor& resid) {
   ep.resid = resid.data_ptr<float>();
   ep.ldr = (int)resid.size(1);
   run_gemm(dsse::kResidAdd, x, w, ep);
+}
+
+// Residual projection whose split-K reduction is left to the consuming RMSNorm (rmsnorm with `part`).
+// Returns S > 0 when fp32 partial slabs [S, M, N] were written to `part` (resid untouched), or 0 when
+// the product was already added into `resid` (single K-slice or register-streaming kernel).
+int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor& part) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(part, "part");
+  check_dtype(part, at::kFloat, "part");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const bool shape_ok = M >= 1 && M <= 64 && K % 128 == 0 && N % 16 == 0 && w.size(1) == K;
+  const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
+  if (impl == 2) {
+    const SCfg c = pick_stream(M, N, K);
+    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      dsse::GemmEpi ep{};
+      DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kResidAdd, c.mt, c.nt, c.nw, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N,
+                                      &ep, part.data_ptr<float>(), cur_stream()));
+      return c.S;
+    }
+  } else if (impl == 1) {
+    XCfg c = pick_xlds(M, N, K);
+    if (N % (16 * c.nt) != 0) c.nt = 1;
+    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      DSSE_CHECK_HIP(dsse_gemm_xlds_partial(c.mt, c.nt, c.nw, c.depth, c.ks, c.tg, x.data_ptr(), K, M, w.data_ptr(), K,
+                                            N, part.data_ptr<float>(), cur_stream()));
+      return c.S;
+    }
+  }
+  gemm_resid(x, w, resid);
+  return 0;
 }
 
 void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out) {
@@ -187,7 +267,8 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
 }
 
 void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
-             const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids) {
+             const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids,
+             const c10::optional<Tensor>& part, int64_t nsplit) {
   check_gpu(resid, "resid");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -217,8 +298,16 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     mode = 1;
     dptr = delta->data_ptr();
   }
+  const float* pptr = nullptr;
+  if (part.has_value() && nsplit > 0 && mode == 0) {
+    check_gpu(*part, "part");
+    check_dtype(*part, at::kFloat, "part");
+    TORCH_CHECK(part->numel() >= nsplit * M * H, "part too small for ", nsplit, " slabs");
+    mode = 3;
+    pptr = part->data_ptr<float>();
+  }
   DSSE_CHECK_HIP(dsse_rmsnorm(mode, M, resid.data_ptr<float>(), H, dptr, eptr, iptr, w.data_ptr(),
-                              y.data_ptr(), (float)eps, cur_stream()));
+                              y.data_ptr(), (float)eps, pptr, (int)nsplit, cur_stream()));
 }
 
 void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& rope,
@@ -398,7 +487,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 2; }
+int64_t kernels_abi_version() { return 3; }
 
 }  // namespace
 
@@ -409,7 +498,8 @@ TORCH_LIBRARY(dsse, m) {
   m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
-        "Tensor? ids=None) -> ()");
+        "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
+  m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("silu_mul(Tensor gu, Tensor(a!) h) -> ()");
@@ -429,6 +519,7 @@ TORCH_LIBRARY(dsse, m) {
 TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("gemm_out", &gemm_out);
   m.impl("gemm_resid", &gemm_resid);
+  m.impl("gemm_resid_split", &gemm_resid_split);
   m.impl("gemm_silu", &gemm_silu);
   m.impl("gemm_qkv_rope", &gemm_qkv_rope);
   m.impl("rmsnorm", &rmsnorm);

@@ -14,11 +14,14 @@ DEV int vperm_tok(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4
 // MODE 2: resid = embed[ids[m]]; y = rmsnorm(resid)
 // The residual stream is fp32 [M, H]; y is the bf16 input of the next GEMM.
 // One 256-thread workgroup per row; each thread keeps its H/256 values in registers.
+// MODE 3: resid += sum_s part[s, m, :] (fp32 split-K slabs of the O / down projection, fusing the
+//         split-K reduction into the norm that consumes it); y = rmsnorm(resid)
 template <int MODE>
 __global__ void __launch_bounds__(256)
 rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
                const bf16* __restrict__ embed, const int* __restrict__ ids,
-               const bf16* __restrict__ w, bf16* __restrict__ y, float eps) {
+               const bf16* __restrict__ w, bf16* __restrict__ y, float eps,
+               const float* __restrict__ part = nullptr, int nsplit = 0, int M = 0) {
   const int m = blockIdx.x, tid = threadIdx.x;
   float* rrow = resid + (size_t)m * H;
   constexpr int kMaxIt = 8;  // H <= 8192
@@ -38,6 +41,12 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
         if constexpr (MODE == 1) {
           const bf16x4 d = *reinterpret_cast<const bf16x4*>(delta + (size_t)m * H + i);
           x.x += bf2f(d[0]); x.y += bf2f(d[1]); x.z += bf2f(d[2]); x.w += bf2f(d[3]);
+        }
+        if constexpr (MODE == 3) {
+          for (int s = 0; s < nsplit; ++s) {
+            const float4 d = *reinterpret_cast<const float4*>(part + ((size_t)s * M + m) * H + i);
+            x.x += d.x; x.y += d.y; x.z += d.z; x.w += d.w;
+          }
         }
       }
       if constexpr (MODE != 0) *reinterpret_cast<float4*>(rrow + i) = x;
@@ -152,16 +161,17 @@ using namespace dsse;
 
 extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta,
                                    const void* embed, const int* ids, const void* w, void* y,
-                                   float eps, hipStream_t st) {
+                                   float eps, const float* part, int nsplit, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   const bf16* d = reinterpret_cast<const bf16*>(delta);
   const bf16* e = reinterpret_cast<const bf16*>(embed);
   const bf16* wp = reinterpret_cast<const bf16*>(w);
   bf16* yp = reinterpret_cast<bf16*>(y);
   switch (mode) {
-    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
-    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
-    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps); break;
+    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

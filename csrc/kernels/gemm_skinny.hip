@@ -34,7 +34,7 @@ DEV void load_chunk(bf16x8 (&wf)[NT][4], bf16x8 (&xf)[MT][4], const bf16* const 
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) wf[t][s] = ld_bf16x8(wp[t] + off + 8 * s);
+    for (int s = 0; s < 4; ++s) wf[t][s] = ld_bf16x8(wp[t] + (size_t)c * kTileChunk + 512 * s);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -68,7 +68,7 @@ skinny_gemm_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 
   const bf16* wp[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wp[t] = W + (size_t)(n0 + 16 * t + r) * K + 32 * g;
+  for (int t = 0; t < NT; ++t) wp[t] = W + (size_t)((n0 >> 4) + t) * (K >> 7) * kTileChunk + lane * 8;
   const bf16* xp[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {

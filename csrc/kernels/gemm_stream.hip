@@ -1,0 +1,183 @@
+// X-streaming decode GEMM:  Y[M, N] = X[M, K] · W[N, K]ᵀ, 16 < M <= 64 (any M <= 64 works).
+//
+// Successor of gemm_xlds.hip for the batched decode step.  gemm_xlds stages a whole K-slice of X
+// (up to 128 KiB) into LDS before its waves start streaming weights, and splits K across
+// workgroups to bound that slice: measured on MI355X (profiles/gemm_sweep_r1.md) the prologue
+// (~5 µs per workgroup at ≈11 B/clk/CU) plus the fp32 split-K slabs cost 25-40 % at M = 64.
+//
+// Here a workgroup of NW waves owns NW tile-groups (NT tiles of 16 output columns each, one per
+// wave, accumulators live for the whole K range) and X flows through two LDS slices of CPS·128
+// columns: while the waves multiply slice i, every thread has already issued the global loads of
+// slice i+1 into registers and writes them to the other buffer after its last MFMA — one barrier per
+// slice and no prologue beyond the first (small) slice.  Weights stream HBM -> VGPRs from the tiled
+// layout (api.h kTileChunk: 4 contiguous KiB per (tile, K-chunk)) through a CPS-deep register ring
+// that runs across slice boundaries.  Split-K (grid.y = S) is only used when N is too narrow to give
+// ~one workgroup per CU (O / down / QKV projections); then fp32 slabs [S, M, N] go to `part`.
+//
+// Rows m >= M of the X slices are never written; their MFMA rows produce garbage that is never
+// stored (MFMA output rows depend only on the same A row).
+#include "gemm_epilogue.h"
+
+namespace dsse {
+
+constexpr int kStreamCPS = 4;  // K-chunks of 128 per LDS slice
+
+template <int MT, int NT, int NW, int MODE>
+__global__ void __launch_bounds__(64 * NW)
+gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
+                   int Kr, GemmEpi ep, float* __restrict__ part) {
+  constexpr int CPS = kStreamCPS;
+  constexpr int MP = 16 * MT;
+  constexpr int ROWB = CPS * 256;                        // bytes of one X row in a slice
+  constexpr int BUF = MP * ROWB;                         // bytes per slice buffer
+  constexpr int PPT = (MP * CPS * 16 + 64 * NW - 1) / (64 * NW);  // 16-byte pieces per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int tgi = blockIdx.x * NW + w;  // host guarantees N / (16 NT) % NW == 0: every wave is busy
+  const int ks = blockIdx.y;
+  const int k0 = ks * Kr;
+  const int nch = Kr >> 7;   // multiple of CPS (host-checked)
+  const int nsl = nch / CPS;
+  const int npieces = min(M, MP) * CPS * 16;
+  const int KC = K >> 7;
+
+  const bf16* wbase = W + ((size_t)tgi * NT * KC + (k0 >> 7)) * kTileChunk + lane * 8;
+  auto load_w = [&](int c, bf16x8 (&wf)[NT][4]) {
+    const bf16* p = wbase + (size_t)min(c, nch - 1) * kTileChunk;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#if DSSE_W_NT
+        wf[t][s] = ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
+#else
+        wf[t][s] = ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
+#endif
+      }
+  };
+
+  bf16x8 xs[PPT];
+  auto load_x = [&](int sl) {
+    const bf16* src = X + k0 + sl * (CPS * 128);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int idx = threadIdx.x + i * 64 * NW;
+      if (idx < npieces) xs[i] = ld_bf16x8(src + (size_t)(idx / (CPS * 16)) * ldx + 8 * (idx % (CPS * 16)));
+    }
+  };
+  auto store_x = [&](int buf) {
+    char* dst = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int idx = threadIdx.x + i * 64 * NW;
+      if (idx < npieces) {
+        const int row = idx / (CPS * 16), c = idx % (CPS * 16);
+        *reinterpret_cast<bf16x8*>(dst + row * ROWB + ((c >> 4) << 8) + (((c & 15) ^ swz(row & 15)) << 4)) = xs[i];
+      }
+    }
+  };
+
+  bf16x8 ring[CPS][NT][4];
+#pragma unroll
+  for (int d = 0; d < CPS - 1; ++d) load_w(d, ring[d]);
+  load_x(0);
+  store_x(0);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int sl = 0; sl < nsl; ++sl) {
+    __syncthreads();  // slice sl visible; everyone is done reading slice sl - 1's buffer
+    const bool more = sl + 1 < nsl;
+    if (more) load_x(sl + 1);
+    const char* xb0 = smem + (sl & 1) * BUF;
+#pragma unroll
+    for (int d = 0; d < CPS; ++d) {
+      load_w(sl * CPS + d + CPS - 1, ring[(d + CPS - 1) % CPS]);
+      const char* xb = xb0 + (d << 8);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ch = ((4 * g + s) ^ swz(r)) << 4;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf, ring[d][t][s], acc[mt][t]);
+        }
+      }
+    }
+    if (more) store_x((sl + 1) & 1);
+  }
+
+  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = acc[mt][t][i];
+        const float partner = (MODE == kSiluMul || MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
+        epilogue<MODE>(ep, part_ks, M, N, 16 * mt + 4 * g + i, tgi * NT + t, r, v, partner);
+      }
+}
+
+template <int MT, int NT, int NW, int MODE>
+static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
+                           float* part, hipStream_t st) {
+  const int TG = N / (16 * NT);
+  const size_t lds = (size_t)2 * 16 * MT * kStreamCPS * 256;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, MODE>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  dim3 grid(TG / NW, S), block(64 * NW);
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep,
+                     part);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_s_mode(int mt, int nt, int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
+                                int S, const GemmEpi& ep, float* part, hipStream_t st) {
+#define DSSE_S_CASE(MT_, NT_, NW_) \
+  if (mt == MT_ && nt == NT_ && nw == NW_) return launch_s<MT_, NT_, NW_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+#define DSSE_S_MT(MT_) DSSE_S_CASE(MT_, 1, 8) DSSE_S_CASE(MT_, 2, 8) DSSE_S_CASE(MT_, 1, 4)
+  DSSE_S_MT(1) DSSE_S_MT(2) DSSE_S_MT(4)
+#undef DSSE_S_MT
+#undef DSSE_S_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace dsse
+
+// Shape contract (checked by the caller): K % (512 S) == 0, (N / (16 nt)) % nw == 0, M <= 16 mt <= 64.
+// part: fp32 [S, M, N] workspace when S > 1.  partial_only: leave the slabs for the consumer (the fused
+// residual + RMSNorm kernel) instead of reducing them here.
+extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int S, int partial_only, const void* X,
+                                       int ldx, int M, const void* W, int K, int N, const dsse::GemmEpi* ep,
+                                       float* part, hipStream_t st) {
+  using namespace dsse;
+  const bf16* x = reinterpret_cast<const bf16*>(X);
+  const bf16* w = reinterpret_cast<const bf16*>(W);
+  if (S == 1) {
+    switch (mode) {
+      case kStoreBf16: return launch_s_mode<kStoreBf16>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_s_mode<kStoreF32>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_s_mode<kResidAdd>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_s_mode<kSiluMul>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_s_mode<kQkvRope>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+    }
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = launch_s_mode<kPartial>(mt, nt, nw, x, ldx, M, w, K, N, S, *ep, part, st);
+  if (e != hipSuccess || partial_only) return e;
+  return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
+}

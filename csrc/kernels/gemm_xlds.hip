@@ -15,57 +15,9 @@
 //   S == 1: the fused epilogue of gemm_skinny.hip (bf16 / fp32 / residual add / SiLU·mul /
 //   RoPE + paged KV write) runs in the workgroup; S > 1: fp32 partials [S, M, N] are reduced by
 //   splitk_reduce_kernel, which applies the same epilogue.
-#include "api.h"
+#include "gemm_epilogue.h"
 
 namespace dsse {
-
-constexpr int kPartial = 5;  // internal mode: write fp32 split-K partial slabs
-
-DEV int vperm2(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4 + (off & 3); }
-
-// 16-byte chunk swizzle inside each 256-byte window of an LDS row: conflict-free ds_read_b128 for
-// the MFMA A-operand pattern (lane l reads row l & 15, chunk 4(l >> 4) + s).
-DEV int swz(int row) { return row ^ ((((row >> 2) ^ (row >> 3)) & 1) << 2); }
-
-// One output element with its epilogue.  `partner` = the value 8 lanes away (same row, paired column).
-template <int MODE>
-DEV void epilogue(const GemmEpi& ep, float* part, int M, int N, int m, int tile, int r, float v, float partner) {
-  if (m >= M) return;
-  const int n = tile * 16 + r;
-  if constexpr (MODE == kStoreBf16) {
-    reinterpret_cast<bf16*>(ep.out)[(size_t)m * ep.ldo + n] = f2bf(v);
-  } else if constexpr (MODE == kStoreF32) {
-    reinterpret_cast<float*>(ep.out)[(size_t)m * ep.ldo + n] = v;
-  } else if constexpr (MODE == kResidAdd) {
-    ep.resid[(size_t)m * ep.ldr + n] += v;
-  } else if constexpr (MODE == kSiluMul) {
-    if (r < 8) reinterpret_cast<bf16*>(ep.out)[(size_t)m * ep.ldo + tile * 8 + r] = f2bf(silu(v) * partner);
-  } else if constexpr (MODE == kQkvRope) {
-    const int unit = tile >> 3, j = tile & 7;
-    const int d = (r < 8) ? (8 * j + r) : (64 + 8 * j + (r - 8));
-    if (unit < ep.nh + ep.nkv) {
-      const float2 cs = ep.rope[(size_t)ep.positions[m] * 64 + 8 * j + (r & 7)];
-      const float rot = (r < 8) ? (v * cs.x - partner * cs.y) : (v * cs.x + partner * cs.y);
-      if (unit < ep.nh) {
-        ep.q_out[(size_t)m * ep.nh * 128 + unit * 128 + d] = f2bf(rot);
-      } else {
-        const int s = ep.slots[m];
-        if (s >= 0) {
-          const int h = unit - ep.nh, blk = s / kBS, off = s % kBS;
-          ep.k_cache[(((size_t)blk * ep.nkv + h) * kBS + off) * 128 + d] = f2bf(rot);
-        }
-      }
-    } else {
-      const int s = ep.slots[m];
-      if (s >= 0) {
-        const int h = unit - ep.nh - ep.nkv, blk = s / kBS, off = s % kBS;
-        ep.v_cache[(((size_t)blk * ep.nkv + h) * 128 + d) * kBS + vperm2(off)] = f2bf(v);
-      }
-    }
-  } else {  // kPartial: part[(ks, m, n)]
-    part[(size_t)m * N + n] = v;
-  }
-}
 
 template <int MT, int NT, int NW, int DEPTH, int MODE>
 __global__ void __launch_bounds__(64 * NW)
@@ -93,11 +45,19 @@ gemm_xlds_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   auto load_unit = [&](int u, bf16x8 (&wf)[NT][4]) {
     const int uu = min(u, U - 1);
     const int tg = my_first + (uu / cpt) * NW, c = uu % cpt;
-    const bf16* base = W + (size_t)(tg * 16 * NT + r) * K + k0 + (c << 7) + 32 * g;
+    // tiled weights: the 4 KiB block of (16-row tile, K-chunk) is contiguous and each of the four
+    // loads below reads one contiguous 1 KiB of it across the wave
+    const bf16* base = W + ((size_t)(tg * NT) * (K >> 7) + (k0 >> 7) + c) * kTileChunk + lane * 8;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) wf[t][s] = ld_bf16x8(base + (size_t)16 * t * K + 8 * s);
+      for (int s = 0; s < 4; ++s) {
+#if DSSE_W_NT
+        wf[t][s] = ld_nt_bf16x8(base + (size_t)t * (K >> 7) * kTileChunk + 512 * s);
+#else
+        wf[t][s] = ld_bf16x8(base + (size_t)t * (K >> 7) * kTileChunk + 512 * s);
+#endif
+      }
   };
 
   // Weight ring: DEPTH chunks of 4 x 16 B per lane per tile.  The first DEPTH-1 loads are issued
@@ -166,25 +126,6 @@ gemm_xlds_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   }
 }
 
-// Sum the S partial slabs and apply the epilogue.  One thread per (row, 16-column tile, j < 8):
-// it owns columns tile*16 + j and tile*16 + 8 + j (the epilogue partners).
-template <int MODE>
-__global__ void __launch_bounds__(256)
-splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, GemmEpi ep) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int tiles = N / 16;
-  if (idx >= M * tiles * 8) return;
-  const int j = idx & 7, tile = (idx >> 3) % tiles, m = (idx >> 3) / tiles;
-  const size_t base = (size_t)m * N + tile * 16 + j;
-  float a = 0.f, b = 0.f;
-  for (int s = 0; s < S; ++s) {
-    a += part[(size_t)s * M * N + base];
-    b += part[(size_t)s * M * N + base + 8];
-  }
-  epilogue<MODE>(ep, nullptr, M, N, m, tile, j, a, b);
-  epilogue<MODE>(ep, nullptr, M, N, m, tile, j + 8, b, a);
-}
-
 template <int MT, int NT, int NW, int DEPTH, int MODE>
 static hipError_t launch_x(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int Ks, int tg,
                            const GemmEpi& ep, float* part, hipStream_t st) {
@@ -220,6 +161,16 @@ static hipError_t launch_x_mode(int mt, int nt, int nw, int depth, const bf16* X
 
 }  // namespace dsse
 
+// Split-K partial slabs only (no reduce): part[S, M, N]; the consumer (e.g. the fused
+// residual-add + RMSNorm kernel) performs the reduction.
+extern "C" hipError_t dsse_gemm_xlds_partial(int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx,
+                                             int M, const void* W, int K, int N, float* part, hipStream_t st) {
+  using namespace dsse;
+  GemmEpi ep{};
+  return launch_x_mode<kPartial>(mt, nt, nw, depth, reinterpret_cast<const bf16*>(X), ldx, M,
+                                 reinterpret_cast<const bf16*>(W), K, N, Ks, tg, ep, part, st);
+}
+
 // X-in-LDS decode GEMM.  part: fp32 workspace of S * M * N floats when Ks < K (S > 1), else unused.
 extern "C" hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx,
                                      int M, const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
@@ -240,15 +191,5 @@ extern "C" hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth
   }
   hipError_t e = launch_x_mode<kPartial>(mt, nt, nw, depth, x, ldx, M, w, K, N, Ks, tg, *ep, part, st);
   if (e != hipSuccess) return e;
-  const int threads = M * (N / 16) * 8;
-  const dim3 grid((threads + 255) / 256), block(256);
-  switch (mode) {
-    case kStoreBf16: hipLaunchKernelGGL(splitk_reduce_kernel<kStoreBf16>, grid, block, 0, st, part, S, M, N, *ep); break;
-    case kStoreF32: hipLaunchKernelGGL(splitk_reduce_kernel<kStoreF32>, grid, block, 0, st, part, S, M, N, *ep); break;
-    case kResidAdd: hipLaunchKernelGGL(splitk_reduce_kernel<kResidAdd>, grid, block, 0, st, part, S, M, N, *ep); break;
-    case kSiluMul: hipLaunchKernelGGL(splitk_reduce_kernel<kSiluMul>, grid, block, 0, st, part, S, M, N, *ep); break;
-    case kQkvRope: hipLaunchKernelGGL(splitk_reduce_kernel<kQkvRope>, grid, block, 0, st, part, S, M, N, *ep); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+  return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

@@ -68,15 +68,24 @@ def _parallel(jobs, verbose):
             f.result()
 
 
-def build_kernels(verbose: bool = False, force: bool = False) -> Path:
+KERNEL_VARIANTS = {"nt": ["-DDSSE_W_NT=1"]}  # experiment builds: libdsse_kernels_<variant>.so
+
+
+def kernels_so(variant: str | None = None) -> Path:
+    return LIB_DIR / (f"libdsse_kernels_{variant}.so" if variant else "libdsse_kernels.so")
+
+
+def build_kernels(verbose: bool = False, force: bool = False, variant: str | None = None) -> Path:
     """Compile csrc/kernels into _lib/libdsse_kernels.so (gfx950 code objects + torch ops)."""
     inc, api_inc, torch_lib, abi = _torch_paths()
     kdir = CSRC / "kernels"
-    obj_dir = BUILD_DIR / "kernels"
+    obj_dir = BUILD_DIR / ("kernels" + (f"_{variant}" if variant else ""))
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
     headers = sorted(kdir.glob("*.h"))
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-unused-result"]
+    common += KERNEL_VARIANTS.get(variant, [])
+    out_so = kernels_so(variant)
     jobs, objs = [], []
     for src in sorted(kdir.glob("*.hip")):
         obj = obj_dir / (src.stem + ".o")
@@ -92,13 +101,13 @@ def build_kernels(verbose: bool = False, force: bool = False) -> Path:
             "-I", inc, "-I", api_inc, "-c", bsrc, "-o", bobj,
         ])
     _parallel(jobs, verbose)
-    if force or _stale(KERNELS_SO, objs):
+    if force or _stale(out_so, objs):
         _run([
-            HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", KERNELS_SO,
+            HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out_so,
             "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             f"-Wl,-rpath,{torch_lib}",
         ], verbose)
-    return KERNELS_SO
+    return out_so
 
 
 def _py_ext_suffix() -> str:
@@ -168,6 +177,8 @@ if __name__ == "__main__":
     force = "--force" in sys.argv
     if what == "kernels":
         build_kernels(True, force)
+    elif what.startswith("kernels-"):
+        build_kernels(True, force, variant=what.split("-", 1)[1])
     elif what == "runtime":
         build_runtime(True, force)
     elif what.startswith("runtime-"):

@@ -106,6 +106,8 @@ class ModelRunner:
         self.attn = torch.zeros(Bm, nh * 128, **bf)
         self.h = torch.zeros(Bm, F, **bf)
         self.tmp = torch.zeros(Bm, H, **bf)
+        # fp32 split-K slabs of the residual projections (reduced inside the next RMSNorm)
+        self.split_part = torch.zeros(32 * Bm * H, device=dev, dtype=torch.float32)
         self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
         nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
         self._cand = {b: torch.zeros(b, nch, 2, device=dev, dtype=torch.float32) for b in batch_buckets(Bm)}
@@ -134,28 +136,28 @@ class ModelRunner:
         a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
         for li, L in enumerate(w.layers):
-            ops.gemm_qkv_rope(x, L.wqkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+            ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
                               self.kv.v[li], nh, nkv)
             ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
                                 self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
                                 self.part_ml, part, nparts)
             if comm.size == 1:
-                ops.gemm_resid(self.attn[r], L.wo, resid)
-                ops.rmsnorm(resid, L.ffn_norm, x, eps)
+                ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
+                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
             else:
-                ops.gemm_out(self.attn[r], L.wo, self.tmp[r])
+                ops.gemm_out(self.attn[r], L.wo_t, self.tmp[r])
                 comm.all_reduce(self.tmp[r])
                 ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=self.tmp[r])
-            ops.gemm_silu(x, L.wgu, self.h[r])
+            ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             if comm.size == 1:
-                ops.gemm_resid(self.h[r], L.wd, resid)
-                ops.rmsnorm(resid, w_next, x, eps)
+                ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
+                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
             else:
-                ops.gemm_out(self.h[r], L.wd, self.tmp[r])
+                ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
                 comm.all_reduce(self.tmp[r])
                 ops.rmsnorm(resid, w_next, x, eps, delta=self.tmp[r])
-        ops.gemm_out(x, w.lm_head, self.logits[r])
+        ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
 
@@ -293,7 +295,7 @@ class ModelRunner:
         if logits is None:
             logits = torch.empty(len(last), w.vocab_local, **f32)
             if len(last) <= 64:
-                ops.gemm_out(xl, w.lm_head, logits)
+                ops.gemm_out(xl, w.lm_head_t, logits)
             else:
                 logits = (xl @ w.lm_head.t()).float()
         slot_idx = torch.tensor([seqs[i].slot for i in last], dtype=torch.long, device=dev)

@@ -12,7 +12,11 @@ The decode kernels want, per rank (t = TP degree, r = rank):
 * ``lm_head`` [V/t, H]                 — vocab-parallel; the sampler merges per-rank candidates.
 * ``embed`` [V, H] replicated (256 MiB; HBM is plentiful, and it avoids an all-reduce per step).
 
-All matrices are row-major [out, in] bf16 and contiguous, which is what the skinny GEMM streams.
+All matrices are row-major [out, in] bf16 and contiguous (the layout the prefill GEMMs — hipBLASLt via
+``torch.matmul`` — consume).  The decode GEMMs stream a second copy of each matrix in the tiled layout
+of :func:`ops.reference.tile_weight` (``*_t`` fields, made by :func:`attach_tiled`): every weight load
+instruction then reads 1 KiB of contiguous HBM.  The copy costs one more model's worth of HBM (14.5 GB
+for Mistral-7B at TP=1, 5 % of an MI355X's 288 GB).
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ from dataclasses import dataclass
 import torch
 
 from ..models.mistral import MistralConfig
-from ..ops.reference import gate_up_perm, rotary_perm
+from ..ops.reference import gate_up_perm, rotary_perm, tile_weight
 
 
 @dataclass
@@ -33,6 +37,11 @@ class LayerWeights:
     ffn_norm: torch.Tensor
     wgu: torch.Tensor
     wd: torch.Tensor
+    # decode copies in the tiled layout (attach_tiled)
+    wqkv_t: torch.Tensor = None
+    wo_t: torch.Tensor = None
+    wgu_t: torch.Tensor = None
+    wd_t: torch.Tensor = None
 
 
 @dataclass
@@ -44,6 +53,7 @@ class EngineWeights:
     layers: list
     final_norm: torch.Tensor
     lm_head: torch.Tensor
+    lm_head_t: torch.Tensor = None
 
     @property
     def nh(self) -> int:
@@ -66,10 +76,23 @@ class EngineWeights:
         return self.tp_rank * self.vocab_local
 
     def nbytes(self) -> int:
+        """Bytes of one copy of the model (what a decode step streams)."""
         n = self.embed.numel() + self.final_norm.numel() + self.lm_head.numel()
         for L in self.layers:
             n += sum(t.numel() for t in (L.attn_norm, L.wqkv, L.wo, L.ffn_norm, L.wgu, L.wd))
         return 2 * n
+
+
+@torch.no_grad()
+def attach_tiled(w: EngineWeights) -> EngineWeights:
+    """Add the tiled decode copies of every GEMM weight (idempotent)."""
+    for L in w.layers:
+        if L.wqkv_t is None:
+            L.wqkv_t, L.wo_t = tile_weight(L.wqkv), tile_weight(L.wo)
+            L.wgu_t, L.wd_t = tile_weight(L.wgu), tile_weight(L.wd)
+    if w.lm_head_t is None:
+        w.lm_head_t = tile_weight(w.lm_head)
+    return w
 
 
 def _permute_units(w: torch.Tensor) -> torch.Tensor:
@@ -101,9 +124,9 @@ def convert_standard(cfg: MistralConfig, std, tp_rank: int = 0, tp_size: int = 1
             attn_norm=L["attn_norm"].contiguous().to(device), wqkv=wqkv.contiguous().to(device),
             wo=wo.contiguous().to(device), ffn_norm=L["ffn_norm"].contiguous().to(device),
             wgu=wgu.contiguous().to(device), wd=wd.contiguous().to(device)))
-    return EngineWeights(cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, embed=std["embed"].contiguous().to(device),
-                         layers=layers, final_norm=std["final_norm"].contiguous().to(device),
-                         lm_head=std["lm_head"][r * V:(r + 1) * V].contiguous().to(device))
+    return attach_tiled(EngineWeights(
+        cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, embed=std["embed"].contiguous().to(device), layers=layers,
+        final_norm=std["final_norm"].contiguous().to(device), lm_head=std["lm_head"][r * V:(r + 1) * V].contiguous().to(device)))
 
 
 @torch.no_grad()
@@ -138,8 +161,8 @@ def random_engine_weights(cfg: MistralConfig, tp_rank: int = 0, tp_size: int = 1
     for _ in range(cfg.num_layers):
         layers.append(LayerWeights(attn_norm=norm(H), wqkv=lin((nh + 2 * nkv) * D, H), wo=lin(H, nh * D),
                                    ffn_norm=norm(H), wgu=lin(2 * F, H), wd=lin(H, F)))
-    return EngineWeights(cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, embed=embed, layers=layers,
-                         final_norm=norm(H), lm_head=lin(V, H))
+    return attach_tiled(EngineWeights(cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, embed=embed, layers=layers,
+                                      final_norm=norm(H), lm_head=lin(V, H)))
 
 
 def load_safetensors(cfg: MistralConfig, path: str, tp_rank: int = 0, tp_size: int = 1, device="cpu") -> EngineWeights:

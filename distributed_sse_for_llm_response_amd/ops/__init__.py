@@ -17,7 +17,9 @@ import torch
 
 from . import reference as ref
 
-_LIB = Path(__file__).resolve().parent.parent / "_lib" / "libdsse_kernels.so"
+_VARIANT = os.environ.get("DSSE_KERNELS_VARIANT", "")  # experiment builds (e.g. "nt"), see _build.py
+_LIB = Path(__file__).resolve().parent.parent / "_lib" / (
+    f"libdsse_kernels_{_VARIANT}.so" if _VARIANT else "libdsse_kernels.so")
 _loaded = False
 _load_error: str | None = None
 
@@ -91,11 +93,20 @@ def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv
         ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
 
 
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None):
+def gemm_resid_split(x, w, resid, part) -> int:
+    """resid += x · wᵀ, or (when the X-in-LDS kernel splits K) write fp32 slabs [S, M, N] into `part`
+    and return S so the following rmsnorm(part=..., nsplit=S) folds the reduction into the norm."""
+    if _hip(x):
+        return int(torch.ops.dsse.gemm_resid_split(x, w, resid, part))
+    ref.gemm_resid(x, w, resid)
+    return 0
+
+
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
     if _hip(resid):
-        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids)
+        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
     else:
-        ref.rmsnorm(resid, w, y, eps, delta, embed, ids)
+        ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
 
 
 def rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):

@@ -43,6 +43,25 @@ def vperm(off: torch.Tensor) -> torch.Tensor:
     return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4 + (off & 3)
 
 
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """Row-major [N, K] weight -> the decode GEMMs' tiled layout (same shape, permuted storage).
+
+    Blocks of (16-row tile T, 128-column chunk c) are stored contiguously in (T, c) order; inside a
+    block, element [s][lane][j] with lane = r + 16 g holds W[16T + r][128c + 32g + 8s + j], i.e. the
+    MFMA B fragment of k-step s (csrc/kernels/api.h kTileChunk), so every weight load instruction of
+    the decode GEMM reads 1 KiB contiguous.
+    """
+    N, K = w.shape
+    assert N % 16 == 0 and K % 128 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 128, 4, 4, 8).permute(0, 2, 4, 3, 1, 5).contiguous().view(N, K)
+
+
+def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`tile_weight`."""
+    N, K = wt.shape
+    return wt.reshape(N // 16, K // 128, 4, 4, 16, 8).permute(0, 4, 1, 3, 2, 5).reshape(N, K)
+
+
 def rope_table(max_pos: int, theta: float, device=None) -> torch.Tensor:
     """[max_pos, 64, 2] fp32 (cos, sin) for the rotate-half convention, head_dim 128."""
     inv = theta ** (-torch.arange(0, HEAD_DIM, 2, dtype=torch.float64) / HEAD_DIM)
@@ -79,23 +98,24 @@ def _write_kv(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache, v_
 
 
 # ---------------------------------------------------------------- GEMMs
+# The decode GEMMs take their weight in the tiled layout (tile_weight), like the HIP kernels.
 def gemm_out(x, w, out):
-    out.copy_((x.float() @ w.float().t()).to(out.dtype))
+    out.copy_((x.float() @ untile_weight(w).float().t()).to(out.dtype))
 
 
 def gemm_resid(x, w, resid):
-    resid.add_(x.float() @ w.float().t())
+    resid.add_(x.float() @ untile_weight(w).float().t())
 
 
 def gemm_silu(x, w, out):
-    y = (x.float() @ w.float().t()).view(x.shape[0], -1, 2, 8)
+    y = (x.float() @ untile_weight(w).float().t()).view(x.shape[0], -1, 2, 8)
     g, u = y[:, :, 0, :], y[:, :, 1, :]
     out.copy_((torch.nn.functional.silu(g) * u).reshape(x.shape[0], -1).to(out.dtype))
 
 
 def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
     M = x.shape[0]
-    y = x.float() @ w.float().t()
+    y = x.float() @ untile_weight(w).float().t()
     qkv = _unpermute_units(y, nh + 2 * nkv)
     rot = _rope(qkv[:, : nh + nkv], positions[:M], rope)
     q_out.view(-1)[: M * nh * HEAD_DIM].copy_(rot[:, :nh].reshape(-1).to(q_out.dtype))
@@ -116,12 +136,15 @@ def silu_mul(gu, h):
 
 
 # ---------------------------------------------------------------- norms
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None):
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
     M = y.shape[0]
+    H = y.shape[1]
     if embed is not None:
         resid[:M] = embed[ids[:M].long()].float()
     elif delta is not None:
         resid[:M] += delta[:M].float()
+    elif part is not None and nsplit > 0:
+        resid[:M] += part.view(-1)[: nsplit * M * H].view(nsplit, M, H).sum(0)
     r = resid[:M]
     y.copy_((r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(y.dtype))
 

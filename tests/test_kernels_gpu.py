@@ -29,6 +29,9 @@ GEMM_CONFIGS = {
     "xlds-ks256-nw4": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "256", "DSSE_X_NW": "4"},
     "xlds-ks512-nt2": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "512", "DSSE_X_NT": "2", "DSSE_X_TG": "3"},
     "xlds-d8": {"DSSE_GEMM_IMPL": "1", "DSSE_X_DEPTH": "8", "DSSE_X_TG": "16"},
+    "stream-default": {"DSSE_GEMM_IMPL": "2"},
+    "stream-nt2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NT": "2"},
+    "stream-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
@@ -46,7 +49,7 @@ def tiles(request, monkeypatch):
 def test_gemm_out_bf16_f32(gpu, tiles, M):
     g = torch.Generator().manual_seed(M)
     x = _rand(M, 1024, dev=gpu, gen=g)
-    w = _rand(512, 1024, dev=gpu, scale=1 / 32, gen=g)
+    w = R.tile_weight(_rand(512, 1024, dev=gpu, scale=1 / 32, gen=g))
     for dt in (torch.bfloat16, torch.float32):
         out = torch.zeros(M, 512, device=gpu, dtype=dt)
         ref = torch.zeros(M, 512, dtype=dt)
@@ -59,7 +62,7 @@ def test_gemm_out_bf16_f32(gpu, tiles, M):
 def test_gemm_resid(gpu, tiles, M, K):
     g = torch.Generator().manual_seed(K)
     x = _rand(M, K, dev=gpu, gen=g)
-    w = _rand(256, K, dev=gpu, scale=1 / math.sqrt(K), gen=g)
+    w = R.tile_weight(_rand(256, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
     r0 = torch.randn(M, 256, generator=g)
     r = r0.clone().to(gpu)
     ops.gemm_resid(x, w, r)
@@ -67,11 +70,34 @@ def test_gemm_resid(gpu, tiles, M, K):
     _close(r, r0, 1e-3, 1e-3, "gemm_resid")
 
 
+@pytest.mark.parametrize("M,K", [(64, 4096), (40, 14336), (4, 4096)])
+def test_gemm_resid_split_then_fused_norm(gpu, M, K):
+    """Split-K slabs reduced inside the RMSNorm equal resid += x·wᵀ followed by the norm."""
+    g = torch.Generator().manual_seed(M + K)
+    H = 1024
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(H, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16()
+    r0 = torch.randn(M, H, generator=g)
+    r = r0.clone().to(gpu)
+    part = torch.zeros(32 * 64 * H, device=gpu)
+    y = torch.zeros(M, H, device=gpu, dtype=torch.bfloat16)
+    ns = ops.gemm_resid_split(x, w, r, part)
+    if M > 16:
+        assert ns > 1
+    ops.rmsnorm(r, nw.to(gpu), y, 1e-5, part=part, nsplit=ns)
+    yr = torch.zeros(M, H, dtype=torch.bfloat16)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    R.rmsnorm(r0, nw, yr, 1e-5)
+    _close(r, r0, 1e-3, 1e-3, "resid")
+    _close(y, yr, 2e-2, 1e-2, "y")
+
+
 @pytest.mark.parametrize("M", [1, 20, 64])
 def test_gemm_silu(gpu, tiles, M):
     g = torch.Generator().manual_seed(M + 100)
     x = _rand(M, 2048, dev=gpu, gen=g)
-    w = _rand(2 * 704, 2048, dev=gpu, scale=1 / 45, gen=g)
+    w = R.tile_weight(_rand(2 * 704, 2048, dev=gpu, scale=1 / 45, gen=g))
     out = torch.zeros(M, 704, device=gpu, dtype=torch.bfloat16)
     ref = torch.zeros(M, 704, dtype=torch.bfloat16)
     ops.gemm_silu(x, w, out)
@@ -84,7 +110,7 @@ def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     nh, nkv, H = 8, 2, 1024
     g = torch.Generator().manual_seed(M + 7)
     x = _rand(M, H, dev=gpu, gen=g)
-    w = _rand((nh + 2 * nkv) * 128, H, dev=gpu, scale=1 / 32, gen=g)
+    w = R.tile_weight(_rand((nh + 2 * nkv) * 128, H, dev=gpu, scale=1 / 32, gen=g))
     rope = R.rope_table(4096, 1e6, gpu)
     positions = torch.randint(0, 4000, (M,), generator=g, dtype=torch.int32)
     slots = torch.randperm(8 * 32, generator=g)[:M].to(torch.int32)
@@ -297,4 +323,4 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 2
+    assert torch.ops.dsse.kernels_abi_version() == 3

@@ -19,6 +19,7 @@ run() {  # name, timeout, cmd...
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} ;;
+    tune) run tune 600 python tools/tune_gemm.py ${TUNE_ARGS:---M 16,32,64 --iters 30} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ${BENCH_ARGS:---steps 32 --warmup 4} ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 8 --warmup 2 ${PROF_ARGS:-} ;;

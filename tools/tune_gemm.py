@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--configs", default="skinny;x;x:DSSE_X_NW=4;x:DSSE_X_NT=2;x:DSSE_X_KS=512",
-                    help="';'-separated; 'skinny' or 'x', optionally ':K=V,K=V' env overrides")
+                    help="';'-separated; 'skinny', 'x' (X-in-LDS) or 's' (X-streaming), optionally ':K=V,K=V' env overrides")
     ap.add_argument("--out", default="")
     ap.add_argument("--grid", action="store_true", help="sweep the X-in-LDS parameter grid")
     args = ap.parse_args()
@@ -71,10 +71,10 @@ def main():
         for M in [int(m) for m in args.M.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             for cfg in args.configs.split(";"):
-                for k in [k for k in os.environ if k.startswith("DSSE_X_") or k.startswith("DSSE_GEMM_")]:
+                for k in [k for k in os.environ if k.startswith(("DSSE_X_", "DSSE_S_", "DSSE_GEMM_"))]:
                     os.environ.pop(k, None)
                 impl, _, kv = cfg.partition(":")
-                os.environ["DSSE_GEMM_IMPL"] = "0" if impl == "skinny" else "1"
+                os.environ["DSSE_GEMM_IMPL"] = {"skinny": "0", "x": "1", "s": "2"}[impl]
                 for item in filter(None, kv.split(",")):
                     k, v = item.split("=")
                     os.environ[k] = v
