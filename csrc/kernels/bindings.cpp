@@ -85,17 +85,25 @@ XCfg pick_xlds(int M, int N, int K) {
   return c;
 }
 
-// X-streaming kernel configuration (gemm_stream.hip).  Env overrides: DSSE_S_NT, DSSE_S_NW, DSSE_S_SPLIT.
+// X-streaming kernel configuration (gemm_stream.hip).  Env overrides: DSSE_S_NT, DSSE_S_NW, DSSE_S_RD,
+// DSSE_S_SPLIT.
 struct SCfg {
-  int mt, nt, nw, S;
+  int mt, nt, nw, rd, S;
   bool ok;
 };
 SCfg pick_stream(int M, int N, int K) {
   SCfg c{};
   c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   c.nt = env_int("DSSE_S_NT", 1);
-  c.nw = env_int("DSSE_S_NW", 8);
+  // 8 waves per workgroup when that still gives ~one workgroup per CU without split-K (gate_up,
+  // LM head), else 4 (narrow O / down / QKV: more, shorter workgroups; measured, profiles/gemm_stream_r1.md)
+  c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
+  if (c.nt == 2) c.nw = 8;  // instantiated (nt, nw): (1, 8), (2, 8), (1, 4) — gemm_stream.hip
+  if (c.nw != 4) c.nw = 8;
   if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
+  if ((N / 16) % c.nw != 0) c.nw = 4;
+  c.rd = env_int("DSSE_S_RD", 1);
+  if (c.nt == 2 || c.rd != 2) c.rd = 1;
   c.ok = K % 512 == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
   const int wgs = N / (16 * c.nt) / c.nw, slices = K / 512;
@@ -144,7 +152,7 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
     const SCfg c = pick_stream(M, N, K);
     at::Tensor part;
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
-    DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+    DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
                                     c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
     return;
   }
@@ -205,7 +213,7 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
       check_dtype(x, at::kBFloat16, "x");
       check_dtype(w, at::kBFloat16, "w");
       dsse::GemmEpi ep{};
-      DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kResidAdd, c.mt, c.nt, c.nw, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N,
+      DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kResidAdd, c.mt, c.nt, c.nw, c.rd, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N,
                                       &ep, part.data_ptr<float>(), cur_stream()));
       return c.S;
     }

@@ -12,26 +12,27 @@ DEV int vperm_tok(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4
 // ---- K1 + K2: (embedding gather | residual add) + RMSNorm ------------------------------------
 // MODE 0: y = rmsnorm(resid)            MODE 1: resid += delta; y = rmsnorm(resid)
 // MODE 2: resid = embed[ids[m]]; y = rmsnorm(resid)
-// The residual stream is fp32 [M, H]; y is the bf16 input of the next GEMM.
-// One 256-thread workgroup per row; each thread keeps its H/256 values in registers.
 // MODE 3: resid += sum_s part[s, m, :] (fp32 split-K slabs of the O / down projection, fusing the
 //         split-K reduction into the norm that consumes it); y = rmsnorm(resid)
+// The residual stream is fp32 [M, H]; y is the bf16 input of the next GEMM.  One workgroup of
+// min(1024, H/4) threads per row (a decode batch has only M <= 64 rows, so the row is spread over
+// as many waves as possible to keep enough loads in flight); each thread owns H / (4·threads) float4s.
 template <int MODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
                const bf16* __restrict__ embed, const int* __restrict__ ids,
                const bf16* __restrict__ w, bf16* __restrict__ y, float eps,
                const float* __restrict__ part = nullptr, int nsplit = 0, int M = 0) {
-  const int m = blockIdx.x, tid = threadIdx.x;
+  const int m = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   float* rrow = resid + (size_t)m * H;
-  constexpr int kMaxIt = 8;  // H <= 8192
+  constexpr int kMaxIt = 2;  // H <= 8192
   float4 v[kMaxIt];
-  const int nit = H / 1024;
+  const int nit = H / (4 * nt);
   float ss = 0.f;
 #pragma unroll
   for (int it = 0; it < kMaxIt; ++it) {
     if (it < nit) {
-      const int i = it * 1024 + tid * 4;
+      const int i = (it * nt + tid) * 4;
       float4 x;
       if constexpr (MODE == 2) {
         const bf16x4 e = *reinterpret_cast<const bf16x4*>(embed + (size_t)ids[m] * H + i);
@@ -43,8 +44,21 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
           x.x += bf2f(d[0]); x.y += bf2f(d[1]); x.z += bf2f(d[2]); x.w += bf2f(d[3]);
         }
         if constexpr (MODE == 3) {
-          for (int s = 0; s < nsplit; ++s) {
-            const float4 d = *reinterpret_cast<const float4*>(part + ((size_t)s * M + m) * H + i);
+          const float* p = part + (size_t)m * H + i;
+          const size_t slab = (size_t)M * H;
+          int s = 0;
+          for (; s + 4 <= nsplit; s += 4) {  // four independent loads in flight per step
+            const float4 d0 = *reinterpret_cast<const float4*>(p + (s + 0) * slab);
+            const float4 d1 = *reinterpret_cast<const float4*>(p + (s + 1) * slab);
+            const float4 d2 = *reinterpret_cast<const float4*>(p + (s + 2) * slab);
+            const float4 d3 = *reinterpret_cast<const float4*>(p + (s + 3) * slab);
+            x.x += (d0.x + d1.x) + (d2.x + d3.x);
+            x.y += (d0.y + d1.y) + (d2.y + d3.y);
+            x.z += (d0.z + d1.z) + (d2.z + d3.z);
+            x.w += (d0.w + d1.w) + (d2.w + d3.w);
+          }
+          for (; s < nsplit; ++s) {
+            const float4 d = *reinterpret_cast<const float4*>(p + s * slab);
             x.x += d.x; x.y += d.y; x.z += d.z; x.w += d.w;
           }
         }
@@ -55,15 +69,16 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
     }
   }
   ss = wave_sum(ss);
-  __shared__ float red[4];
+  __shared__ float red[16];
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
+  float tot = 0.f;
+  for (int i = 0; i < (nt >> 6); ++i) tot += red[i];
   const float inv = rsqrtf(tot / (float)H + eps);
 #pragma unroll
   for (int it = 0; it < kMaxIt; ++it) {
     if (it < nit) {
-      const int i = it * 1024 + tid * 4;
+      const int i = (it * nt + tid) * 4;
       const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + i);
       bf16x4 o;
       o[0] = f2bf(v[it].x * inv * bf2f(wv[0]));
@@ -167,11 +182,12 @@ extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const v
   const bf16* e = reinterpret_cast<const bf16*>(embed);
   const bf16* wp = reinterpret_cast<const bf16*>(w);
   bf16* yp = reinterpret_cast<bf16*>(y);
+  const int nt = std::min(1024, H / 4);  // host-checked: H % 256 == 0, H <= 8192
   switch (mode) {
-    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(256), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

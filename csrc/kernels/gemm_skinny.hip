@@ -12,6 +12,9 @@
 //     (lane group g owns k in [32g, 32g+32) of the chunk) identically for X and W, so every
 //     load is a full 64-byte run while the reduction stays exact.
 //   * the next chunk is loaded while the current one is multiplied (2-deep register pipeline).
+//   * weights come from the tiled layout (api.h kTileChunk) with non-temporal loads: 1 KiB contiguous
+//     per load instruction, and the once-read stream does not evict X from L2 (M = 1: 5.5 -> 6.2 TB/s
+//     on gate_up, 5.9 -> 6.5 TB/s on the LM head; profiles/gemm_stream_r1.md).
 //   * fused epilogues: bf16 store, fp32 store (logits), fp32 residual add (O / down
 //     projections), SiLU·mul over gate/up pairs (gate_up), and RoPE + paged-KV-cache write
 //     (QKV).  The paired epilogues rely on the engine's weight-row permutation: inside each
@@ -34,7 +37,7 @@ DEV void load_chunk(bf16x8 (&wf)[NT][4], bf16x8 (&xf)[MT][4], const bf16* const 
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) wf[t][s] = ld_bf16x8(wp[t] + (size_t)c * kTileChunk + 512 * s);
+    for (int s = 0; s < 4; ++s) wf[t][s] = ld_nt_bf16x8(wp[t] + (size_t)c * kTileChunk + 512 * s);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

@@ -11,7 +11,9 @@
 // slice i+1 into registers and writes them to the other buffer after its last MFMA — one barrier per
 // slice and no prologue beyond the first (small) slice.  Weights stream HBM -> VGPRs from the tiled
 // layout (api.h kTileChunk: 4 contiguous KiB per (tile, K-chunk)) through a CPS-deep register ring
-// that runs across slice boundaries.  Split-K (grid.y = S) is only used when N is too narrow to give
+// that runs across slice boundaries.  The weight loads are non-temporal: streamed once, they must not
+// evict X from L2 — with default loads the kernel slows down linearly in M (X re-fetched through the
+// fabric), with nt it is flat in M (tools/gemm_ab.sh, profiles/gemm_stream_r1.md).  Split-K (grid.y = S) is only used when N is too narrow to give
 // ~one workgroup per CU (O / down / QKV projections); then fp32 slabs [S, M, N] go to `part`.
 //
 // Rows m >= M of the X slices are never written; their MFMA rows produce garbage that is never
@@ -22,7 +24,7 @@ namespace dsse {
 
 constexpr int kStreamCPS = 4;  // K-chunks of 128 per LDS slice
 
-template <int MT, int NT, int NW, int MODE>
+template <int MT, int NT, int NW, int RD, int MODE>
 __global__ void __launch_bounds__(64 * NW)
 gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
                    int Kr, GemmEpi ep, float* __restrict__ part) {
@@ -49,13 +51,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#if DSSE_W_NT
-        wf[t][s] = ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
-#else
-        wf[t][s] = ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
-#endif
-      }
+      for (int s = 0; s < 4; ++s) wf[t][s] = ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
   };
 
   bf16x8 xs[PPT];
@@ -79,9 +75,10 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     }
   };
 
-  bf16x8 ring[CPS][NT][4];
+  constexpr int DEPTH = CPS * RD;  // weight ring: RD slices of chunks in flight
+  bf16x8 ring[DEPTH][NT][4];
 #pragma unroll
-  for (int d = 0; d < CPS - 1; ++d) load_w(d, ring[d]);
+  for (int d = 0; d < DEPTH - 1; ++d) load_w(d, ring[d]);
   load_x(0);
   store_x(0);
 
@@ -91,27 +88,34 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int sl = 0; sl < nsl; ++sl) {
-    __syncthreads();  // slice sl visible; everyone is done reading slice sl - 1's buffer
-    const bool more = sl + 1 < nsl;
-    if (more) load_x(sl + 1);
-    const char* xb0 = smem + (sl & 1) * BUF;
+  // RD slices per iteration so that every ring slot index is a compile-time constant
+  for (int sl0 = 0; sl0 < nsl; sl0 += RD) {
 #pragma unroll
-    for (int d = 0; d < CPS; ++d) {
-      load_w(sl * CPS + d + CPS - 1, ring[(d + CPS - 1) % CPS]);
-      const char* xb = xb0 + (d << 8);
+    for (int h = 0; h < RD; ++h) {
+      const int sl = sl0 + h;
+      if (h > 0 && sl >= nsl) break;
+      __syncthreads();  // slice sl visible; everyone is done reading slice sl - 1's buffer
+      const bool more = sl + 1 < nsl;
+      if (more) load_x(sl + 1);
+      const char* xb0 = smem + (sl & 1) * BUF;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int ch = ((4 * g + s) ^ swz(r)) << 4;
+      for (int d = 0; d < CPS; ++d) {
+        const int slot = h * CPS + d;
+        load_w(sl * CPS + d + DEPTH - 1, ring[(slot + DEPTH - 1) % DEPTH]);
+        const char* xb = xb0 + (d << 8);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
+        for (int s = 0; s < 4; ++s) {
+          const int ch = ((4 * g + s) ^ swz(r)) << 4;
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf, ring[d][t][s], acc[mt][t]);
+          for (int mt = 0; mt < MT; ++mt) {
+            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf, ring[slot][t][s], acc[mt][t]);
+          }
         }
       }
+      if (more) store_x((sl + 1) & 1);
     }
-    if (more) store_x((sl + 1) & 1);
   }
 
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
@@ -127,29 +131,31 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       }
 }
 
-template <int MT, int NT, int NW, int MODE>
+template <int MT, int NT, int NW, int RD, int MODE>
 static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
   const int TG = N / (16 * NT);
   const size_t lds = (size_t)2 * 16 * MT * kStreamCPS * 256;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, MODE>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   dim3 grid(TG / NW, S), block(64 * NW);
-  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep,
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep,
                      part);
   return hipGetLastError();
 }
 
 template <int MODE>
-static hipError_t launch_s_mode(int mt, int nt, int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
+static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
                                 int S, const GemmEpi& ep, float* part, hipStream_t st) {
-#define DSSE_S_CASE(MT_, NT_, NW_) \
-  if (mt == MT_ && nt == NT_ && nw == NW_) return launch_s<MT_, NT_, NW_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-#define DSSE_S_MT(MT_) DSSE_S_CASE(MT_, 1, 8) DSSE_S_CASE(MT_, 2, 8) DSSE_S_CASE(MT_, 1, 4)
+#define DSSE_S_CASE(MT_, NT_, NW_, RD_)         \
+  if (mt == MT_ && nt == NT_ && nw == NW_ && rd == RD_) \
+    return launch_s<MT_, NT_, NW_, RD_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+#define DSSE_S_MT(MT_) \
+  DSSE_S_CASE(MT_, 1, 8, 1) DSSE_S_CASE(MT_, 2, 8, 1) DSSE_S_CASE(MT_, 1, 4, 1) DSSE_S_CASE(MT_, 1, 4, 2) DSSE_S_CASE(MT_, 1, 8, 2)
   DSSE_S_MT(1) DSSE_S_MT(2) DSSE_S_MT(4)
 #undef DSSE_S_MT
 #undef DSSE_S_CASE
@@ -158,10 +164,11 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, const bf16* X, int ldx, 
 
 }  // namespace dsse
 
+// rd: weight-ring depth in LDS slices (1: 4 chunks = 16 KiB per wave in flight, 2: 8 chunks).
 // Shape contract (checked by the caller): K % (512 S) == 0, (N / (16 nt)) % nw == 0, M <= 16 mt <= 64.
 // part: fp32 [S, M, N] workspace when S > 1.  partial_only: leave the slabs for the consumer (the fused
 // residual + RMSNorm kernel) instead of reducing them here.
-extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int S, int partial_only, const void* X,
+extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X,
                                        int ldx, int M, const void* W, int K, int N, const dsse::GemmEpi* ep,
                                        float* part, hipStream_t st) {
   using namespace dsse;
@@ -169,15 +176,15 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int S, 
   const bf16* w = reinterpret_cast<const bf16*>(W);
   if (S == 1) {
     switch (mode) {
-      case kStoreBf16: return launch_s_mode<kStoreBf16>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kStoreF32: return launch_s_mode<kStoreF32>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kResidAdd: return launch_s_mode<kResidAdd>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kSiluMul: return launch_s_mode<kSiluMul>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kQkvRope: return launch_s_mode<kQkvRope>(mt, nt, nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreBf16: return launch_s_mode<kStoreBf16>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_s_mode<kStoreF32>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_s_mode<kResidAdd>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_s_mode<kSiluMul>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_s_mode<kQkvRope>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
     }
     return hipErrorInvalidValue;
   }
-  hipError_t e = launch_s_mode<kPartial>(mt, nt, nw, x, ldx, M, w, K, N, S, *ep, part, st);
+  hipError_t e = launch_s_mode<kPartial>(mt, nt, nw, rd, x, ldx, M, w, K, N, S, *ep, part, st);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

@@ -46,8 +46,12 @@ def batch_buckets(max_batch: int):
     return sorted(set(out))
 
 
-def decode_partitioning(B: int, nkv: int, max_ctx: int, target_wgs: int = 1024, max_parts: int = 32):
-    """(part, nparts) for flash-decoding so that B·Hkv·nparts workgroups fill the chip."""
+def decode_partitioning(B: int, nkv: int, max_ctx: int, target_wgs: int = 512, max_parts: int = 32):
+    """(part, nparts) for flash-decoding so that B·Hkv·nparts workgroups fill the chip.
+
+    512 = two 256-thread workgroups per CU; at B·Hkv >= 512 (e.g. 64 streams x 8 KV heads) there is a
+    single partition and the combine kernel is skipped.
+    """
     want = max(1, min(max_parts, math.ceil(target_wgs / max(1, B * nkv))))
     part = max(128, math.ceil(max_ctx / want / 128) * 128)
     nparts = math.ceil(max_ctx / part)

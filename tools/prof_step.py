@@ -1,0 +1,55 @@
+"""Per-decode-step kernel breakdown from a rocprofv3 kernel trace.
+
+Usage: python tools/prof_step.py gpurun_out/prof/run_kernel_trace.csv [--marker sample_pick] [--last 6]
+
+A decode step ends with the sampler's pick kernel; the last `--last` complete steps (after prefill) are
+averaged: per kernel name, calls and GPU time per step, plus the step's wall time (end of one pick to
+the end of the next) and the idle share (wall - busy).  Prints a markdown table.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import re
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "").replace("dsse::", "")
+    return name[:70]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--marker", default="sample_pick")
+    ap.add_argument("--last", type=int, default=6)
+    args = ap.parse_args()
+    rows = []
+    with open(args.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    ends = [i for i, (_, _, n) in enumerate(rows) if args.marker in n]
+    if len(ends) < args.last + 1:
+        raise SystemExit(f"only {len(ends)} steps found")
+    sel = ends[-(args.last + 1):]
+    per = collections.defaultdict(lambda: [0, 0.0])
+    wall = busy = 0.0
+    for a, b in zip(sel[:-1], sel[1:]):
+        wall += (rows[b][1] - rows[a][1]) / 1e3
+        for s, e, n in rows[a + 1:b + 1]:
+            per[short(n)][0] += 1
+            per[short(n)][1] += (e - s) / 1e3
+            busy += (e - s) / 1e3
+    k = args.last
+    print(f"decode step: wall {wall / k:.1f} us, kernel busy {busy / k:.1f} us, idle {(wall - busy) / k:.1f} us\n")
+    print("| kernel | calls/step | us/step | % of busy |")
+    print("|---|---|---|---|")
+    for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        print(f"| `{n}` | {c / k:.0f} | {t / k:.1f} | {100 * t / busy:.1f} |")
+
+
+if __name__ == "__main__":
+    main()

@@ -46,6 +46,7 @@ def time_op(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", default="1,16,32,64")
+    ap.add_argument("--ops", default="", help="comma-separated subset of qkv,o,gate_up,down,lm_head")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--configs", default="skinny;x;x:DSSE_X_NW=4;x:DSSE_X_NT=2;x:DSSE_X_KS=512",
@@ -65,6 +66,8 @@ def main():
                         cfgs.append(f"x:DSSE_X_KS={ks},DSSE_X_NW={nw},DSSE_X_DEPTH={depth},DSSE_X_TG={tgm * nw}")
         args.configs = ";".join(cfgs)
     for name, (N, K) in shapes(args.tp).items():
+        if args.ops and name not in args.ops.split(","):
+            continue
         nbytes = N * K * 2
         copies = max(2, (600 << 20) // nbytes + 1)
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
