@@ -161,6 +161,11 @@ def build_runtime(verbose: bool = False, force: bool = False, sanitize: str | No
         _run([cxx, *flags, "-shared", *objs, mod_obj, "-o", out_so], verbose)
     if main_src.exists() and (force or _stale(out_bin, objs + [main_obj])):
         _run([cxx, *flags, *objs, main_obj, "-o", out_bin], verbose)
+    # standalone tools (no runtime library): the native load generator / bench client
+    lg_src = CSRC / "tools" / "loadgen.cpp"
+    lg_bin = LIB_DIR / (f"dsse-loadgen-{sanitize}" if sanitize else "dsse-loadgen")
+    if lg_src.exists() and (force or _stale(lg_bin, [lg_src])):
+        _run([cxx, *flags, lg_src, "-o", lg_bin], verbose)
     return out_so
 
 

@@ -37,5 +37,15 @@ def server_binary() -> Path:
     return _LIB_DIR / "dsse-server"
 
 
+def loadgen_binary() -> Path:
+    """The native load generator / bench client (csrc/tools/loadgen.cpp), built on demand."""
+    p = _LIB_DIR / "dsse-loadgen"
+    if not p.exists() and os.environ.get("DSSE_AUTOBUILD", "1") == "1":
+        from .._build import build_runtime
+
+        build_runtime()
+    return p
+
+
 def __getattr__(name):
     return getattr(load(), name)
