@@ -2,9 +2,11 @@
 """Headline benchmark: concurrent SSE token streams + p50 inter-token latency, Mistral-7B on MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the driver launches one
-rank per GPU with torchrun.  Each rank is an independent Mistral-7B engine replica (DP, one engine
-per GPU, BASELINE config 2/3) serving ``--streams`` concurrent conversations (64 per GPU = config 2),
-so per-GPU work is fixed as N grows (weak scaling).  One timed step = one engine iteration for all
+rank per GPU with torchrun.  Each rank is a Mistral-7B engine replica (DP, one engine per GPU,
+BASELINE config 2/3) serving ``--streams`` concurrent conversations (64 per GPU = config 2), so per-GPU
+work is fixed as N grows (weak scaling).  With ``--delivery sse`` (default) one client process opens
+all N x streams POST /chat SSE connections to rank 0's server, whose C++ data-parallel router spreads
+them over the replicas through shared-memory rings (the ``serve --dp N`` path).  One timed step = one engine iteration for all
 live streams on every rank: the hipGraph-captured decode step (all 32 layers, LM head, sampler,
 token-ring append), the device->host token drain on a side stream, and host-side delivery of every
 token as an SSE ``event: token`` frame carrying the reference's TokenMessage JSON
@@ -47,8 +49,10 @@ def main():
 
     from distributed_sse_for_llm_response_amd.engine import bench_harness
 
-    # the SSE client process must be started before this process initialises the GPU
-    client = bench_harness.spawn_client() if args.delivery == "sse" else None
+    # the SSE client process (rank 0 only: one client drives every replica through the router) must be
+    # started before this process initialises the GPU
+    sse = args.delivery == "sse"
+    client = bench_harness.spawn_client() if sse and int(os.environ.get("RANK", "0")) == 0 else None
 
     import torch
     import torch.distributed as dist
@@ -63,7 +67,7 @@ def main():
     if device.type == "cuda":
         torch.cuda.set_device(device)
 
-    if client is not None:
+    if sse:
         res = bench_harness.run_serving_bench(client, model=args.model, device=device, streams=args.streams,
                                               prompt_len=args.prompt_len, steps=args.steps, warmup=args.warmup,
                                               tp=args.tp, use_graphs=not args.no_graph, rank=rank, world=world)
@@ -77,9 +81,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        itl = torch.tensor([res["p50_itl_ms"]], dtype=torch.float64, device=device)
-        dist.all_reduce(itl, op=dist.ReduceOp.MAX)
-        res["p50_itl_ms"] = float(itl.item())
+        if not sse:  # frame/none: per-rank delivery gaps; sse: the rank-0 client saw every stream
+            itl = torch.tensor([res["p50_itl_ms"]], dtype=torch.float64, device=device)
+            dist.all_reduce(itl, op=dist.ReduceOp.MAX)
+            res["p50_itl_ms"] = float(itl.item())
     replicas = world // args.tp
     total_streams = args.streams * replicas
     tokens = total_streams * args.steps
@@ -102,6 +107,8 @@ def main():
             "p50_itl_ms": round(res["p50_itl_ms"], 4),
             "p99_itl_ms": round(res.get("p99_itl_ms", 0.0), 4),
             "delivery": args.delivery,
+            "tokens_delivered_in_window": res.get("delivered_in_window"),
+            "client_errors": res.get("client_errors", []),
             "config": {"model": res.get("model", args.model), "global_batch": total_streams, "seq_len": args.prompt_len + args.steps
                        + args.warmup, "prompt_len": args.prompt_len,
                        "parallelism": f"dp{replicas}" + (f"xtp{args.tp}" if args.tp > 1 else "")},

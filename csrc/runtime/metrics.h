@@ -71,6 +71,11 @@ class Metrics {
   Histogram engine_decode_step_seconds;
   Histogram engine_ttft_seconds;
   Histogram engine_itl_seconds;
+  // data-parallel router (dp.h)
+  Gauge dp_workers_alive;
+  Counter dp_requests_routed_total;
+  Counter dp_requeued_total;
+  Counter dp_worker_failures_total;
 
   std::string render() const;        // full exposition for :9090/metrics
   std::string render_origin() const;  // "active_chats N\n" (origin /metrics)

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "bus.h"
+#include "dp.h"
 #include "inspector.h"
 #include "json.h"
 #include "metrics.h"
@@ -22,6 +23,22 @@ namespace py = pybind11;
 using namespace dsse;
 
 namespace {
+
+py::dict request_dict(const ChatRequest& r) {
+  py::dict d;
+  d["id"] = r.id;
+  d["conversation_id"] = r.conversation_id;
+  d["message"] = r.message;
+  d["arrival_ns"] = r.arrival_ns;
+  d["max_tokens"] = r.max_tokens;
+  d["temperature"] = r.temperature;
+  d["top_p"] = r.top_p;
+  d["top_k"] = r.top_k;
+  d["seed"] = r.seed;
+  d["ignore_eos"] = r.ignore_eos;
+  d["from_edge"] = r.from_edge;
+  return d;
+}
 
 class Runtime {
  public:
@@ -65,6 +82,8 @@ class Runtime {
   }
   void stop() {
     py::gil_scoped_release nogil;
+    if (dp_) dp_->stop();
+    dp_.reset();
     if (stub_) stub_->stop();
     stub_.reset();
     if (server_) server_->stop();
@@ -78,21 +97,7 @@ class Runtime {
       rs = server_->requests().pop(max, timeout_ms);
     }
     py::list out;
-    for (auto& r : rs) {
-      py::dict d;
-      d["id"] = r.id;
-      d["conversation_id"] = r.conversation_id;
-      d["message"] = r.message;
-      d["arrival_ns"] = r.arrival_ns;
-      d["max_tokens"] = r.max_tokens;
-      d["temperature"] = r.temperature;
-      d["top_p"] = r.top_p;
-      d["top_k"] = r.top_k;
-      d["seed"] = r.seed;
-      d["ignore_eos"] = r.ignore_eos;
-      d["from_edge"] = r.from_edge;
-      out.append(d);
-    }
+    for (auto& r : rs) out.append(request_dict(r));
     return out;
   }
   void submit(const std::string& conv_id, const std::string& message, int max_tokens) {
@@ -103,7 +108,36 @@ class Runtime {
     server_->submit_chat(std::move(r));
   }
 
-  void set_vocab(std::vector<std::string> pieces) { vocab_ = std::move(pieces); }
+  void set_vocab(std::vector<std::string> pieces) {
+    if (dp_) dp_->set_vocab(pieces);
+    vocab_ = std::move(pieces);
+  }
+
+  // Data-parallel mode: this runtime becomes the router for `workers` engine processes (dp.h).
+  void start_dp_router(const std::string& prefix, int workers, int ring_mb, int worker_timeout_ms) {
+    dp_ = std::make_unique<DpRouter>(*server_, prefix, workers, (size_t)ring_mb << 20, worker_timeout_ms);
+    dp_->set_vocab(vocab_);
+    std::string err;
+    if (!dp_->start(&err)) {
+      dp_.reset();
+      throw std::runtime_error("dp router start failed: " + err);
+    }
+  }
+  py::list dp_workers() {
+    py::list out;
+    if (!dp_) return out;
+    for (auto& i : dp_->workers()) {
+      py::dict d;
+      d["ready"] = i.ready;
+      d["alive"] = i.alive;
+      d["outstanding"] = i.outstanding;
+      d["batch"] = i.batch;
+      d["kv_free"] = i.kv_free;
+      d["active"] = i.active;
+      out.append(d);
+    }
+    return out;
+  }
 
   // Publish one engine step: conversation ids, token ids, sequence numbers, done flags.  Token text
   // comes from the vocabulary; `texts` (optional) overrides per entry (e.g. "[DONE]", "[ERROR]").
@@ -154,7 +188,67 @@ class Runtime {
   std::shared_ptr<Bus> bus_;
   std::unique_ptr<Server> server_;
   std::unique_ptr<StubEngine> stub_;
+  std::unique_ptr<DpRouter> dp_;
   std::vector<std::string> vocab_;
+};
+
+// Engine-worker end of a DP channel: the same calls the engine loop makes on a Runtime.
+class DpWorkerPy {
+ public:
+  DpWorkerPy(const std::string& prefix, int worker, int open_timeout_ms) {
+    {
+      py::gil_scoped_release nogil;
+      w_ = std::make_unique<DpWorker>(prefix, worker, open_timeout_ms);
+    }
+    if (!w_->ok()) throw std::runtime_error("dp worker attach failed: " + w_->error());
+  }
+  py::list poll_requests(size_t max, int timeout_ms) {
+    std::vector<ChatRequest> rs;
+    {
+      py::gil_scoped_release nogil;
+      std::vector<std::string> cancels;
+      bool sd = false;
+      rs = w_->poll(max, timeout_ms, &cancels, &sd);
+      cancels_.insert(cancels_.end(), cancels.begin(), cancels.end());
+      if (sd) shutdown_ = true;
+    }
+    py::list out;
+    for (auto& r : rs) out.append(request_dict(r));
+    return out;
+  }
+  std::vector<std::string> pop_cancellations() {
+    std::vector<std::string> out;
+    out.swap(cancels_);
+    return out;
+  }
+  bool shutdown_requested() const { return shutdown_; }
+  int publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
+                     const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
+                     const std::vector<std::string>& texts) {
+    const size_t n = conv_ids.size();
+    if (token_ids.size() != n || seqs.size() != n || dones.size() != n)
+      throw std::invalid_argument("publish_tokens: length mismatch");
+    py::gil_scoped_release nogil;
+    if (!w_->publish_tokens(conv_ids, token_ids, seqs, dones, ts, texts))
+      throw std::runtime_error("dp worker: token ring closed or full");
+    return (int)n;
+  }
+  void set_ready(bool r) {
+    py::gil_scoped_release nogil;
+    if (r) w_->hello();
+    else w_->bye();
+  }
+  void observe(double step_s, double batch, double kv_free, double active, const std::vector<double>& ttft,
+               const std::vector<double>& itl) {
+    py::gil_scoped_release nogil;
+    w_->stats(step_s, batch, kv_free, active, ttft, itl);
+  }
+  void set_vocab(const std::vector<std::string>&) {}  // text is resolved by the router
+
+ private:
+  std::unique_ptr<DpWorker> w_;
+  std::vector<std::string> cancels_;
+  bool shutdown_ = false;
 };
 
 }  // namespace
@@ -181,7 +275,24 @@ PYBIND11_MODULE(_dsse_runtime, m) {
       .def("set_ready", &Runtime::set_ready)
       .def("set_local_engine", &Runtime::set_local_engine)
       .def("start_stub", &Runtime::start_stub, py::arg("tokens") = 50, py::arg("delay_ms") = 50, py::arg("workers") = 2)
-      .def("metrics_text", &Runtime::metrics_text);
+      .def("metrics_text", &Runtime::metrics_text)
+      .def("start_dp_router", &Runtime::start_dp_router, py::arg("prefix"), py::arg("workers"), py::arg("ring_mb") = 8,
+           py::arg("worker_timeout_ms") = 10000)
+      .def("dp_workers", &Runtime::dp_workers);
+
+  py::class_<DpWorkerPy>(m, "DpWorker")
+      .def(py::init<const std::string&, int, int>(), py::arg("prefix"), py::arg("worker"),
+           py::arg("open_timeout_ms") = 60000)
+      .def("poll_requests", &DpWorkerPy::poll_requests, py::arg("max") = 256, py::arg("timeout_ms") = 0)
+      .def("pop_cancellations", &DpWorkerPy::pop_cancellations)
+      .def("shutdown_requested", &DpWorkerPy::shutdown_requested)
+      .def("publish_tokens", &DpWorkerPy::publish_tokens, py::arg("conversation_ids"), py::arg("token_ids"),
+           py::arg("sequences"), py::arg("dones"), py::arg("timestamp_ns") = 0,
+           py::arg("texts") = std::vector<std::string>{})
+      .def("set_ready", &DpWorkerPy::set_ready)
+      .def("observe", &DpWorkerPy::observe)
+      .def("set_vocab", &DpWorkerPy::set_vocab);
+  m.def("dp_ring_name", &dp_ring_name);
 
   m.def("encode_token_message", [](const std::string& cid, const std::string& tok, int64_t seq, bool done, int64_t ts) {
     return encode_token_message(TokenMessage{cid, tok, seq, done, ts});

@@ -150,18 +150,23 @@ def spawn_client():
 
 def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, prompt_len=512, steps=64, warmup=8,
                       tp=1, use_graphs=True, rank=0, world=1, seed=0):
-    """Full serving path: `streams` real POST /chat SSE connections (client process) -> native runtime
-    -> LLMEngine (scheduler, hipGraph decode, token-ring drain) -> bus -> epoll writers -> sockets.
+    """Full serving path: `streams` real POST /chat SSE connections per engine replica (one client process on
+    rank 0) -> native runtime + data-parallel router on rank 0 -> shared-memory ring -> this rank's LLMEngine
+    (scheduler, hipGraph decode, token-ring drain) -> ring -> router -> bus -> epoll writers -> sockets.
 
-    Timed: exactly `steps` engine steps once every stream is decoding.  The p50 inter-token latency is
-    measured by the client (socket receive times of consecutive tokens of a stream) inside the timed
-    window."""
+    Every rank is one replica (tp == 1) and serves the `streams` conversations the router assigns it.
+    Timed: exactly `steps` engine steps on every rank once all of its streams are decoding, bracketed by
+    barrier + device synchronize.  The p50 inter-token latency is measured by the client (socket receive
+    times of consecutive tokens of a stream) inside the timed window."""
     import json as _json
+    import os
 
     from .. import runtime as rt_mod
     from ..models.tokenizer import SyntheticTokenizer
     from .engine import LLMEngine, SamplingParams
 
+    if tp != 1:
+        raise ValueError("serving bench: data-parallel replicas only (tp=1); use --delivery frame for TP")
     device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
     total = steps + warmup
     cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
@@ -171,35 +176,45 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     engine = LLMEngine(r, eos_id=tok.eos_id, prefill_budget=r.max_prefill_tokens,
                        default_params=SamplingParams(temperature=1.0, top_p=1.0, max_tokens=total + 2))
     mod = rt_mod.load()
-    runtime = mod.Runtime({"host": "127.0.0.1", "sse_port": 0, "origin_port": -1, "metrics_port": -1, "resp_port": -1,
-                           "io_threads": 4, "local_engine": True})
-    runtime.set_vocab(tok.pieces())
-    runtime.start()
-    words = [f"w{i % 997}" for i in range(max(1, prompt_len - 8))]
-    client.stdin.write(_json.dumps({"host": "127.0.0.1", "port": runtime.bound_port("edge"), "streams": streams,
-                                    "message": " ".join(words), "max_tokens": total + 2, "rank": rank}) + "\n")
-    client.stdin.flush()
+    prefix = f"/dsse-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid() if world > 1 else os.getpid()}"
+    runtime = None
+    if rank == 0:
+        runtime = mod.Runtime({"host": "127.0.0.1", "sse_port": 0, "origin_port": -1, "metrics_port": -1,
+                               "resp_port": -1, "io_threads": 4, "local_engine": True})
+        runtime.set_vocab(tok.pieces())
+        runtime.start_dp_router(prefix, world, 16, 600_000)
+        runtime.start()
+    chan = mod.DpWorker(prefix, rank, 600_000)
+    chan.set_ready(True)
+    if rank == 0:
+        while sum(1 for i in runtime.dp_workers() if i["ready"]) < world:
+            time.sleep(0.01)
+        words = [f"w{i % 997}" for i in range(max(1, prompt_len - 8))]
+        client.stdin.write(_json.dumps({"host": "127.0.0.1", "port": runtime.bound_port("edge"),
+                                        "streams": streams * world, "message": " ".join(words),
+                                        "max_tokens": total + 2, "prefix": "bench-"}) + "\n")
+        client.stdin.flush()
 
     def publish(events):
         if events:
-            runtime.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
-                                   [e.sequence for e in events], [e.done for e in events], 0,
-                                   [e.text for e in events])
+            chan.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
+                                [e.sequence for e in events], [e.done for e in events], 0, [e.text for e in events])
 
     def pump(block_ms=0):
-        for req in runtime.poll_requests(1024, block_ms):
+        for req in chan.poll_requests(1024, block_ms):
             p = SamplingParams(temperature=1.0, top_p=1.0, max_tokens=req["max_tokens"], ignore_eos=True)
             engine.add_request(req["conversation_id"], tok.chat_prompt(req["message"]), p,
                                arrival_ns=req["arrival_ns"])
 
-    # admission + prefill until every stream is decoding
+    # admission + prefill until every stream of this replica is decoding
     t_admit = time.time()
     while sum(1 for s in engine.slots if s is not None and s.state == "decode") < streams:
         pump(20 if not engine.has_work() else 0)
         if engine.has_work():
             publish(engine.step())
-        if time.time() - t_admit > 600:
+        if time.time() - t_admit > 900:
             raise RuntimeError("bench: streams did not all start decoding")
+    _sync(device, world)
     for _ in range(warmup):
         publish(engine.step())
     _sync(device, world)
@@ -212,10 +227,14 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     t1_ns = time.time_ns()
     while engine.has_work():
         publish(engine.step())
-    out = client.stdout.readline()
-    client.wait(timeout=120)
-    runtime.stop()
-    res = _json.loads(out) if out.strip() else {"arrivals": [], "errors": ["client produced no output"]}
+    res = {"arrivals": [], "errors": []}
+    if rank == 0:
+        out = client.stdout.readline()
+        client.wait(timeout=300)
+        res = _json.loads(out) if out.strip() else {"arrivals": [], "errors": ["client produced no output"]}
+    _sync(device, world)
+    if runtime is not None:
+        runtime.stop()
     by_stream = {}
     for s, seq, t_ns, _ts in res["arrivals"]:
         by_stream.setdefault(s, []).append(t_ns)

@@ -59,7 +59,12 @@ def build_engine(cfg: ServeConfig, device=None, comm=None):
 
 
 class EngineLoop(threading.Thread):
-    """Pulls chat requests from the runtime, steps the engine, publishes token events."""
+    """Pulls chat requests from the runtime, steps the engine, publishes token events.
+
+    `runtime` is either the in-process ``Runtime`` (single replica, TP leader) or a ``DpWorker`` channel
+    to a data-parallel router (``serving/dp.py``); both expose poll_requests / pop_cancellations /
+    publish_tokens / set_ready.  A DP worker ships its engine metrics to the router (``observe``).
+    """
 
     def __init__(self, runtime, engine: LLMEngine, tokenizer, cfg: ServeConfig):
         super().__init__(daemon=True, name="engine-loop")
@@ -67,9 +72,16 @@ class EngineLoop(threading.Thread):
         self.stop_flag = threading.Event()
         self.error = None
         rt = rt_mod.load()
-        engine.on_ttft = rt.observe_ttft
-        engine.on_itl = rt.observe_itl
         self._rt = rt
+        self._remote = hasattr(runtime, "observe")
+        self._ttft, self._itl = [], []
+        self._last_obs = 0.0
+        if self._remote:
+            engine.on_ttft = self._ttft.append
+            engine.on_itl = self._itl.append
+        else:
+            engine.on_ttft = rt.observe_ttft
+            engine.on_itl = rt.observe_itl
 
     def _params(self, req) -> SamplingParams:
         d = self.engine.default_params
@@ -87,9 +99,29 @@ class EngineLoop(threading.Thread):
                                [e.sequence for e in events], [e.done for e in events], 0,
                                [e.text for e in events])
 
+    def _observe(self):
+        e = self.engine
+        running, free = float(e.num_running()), float(e.alloc.num_free)
+        if not self._remote:
+            self._rt.engine_observe(e.stats["last_step_s"], running, free)
+            self._rt.set_active_chats(running + len(e.waiting))
+            return
+        now = time.monotonic()
+        if now - self._last_obs < 0.05 and len(self._itl) < 4096:
+            return  # batch the observations: one stats message per ~50 ms
+        self._last_obs = now
+        ttft, itl = self._ttft[:], self._itl[:]
+        self._ttft.clear()
+        self._itl.clear()
+        self.rt.observe(e.stats["last_step_s"], running, free, running + len(e.waiting), ttft, itl)
+
+    def _shutdown(self) -> bool:
+        f = getattr(self.rt, "shutdown_requested", None)
+        return bool(f and f())
+
     def run(self):
         try:
-            while not self.stop_flag.is_set():
+            while not self.stop_flag.is_set() and not self._shutdown():
                 busy = self.engine.has_work()
                 for req in self.rt.poll_requests(256, 0 if busy else 20):
                     self.engine.add_request(req["conversation_id"], self.tok.chat_prompt(req["message"]),
@@ -100,9 +132,7 @@ class EngineLoop(threading.Thread):
                     continue
                 events = self.engine.step()
                 self.publish(events)
-                self._rt.engine_observe(self.engine.stats["last_step_s"], float(self.engine.num_running()),
-                                        float(self.engine.alloc.num_free))
-                self._rt.set_active_chats(float(self.engine.num_running() + len(self.engine.waiting)))
+                self._observe()
         except Exception as e:  # noqa: BLE001 - surfaced to the operator, readiness drops
             self.error = e
             self.rt.set_ready(False)

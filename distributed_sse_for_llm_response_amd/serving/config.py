@@ -5,7 +5,7 @@ Reference keys (same names, same defaults where they apply here):
   (llm-stream-proxy, src/llm-stream-proxy/main.go:70-96; the origin gets its own port because both
   services default to 8080 and they now share a process), LLM_PROXY_URL, INSPECTION_MODE,
   INSPECTION_BUFFER_MS, LOG_LEVEL, MODEL_NAME, REDIS_ADDR (the RESP ingest port, e.g. ":6379").
-Engine keys (new): TP, DP, MAX_MODEL_LEN, MAX_BATCH, KV_BLOCK (fixed 32), GPU_MEMORY_UTILIZATION,
+Engine keys (new): TP, DP, DP_PREFIX, DP_WORKER_TIMEOUT_MS, MAX_MODEL_LEN, MAX_BATCH, KV_BLOCK (fixed 32), GPU_MEMORY_UTILIZATION,
   SEED, MAX_TOKENS, PREFILL_BUDGET, TOKENIZER_PATH, WEIGHTS_PATH.
 """
 from __future__ import annotations
@@ -56,6 +56,8 @@ class ServeConfig:
     weights_path: str = ""
     stub_tokens: int = 50
     stub_token_delay_ms: int = 50
+    dp_prefix: str = ""          # shared-memory ring name prefix of a DP group (default from MASTER_PORT)
+    dp_worker_timeout_ms: int = 10000
 
     @classmethod
     def from_env(cls) -> "ServeConfig":
@@ -88,6 +90,8 @@ class ServeConfig:
         c.weights_path = _env("WEIGHTS_PATH", c.weights_path)
         c.stub_tokens = _env("STUB_TOKENS", c.stub_tokens, int)
         c.stub_token_delay_ms = _env("STUB_TOKEN_DELAY_MS", c.stub_token_delay_ms, int)
+        c.dp_prefix = _env("DP_PREFIX", c.dp_prefix)
+        c.dp_worker_timeout_ms = _env("DP_WORKER_TIMEOUT_MS", c.dp_worker_timeout_ms, int)
         return c
 
     @classmethod
@@ -102,6 +106,17 @@ class ServeConfig:
             if v is not None:
                 setattr(self, f.name, v)
         return self
+
+    def to_json(self) -> str:
+        import json
+
+        return json.dumps(asdict(self))
+
+    @classmethod
+    def from_json(cls, s: str) -> "ServeConfig":
+        import json
+
+        return cls(**json.loads(s))
 
     def runtime_dict(self) -> dict:
         d = asdict(self)

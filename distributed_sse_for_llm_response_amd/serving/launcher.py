@@ -68,13 +68,22 @@ class TPLeaderLoop(EngineLoop):
 
 
 def serve_main(cfg: ServeConfig) -> int:
+    if cfg.dp > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        from .dp import spawn_dp
+
+        return spawn_dp(cfg, cfg.dp)
+    if cfg.dp > 1:
+        # DP replicas share nothing on the token path: no process group is needed
+        from .dp import serve_dp
+
+        rank, local, world = (int(os.environ.get(k, d)) for k, d in (("RANK", "0"), ("LOCAL_RANK", "0"),
+                                                                     ("WORLD_SIZE", "1")))
+        if cfg.engine == "gpu":
+            torch.cuda.set_device(local)
+        return serve_dp(cfg, rank, local, world)
     rank, local, world = init_distributed()
     if cfg.engine == "gpu":
         torch.cuda.set_device(local)
-    if world > 1 and cfg.dp > 1:
-        from .dp import serve_dp
-
-        return serve_dp(cfg, rank, local, world)
     if world > 1:
         comm = TPComm(rank=rank, size=world, group=None)
         if rank == 0:

@@ -1,0 +1,50 @@
+"""bench.py contract on CPU (tiny model): one JSON line with the driver's fields, for 1 rank and for 2
+ranks under torchrun (gloo), through the full serving path (client -> router -> replicas -> SSE)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{\"metric\"")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_contract(world):
+    args = ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--streams", "3", "--prompt-len", "24"]
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    if world == 1:
+        cmd = [sys.executable, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == world and d["steps"] == 3 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["config"]["global_batch"] == 3 * world and d["config"]["parallelism"] == f"dp{world}"
+    assert d["value"] > 0 and d["client_errors"] == []
+    assert d["tokens_delivered_in_window"] >= 3 * world * 2

@@ -1,0 +1,187 @@
+"""Data-parallel serving on CPU: the C++ router + shared-memory rings (csrc/runtime/dp.h) with fake
+engine workers (threads), worker-failure requeue, and the real `serve --dp 2 --engine cpu` launcher."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+import uuid
+
+import pytest
+
+from distributed_sse_for_llm_response_amd import runtime as rtmod
+from distributed_sse_for_llm_response_amd.utils.sse_client import request
+
+H = "127.0.0.1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _router(workers, timeout_ms=10000):
+    mod = rtmod.load()
+    rt = mod.Runtime({"sse_port": 0, "origin_port": 0, "metrics_port": 0, "resp_port": -1, "io_threads": 2,
+                      "host": H, "local_engine": True})
+    rt.set_vocab([f"tok{i}" for i in range(100)])
+    prefix = f"/dsse-test-{uuid.uuid4().hex[:8]}"
+    rt.start_dp_router(prefix, workers, 1, timeout_ms)
+    rt.start()
+    return rt, prefix
+
+
+class FakeWorker(threading.Thread):
+    """Streams `n` tokens (ids 10, 11, ...) for each routed request; can go silent to simulate a crash."""
+
+    def __init__(self, prefix, rank, n=5, die_after_requests=None):
+        super().__init__(daemon=True)
+        self.chan = rtmod.load().DpWorker(prefix, rank, 5000)
+        self.rank, self.n, self.die_after = rank, n, die_after_requests
+        self.served = []
+        self.stop = threading.Event()
+
+    def run(self):
+        self.chan.set_ready(True)
+        while not self.stop.is_set() and not self.chan.shutdown_requested():
+            for req in self.chan.poll_requests(16, 50):
+                self.served.append(req["conversation_id"])
+                if self.die_after is not None and len(self.served) >= self.die_after:
+                    return  # crash: no tokens, no bye, no heartbeats
+                c = req["conversation_id"]
+                self.chan.publish_tokens([c] * self.n, list(range(10, 10 + self.n)), list(range(1, self.n + 1)),
+                                         [False] * self.n, 0, [])
+                self.chan.publish_tokens([c], [-1], [self.n + 1], [True], 0, ["[DONE]"])
+            self.chan.observe(0.005, 1.0, 100.0, 1.0, [0.01], [0.005])
+
+
+def _chat(port, msg="hi", conv=None):
+    body = {"message": msg}
+    if conv:
+        body["conversation_id"] = conv
+    r = request(H, port, "POST", "/chat", body, timeout=30)
+    return r, [e.json() for e in r.events if e.event == "token"]
+
+
+def test_router_spreads_requests_and_resolves_vocab():
+    rt, prefix = _router(2)
+    ws = [FakeWorker(prefix, 0), FakeWorker(prefix, 1)]
+    try:
+        for w in ws:
+            w.start()
+        deadline = time.time() + 10
+        while time.time() < deadline and not all(i["ready"] for i in rt.dp_workers()):
+            time.sleep(0.02)
+        port = rt.bound_port("edge")
+        results = [None] * 6
+
+        def one(i):
+            results[i] = _chat(port, conv=f"c{i}")
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(30)
+        for i, (r, toks) in enumerate(results):
+            assert r.status == 200
+            assert [t["token"] for t in toks] == ["tok10", "tok11", "tok12", "tok13", "tok14", "[DONE]"]
+            assert [t["sequence"] for t in toks] == [1, 2, 3, 4, 5, 6]
+            assert all(t["conversation_id"] == f"c{i}" for t in toks)
+        assert len(ws[0].served) > 0 and len(ws[1].served) > 0
+        assert len(ws[0].served) + len(ws[1].served) == 6
+        m = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
+        assert "dp_workers_alive 2" in m
+        assert "dp_requests_routed_total 6" in m
+        assert all(i["outstanding"] == 0 for i in rt.dp_workers())
+    finally:
+        for w in ws:
+            w.stop.set()
+        rt.stop()
+
+
+def test_router_requeues_from_a_dead_worker():
+    rt, prefix = _router(2, timeout_ms=800)
+    good, bad = FakeWorker(prefix, 0), FakeWorker(prefix, 1, die_after_requests=1)
+    try:
+        good.start()
+        bad.start()
+        deadline = time.time() + 10
+        while time.time() < deadline and not all(i["ready"] for i in rt.dp_workers()):
+            time.sleep(0.02)
+        port = rt.bound_port("edge")
+        results = {}
+
+        def one(c):
+            results[c] = _chat(port, conv=c)
+
+        ts = [threading.Thread(target=one, args=(f"r{i}",)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(30)
+        assert len(bad.served) == 1  # it took one request and died
+        for c, (r, toks) in results.items():
+            assert r.status == 200, c
+            assert toks[-1]["done"] and toks[-1]["token"] == "[DONE]", (c, toks)
+            assert len(toks) == 6
+        assert bad.served[0] in good.served  # restarted from the prompt on the live worker
+        info = rt.dp_workers()
+        assert info[1]["alive"] is False and info[0]["alive"] is True
+        m = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
+        assert "dp_worker_failures_total 1" in m and "dp_requeued_total 1" in m
+    finally:
+        good.stop.set()
+        rt.stop()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind((H, 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_serve_dp2_cpu_engines_end_to_end():
+    sse, met = _free_port(), _free_port()
+    env = dict(os.environ, MASTER_PORT=str(_free_port()), PYTHONPATH=ROOT)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.Popen([sys.executable, "-m", "distributed_sse_for_llm_response_amd", "serve", "--dp", "2",
+                          "--engine", "cpu", "--host", H, "--sse-port", str(sse), "--origin-port", "-1",
+                          "--metrics-port", str(met), "--max-tokens", "6", "--temperature", "0"],
+                         env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        deadline = time.time() + 240
+        ready = False
+        while time.time() < deadline and p.poll() is None:
+            try:
+                ready = request(H, met, "GET", "/metrics", timeout=2).body.decode().count("dp_workers_alive 2") == 1
+            except OSError:
+                ready = False
+            if ready:
+                break
+            time.sleep(0.5)
+        assert ready, p.stdout.read() if p.poll() is not None else "router never saw 2 workers"
+        outs = [None] * 4
+
+        def one(i):
+            outs[i] = _chat(sse, msg="hello there", conv=f"dp{i}")
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        for r, toks in outs:
+            assert r.status == 200
+            assert toks[-1]["done"] and 2 <= len(toks) <= 7
+            assert [t["sequence"] for t in toks] == list(range(1, len(toks) + 1))
+        # greedy + same seed on both replicas: the same prompt gives the same text on either GPU
+        texts = {"".join(t["token"] for t in toks[:-1]) for _, toks in outs}
+        assert len(texts) == 1
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
