@@ -32,7 +32,8 @@ class TPComm:
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         """out: [size * numel(inp)] contiguous."""
         if self.size > 1:
-            dist.all_gather_into_tensor(out, inp, group=self.group)
+            # flat views: RCCL accepts stacked outputs, gloo only the dim-0 concatenation
+            dist.all_gather_into_tensor(out.view(-1), inp.contiguous().view(-1), group=self.group)
         else:
             out.copy_(inp.view(-1)[: out.numel()].view_as(out))
 

@@ -33,9 +33,10 @@ def build_engine(cfg: ServeConfig, device=None, comm=None):
 
     if cfg.engine == "cpu":
         mcfg = TINY if cfg.model.startswith("mistral-7b") else get_config(cfg.model)
-        w = convert_standard(mcfg, init_standard_weights(mcfg, seed=cfg.seed))
+        tp_rank, tp = (comm.rank, comm.size) if comm is not None else (0, 1)
+        w = convert_standard(mcfg, init_standard_weights(mcfg, seed=cfg.seed), tp_rank=tp_rank, tp_size=tp)
         runner = ModelRunner(w, num_blocks=256, max_batch=min(cfg.max_batch, 8),
-                             max_model_len=min(cfg.max_model_len, 1024), device="cpu", use_graphs=False)
+                             max_model_len=min(cfg.max_model_len, 1024), device="cpu", comm=comm, use_graphs=False)
     else:
         device = device or torch.device("cuda", torch.cuda.current_device())
         mcfg = get_config(cfg.model)

@@ -81,13 +81,18 @@ def serve_main(cfg: ServeConfig) -> int:
         if cfg.engine == "gpu":
             torch.cuda.set_device(local)
         return serve_dp(cfg, rank, local, world)
-    rank, local, world = init_distributed()
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    device = None
     if cfg.engine == "gpu":
-        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+    rank, local, world = init_distributed(backend="nccl" if cfg.engine == "gpu" else "gloo", device=device)
     if world > 1:
+        if cfg.tp not in (1, world):
+            raise ValueError(f"TP={cfg.tp} but WORLD_SIZE={world}: one TP group spans the whole launch (use DP for replicas)")
         comm = TPComm(rank=rank, size=world, group=None)
         if rank == 0:
-            app = ServingApp(cfg, device=torch.device("cuda", local), comm=comm)
+            app = ServingApp(cfg, device=device, comm=comm)
             app.rt.start()
             app.loop = TPLeaderLoop(app.rt, app.engine, app.tok, cfg)
             app.loop.start()
@@ -96,7 +101,7 @@ def serve_main(cfg: ServeConfig) -> int:
                   flush=True)
             app.serve_forever()
         else:
-            engine, tok = build_engine(cfg, device=torch.device("cuda", local), comm=comm)
+            engine, tok = build_engine(cfg, device=device, comm=comm)
             TPFollowerLoop(engine, tok, cfg).run()
         return 0
     app = ServingApp(cfg).start()

@@ -1,0 +1,150 @@
+"""Tensor parallelism on CPU (gloo, 2 ranks): Megatron-sharded weights, two all-reduces per layer and the
+vocab-parallel sampler must reproduce the TP=1 / fp32 reference generation, identically on every rank."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
+from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights, reference_forward
+from distributed_sse_for_llm_response_amd.parallel.comm import TPComm
+
+PROMPTS = [[5, 17, 99, 3, 8, 1000, 42], list(range(100, 150)), [7] * 33]
+BTS = [[0, 1, 2], [10, 4, 5, 6], [20, 21, 22]]
+STEPS = 5
+
+
+def _generate(rank, world, temperature):
+    cfg = TINY
+    std = init_standard_weights(cfg, seed=3)
+    comm = TPComm(rank=rank, size=world, group=None) if world > 1 else TPComm()
+    w = convert_standard(cfg, std, tp_rank=rank, tp_size=world)
+    r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device="cpu", comm=comm, use_graphs=False)
+    for i, bt in enumerate(BTS):
+        r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    r.temperature[:3] = temperature
+    r.seeds[:3, 0] = torch.tensor([11, 22, 33], dtype=torch.int32)
+    r.prefill([PrefillSeq(i, p, 0, BTS[i], True) for i, p in enumerate(PROMPTS)], ring_row=0)
+    r.active[:3] = 1
+    gen = [[int(r.ids[i])] for i in range(3)]
+    for _ in range(STEPS):
+        r.decode(4)
+        for i in range(3):
+            gen[i].append(int(r.ids[i]))
+    return gen
+
+
+def _worker(rank, world, port, temperature, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out[rank] = _generate(rank, world, temperature)
+    finally:
+        dist.destroy_process_group()
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_run(world, temperature):
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, _port(), temperature, out), nprocs=world, join=True)
+        return [out[r] for r in range(world)]
+
+
+@pytest.mark.timeout(600)
+def test_tp2_greedy_matches_reference_and_tp1():
+    res = _tp_run(2, 0.0)
+    assert res[0] == res[1], "TP ranks disagree on the sampled tokens"
+    gen = res[0]
+    std = init_standard_weights(TINY, seed=3)
+    worst = 0.0
+    for i in range(3):
+        logits, _ = reference_forward(TINY, std, torch.tensor(PROMPTS[i] + gen[i]))
+        L = len(PROMPTS[i])
+        for j, g in enumerate(gen[i]):
+            row = logits[L - 1 + j]
+            worst = max(worst, float(row.max() - row[g]))
+    assert worst < 0.05
+    assert gen == _generate(0, 1, 0.0)
+
+
+@pytest.mark.timeout(600)
+def test_tp2_stochastic_sampling_is_tp_invariant():
+    """Gumbel-max keyed by (seed, position, global vocab index): the same draw at TP=1 and TP=2."""
+    res = _tp_run(2, 1.0)
+    assert res[0] == res[1]
+    assert res[0] == _generate(0, 1, 1.0)
+
+
+def _free_port():
+    return _port()
+
+
+@pytest.mark.timeout(600)
+def test_serve_tp2_cpu_end_to_end():
+    """`torchrun --nproc-per-node 2 ... serve --engine cpu`: rank 0 serves SSE, both ranks step the sharded model."""
+    import subprocess
+    import sys
+    import threading
+    import time
+
+    from distributed_sse_for_llm_response_amd.utils.sse_client import request
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sse, met = _free_port(), _free_port()
+    env = dict(os.environ, PYTHONPATH=root)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          "-m", "distributed_sse_for_llm_response_amd", "serve", "--engine", "cpu", "--tp", "2",
+                          "--host", "127.0.0.1", "--sse-port", str(sse), "--origin-port", "-1",
+                          "--metrics-port", str(met), "--max-tokens", "5", "--temperature", "0"],
+                         cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        deadline = time.time() + 240
+        ok = False
+        while time.time() < deadline and p.poll() is None:
+            try:
+                ok = request("127.0.0.1", sse, "GET", "/readyz", timeout=2).status == 200
+            except OSError:
+                ok = False
+            if ok:
+                break
+            time.sleep(0.5)
+        assert ok, p.stdout.read() if p.poll() is not None else "TP server never became ready"
+        outs = [None] * 3
+
+        def one(i):
+            r = request("127.0.0.1", sse, "POST", "/chat", {"message": "same prompt", "conversation_id": f"tp{i}"},
+                        timeout=120)
+            outs[i] = [e.json() for e in r.events if e.event == "token"]
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        texts = set()
+        for toks in outs:
+            assert toks and toks[-1]["done"]
+            assert [t["sequence"] for t in toks] == list(range(1, len(toks) + 1))
+            texts.add("".join(t["token"] for t in toks[:-1]))
+        assert len(texts) == 1  # greedy: identical prompts give identical streams
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
