@@ -1,0 +1,245 @@
+// Flash prefill attention on MFMA for gfx950 (K12 of SURVEY.md §2.4): causal, GQA, paged KV,
+// chunked prefill (queries = the last q_len positions of a ctx_len context).
+//
+// Measured need (profiles/ttft_r1.md): the decode-derived kernel in attention.hip (no LDS, K/V read
+// straight from the paged cache by every wave) ran an 8k-token causal prefill at ~157 TFLOP/s,
+// 56 % of the TTFT.  This kernel is the classic LDS-staged flash structure, laid out for CDNA4:
+//
+//   workgroup  = one KV head x 64 query tokens; 2G waves (G = Hq/Hkv q heads x 2 halves of 32
+//                queries), so every K/V byte staged in LDS feeds 2G waves (GQA reuse in LDS);
+//   key loop   = 64 keys (two 32-token pages) per iteration, double-buffered LDS (2 x 32 KiB);
+//                the next block's K and V are loaded into registers before the MFMAs of this block
+//                and written to the other buffer after them (one barrier per iteration);
+//   scores     = Sᵀ = K·Qᵀ (keys on MFMA rows, queries on lanes): a query's softmax statistics live
+//                in one lane column, and the exponentiated scores are already the B operand of
+//                Oᵀ = Vᵀ·Pᵀ — the V cache stores each page transposed with the token permutation
+//                vperm(), so lane group g's 8 keys {4g..4g+3, 16+4g..16+4g+3} are one 16-byte run;
+//   LDS images = K [64 keys][256 B] with the XOR-swizzled 16-byte chunks of gemm_xlds, Vᵀ [128 d]
+//                [128 B] with chunk ^= (d >> 1) & 7: both read with conflict-free ds_read_b128;
+//   softmax    = online, base 2, masked scores contribute exactly 0 (fully masked columns stay 0).
+#include "api.h"
+
+namespace dsse {
+
+namespace {
+constexpr int kD = 128;
+constexpr int kBQ = 64;    // query tokens per workgroup
+constexpr int kBK = 64;    // keys per iteration (2 pages)
+constexpr int kKBytes = kBK * kD * 2;  // 16 KiB
+constexpr int kStage = 2 * kKBytes;    // K + Vᵀ
+}  // namespace
+
+template <int G>
+__global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
+  constexpr int NW = 2 * G;
+  constexpr int NT = 64 * NW;
+  constexpr int PIECES = kStage / 16;  // 16-byte pieces per stage = 2048
+  constexpr int PPT = PIECES / NT;             // pieces per thread
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int wh = w % G, wq = w / G;
+  const int item = blockIdx.x, h = blockIdx.y;
+  const int b = p.work_seq[item];
+  const int qlen = p.q_len[b], ctx = p.ctx_len[b];
+  const int pos0 = ctx - qlen;                 // absolute position of query 0 of this chunk
+  const int tile = p.work_tile[item];
+  const int q0 = tile * kBQ + wq * 32;         // this wave's first query (within the chunk)
+  const int wg_last_q = min(qlen, (tile + 1) * kBQ) - 1;
+  if (tile * kBQ >= qlen) return;              // uniform
+  const int kmax = pos0 + wg_last_q + 1;       // keys [0, kmax) are visible to some query of the WG
+  const int nblk = (kmax + kBK - 1) / kBK;
+  const int w_last_pos = pos0 + min(qlen, q0 + 32) - 1;  // last visible key of this wave
+  const int w_first_pos = pos0 + q0;
+  const int head = h * G + wh;
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  const int npages = (kmax + kBS - 1) / kBS;
+
+  // Q fragments (B operand of Sᵀ = K·Qᵀ): lane (r, g) holds Q[query 16qt + r][d = 32g + 8s + j]
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = min(q0 + 16 * qt + r, qlen - 1);
+    const bf16* qp = p.q + ((size_t)(p.q_start[b] + qi) * p.hq + head) * kD + 32 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[qt][s] = ld_bf16x8(qp + 8 * s);
+  }
+
+  // ---- staging: pieces [0, 1024) = K (page, token, 16-byte chunk), [1024, 2048) = V (page, d, chunk)
+  bf16x8 st[PPT];
+  auto load_block = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int pc = threadIdx.x + i * NT;
+      const int v = pc >> 10, off = pc & 1023;
+      const int page = off >> 9, o2 = off & 511;
+      const int pg = min(2 * j + page, npages - 1);  // pages past the context: harmless re-read, masked
+      const int blk = bt[pg];
+      const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
+                               : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
+      st[i] = ld_bf16x8(src);
+    }
+  };
+  auto store_block = [&](int buf) {
+    char* base = smem + buf * kStage;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int pc = threadIdx.x + i * NT;
+      const int v = pc >> 10, off = pc & 1023;
+      const int page = off >> 9, o2 = off & 511;
+      int dst;
+      if (v == 0) {
+        const int key = page * kBS + (o2 >> 4), c = o2 & 15;
+        dst = key * 256 + ((c ^ swz(key & 15)) << 4);
+      } else {
+        const int d = o2 >> 2, c = page * 4 + (o2 & 3);
+        dst = kKBytes + d * 128 + ((c ^ ((d >> 1) & 7)) << 4);
+      }
+      *reinterpret_cast<bf16x8*>(base + dst) = st[i];
+    }
+  };
+
+  f32x4 o[8][2];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+  const float sc = p.scale_log2;
+
+  load_block(0);
+  store_block(0);
+  for (int j = 0; j < nblk; ++j) {
+    __syncthreads();
+    const bool more = j + 1 < nblk;
+    if (more) load_block(j + 1);
+    const int key0 = j * kBK;
+    if (key0 <= w_last_pos) {  // this wave sees at least one key of the block
+      const char* kb = smem + (j & 1) * kStage;
+      const char* vb = kb + kKBytes;
+      // Sᵀ[key tile kt][query tile qt]
+      f32x4 s4[4][2];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = 16 * kt + r;
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 256 + (((4 * g + s) ^ swz(r)) << 4));
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
+        }
+      }
+      const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
+      bf16x8 pf[2][2];  // [qt][page t]
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int qpos = pos0 + q0 + 16 * qt + r;
+        const bool qvalid = q0 + 16 * qt + r < qlen;
+        float mx = -1e30f;
+        if (need_mask) {
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int key = key0 + 16 * kt + 4 * g + i;
+              const float v = (qvalid && key <= qpos) ? s4[kt][qt][i] * sc : -1e30f;
+              s4[kt][qt][i] = v;
+              mx = fmaxf(mx, v);
+            }
+        } else {
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = s4[kt][qt][i] * sc;
+              s4[kt][qt][i] = v;
+              mx = fmaxf(mx, v);
+            }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run[qt], mx);
+        // raw v_exp_f32 (no denormal range reduction: arguments are <= 0 and underflow to 0 is wanted);
+        // a column with no visible key yet keeps m = -1e30 and must produce p = 0, not exp2(0)
+        const float m_use = m_new < -1e29f ? 0.f : m_new;
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qt] - m_use);
+        float sum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float e = __builtin_amdgcn_exp2f(s4[kt][qt][i] - m_use);
+            s4[kt][qt][i] = e;
+            sum += e;
+          }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        l_run[qt] = l_run[qt] * alpha + sum;
+        m_run[qt] = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          o[dt][qt][0] *= alpha;
+          o[dt][qt][1] *= alpha;
+          o[dt][qt][2] *= alpha;
+          o[dt][qt][3] *= alpha;
+        }
+        // Pᵀ fragments: page t = key tiles 2t (keys 4g+i) and 2t+1 (keys 16+4g+i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            pf[qt][t][i] = f2bf(s4[2 * t][qt][i]);
+            pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
+          }
+      }
+      // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          const int d = 16 * dt + r;
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vb + d * 128 + (((t * 4 + g) ^ ((d >> 1) & 7)) << 4));
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
+        }
+    }
+    if (more) store_block((j + 1) & 1);
+  }
+
+  // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + 16 * qt + r;
+    if (qi >= qlen) continue;
+    const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
+    bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + head) * kD + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16x4 v;
+      v[0] = f2bf(o[dt][qt][0] * inv);
+      v[1] = f2bf(o[dt][qt][1] * inv);
+      v[2] = f2bf(o[dt][qt][2] * inv);
+      v[3] = f2bf(o[dt][qt][3] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
+    }
+  }
+}
+
+}  // namespace dsse
+
+// Work items: (sequence, 64-query tile) pairs; grid = (num_work, Hkv).  Requires G = Hq/Hkv in {1, 2, 4}.
+extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
+  using namespace dsse;
+  if (num_work <= 0) return hipSuccess;
+  const dim3 grid(num_work, p->hkv);
+  switch (p->group) {
+    case 1: hipLaunchKernelGGL(flash_prefill_kernel<1>, grid, dim3(128), 0, st, *p); break;
+    case 2: hipLaunchKernelGGL(flash_prefill_kernel<2>, grid, dim3(256), 0, st, *p); break;
+    case 4: hipLaunchKernelGGL(flash_prefill_kernel<4>, grid, dim3(512), 0, st, *p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}

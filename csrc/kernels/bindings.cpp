@@ -383,6 +383,8 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
   const int num_work = (int)work_seq.numel();
   TORCH_CHECK(work_tile.numel() == num_work, "work lists differ in length");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 decode, 1 prefill (16-query tiles), 2 flash prefill (64-query tiles)");
+  if (mode == 2) TORCH_CHECK(hq / hkv == 1 || hq / hkv == 2 || hq / hkv == 4, "flash prefill supports G in {1, 2, 4}");
   const int kwv = mode == 0 ? 4 : 1, qw = mode == 0 ? 1 : 4;
   TORCH_CHECK(part % (32 * kwv) == 0 && part > 0, "partition size must be a multiple of ", 32 * kwv);
   TORCH_CHECK(nparts >= 1, "nparts >= 1");
@@ -412,7 +414,8 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   p.part = (int)part;
   p.nparts = (int)nparts;
   p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
-  DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
+  if (mode == 2) DSSE_CHECK_HIP(dsse_flash_prefill(num_work, &p, cur_stream()));
+  else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
 }
 
 dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,

@@ -57,6 +57,11 @@ DEV T wave_sum(T v) {
   return v;
 }
 
+// 16-byte chunk swizzle inside each 256-byte window of an LDS row: conflict-free ds_read_b128 for the
+// MFMA operand pattern "lane l reads row l & 15, chunk 4 (l >> 4) + s" (X tiles of the decode GEMMs,
+// K tiles of the flash prefill).  Apply as chunk ^ swz(row & 15) on both the write and the read.
+DEV int swz(int row) { return row ^ ((((row >> 2) ^ (row >> 3)) & 1) << 2); }
+
 DEV float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 // Philox4x32-10 counter-based RNG (one 32-bit output used per call site).

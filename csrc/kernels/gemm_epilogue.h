@@ -10,10 +10,6 @@ constexpr int kPartial = 5;  // internal mode: write fp32 split-K partial slabs 
 
 DEV int vperm_tok(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4 + (off & 3); }
 
-// 16-byte chunk swizzle inside each 256-byte window of an LDS row of X: conflict-free ds_read_b128
-// for the MFMA A-operand pattern (lane l reads row l & 15, chunk 4(l >> 4) + s).
-DEV int swz(int row) { return row ^ ((((row >> 2) ^ (row >> 3)) & 1) << 2); }
-
 template <int MODE>
 DEV void epilogue(const GemmEpi& ep, float* part, int M, int N, int m, int tile, int r, float v, float partner) {
   if (m >= M) return;

@@ -35,6 +35,7 @@ from .weights import EngineWeights
 
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
+PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
 
 
 def batch_buckets(max_batch: int):
@@ -245,9 +246,14 @@ class ModelRunner:
             q_len.append(len(s.tokens))
             ctx_len.append(s.start_pos + len(s.tokens))
             bt[i, : len(s.block_table)] = torch.tensor(s.block_table, dtype=torch.int32)
-            for tile in range(math.ceil(len(s.tokens) / 16)):
+            for tile in range(math.ceil(len(s.tokens) / PREFILL_TILE)):
                 work_seq.append(i)
                 work_tile.append(tile)
+        # flash prefill: heaviest (most keys) 64-query tiles first, so the causal tail balances over the CUs
+        order = sorted(range(len(work_seq)), key=lambda k: -(ctx_len[work_seq[k]] - q_len[work_seq[k]]
+                                                              + min(q_len[work_seq[k]], (work_tile[k] + 1) * PREFILL_TILE)))
+        work_seq = [work_seq[k] for k in order]
+        work_tile = [work_tile[k] for k in order]
         T = len(ids)
         meta = torch.tensor(ids + pos + slots + q_start + q_len + ctx_len + work_seq + work_tile, dtype=torch.int32)
         if dev.type == "cuda":
@@ -278,7 +284,7 @@ class ModelRunner:
             qkv = x @ L.wqkv.t()
             ops.rope_kv_write(qkv, d_pos, d_slots, self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             del qkv
-            ops.paged_attention(1, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
+            ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
                                 self.part_o, self.part_ml, part, 1)
             o_proj = attn.view(T, nh * 128) @ L.wo.t()
             comm.all_reduce(o_proj)

@@ -139,7 +139,8 @@ def ring_advance(counter):
 
 def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, out,
                     part_o, part_ml, part, nparts):
-    """mode 0 = decode (flash-decoding partitions), mode 1 = prefill (causal, one partition)."""
+    """mode 0 = decode (flash-decoding partitions), 1 = prefill on 16-query tiles (decode-style kernel),
+    2 = flash prefill on 64-query tiles (LDS-staged K/V, attention_prefill.hip)."""
     if _hip(q):
         torch.ops.dsse.paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
                                        work_tile, out, part_o, part_ml, part, nparts)

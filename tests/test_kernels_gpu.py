@@ -208,16 +208,20 @@ def test_paged_attention_decode(gpu, ctxs, part):
     _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention")
 
 
-@pytest.mark.parametrize("case", [([45], [45]), ([300, 17], [300, 17]), ([700, 64], [100, 64]), ([4096], [1000])])
-def test_paged_attention_prefill(gpu, case):
+@pytest.mark.parametrize("mode,hq", [(1, 32), (2, 32), (2, 16), (2, 8)])
+@pytest.mark.parametrize("case", [([45], [45]), ([300, 17], [300, 17]), ([700, 64], [100, 64]), ([4096], [1000]),
+                                  ([129, 1], [65, 1])])
+def test_paged_attention_prefill(gpu, case, mode, hq):
+    """mode 1: decode-style kernel on 16-query tiles; mode 2: flash prefill on 64-query tiles (G = hq / 8)."""
     ctxs, qlens = case
-    g = torch.Generator().manual_seed(sum(ctxs))
+    g = torch.Generator().manual_seed(sum(ctxs) + hq)
     B = len(ctxs)
-    kc, vc, bt, q, q_start = _attn_setup(ctxs, qlens, gen=g)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, qlens, hq=hq, gen=g)
     qlen, ctx = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
+    tile = 16 if mode == 1 else 64
     ws, wt = [], []
     for b in range(B):
-        for t in range(math.ceil(qlens[b] / 16)):
+        for t in reversed(range(math.ceil(qlens[b] / tile))):
             ws.append(b)
             wt.append(t)
     ws, wt = torch.tensor(ws, dtype=torch.int32), torch.tensor(wt, dtype=torch.int32)
@@ -225,10 +229,10 @@ def test_paged_attention_prefill(gpu, case):
     out = torch.zeros_like(q)
     out_g = torch.zeros_like(q).to(gpu)
     dummy = torch.zeros(1, device=gpu)
-    ops.paged_attention(1, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
-                        ws.to(gpu), wt.to(gpu), out_g, dummy, dummy, part, 1)
-    R.paged_attention(1, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
-    _close(out_g, out, 1e-2, 2e-2, "prefill attention")
+    ops.paged_attention(mode, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu),
+                        ctx.to(gpu), ws.to(gpu), wt.to(gpu), out_g, dummy, dummy, part, 1)
+    R.paged_attention(mode, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
+    _close(out_g, out, 1e-2, 2e-2, f"prefill attention mode {mode}")
 
 
 def _sampler_inputs(B, V, gen, temps, topk, topp):
