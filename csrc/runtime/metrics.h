@@ -76,6 +76,9 @@ class Metrics {
   Counter dp_requests_routed_total;
   Counter dp_requeued_total;
   Counter dp_worker_failures_total;
+  // edge relay (relay.h)
+  Gauge relay_upstream_connections;
+  Counter relay_frames_total;
 
   std::string render() const;        // full exposition for :9090/metrics
   std::string render_origin() const;  // "active_chats N\n" (origin /metrics)

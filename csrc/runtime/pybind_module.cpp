@@ -53,6 +53,7 @@ class Runtime {
     c.resp_port = geti("resp_port", c.resp_port);
     c.io_threads = geti("io_threads", c.io_threads);
     c.llm_proxy_url = gets("llm_proxy_url", "");
+    c.upstream_url = gets("upstream_url", "");
     c.local_engine = cfg.contains("local_engine") && cfg["local_engine"].cast<bool>();
     c.model_name = gets("model_name", c.model_name);
     c.inspection = parse_inspection_mode(gets("inspection_mode", "disabled"));

@@ -831,6 +831,7 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
     c.sink = sink;
     srv_.bus().subscribe(conv, sink, -1, nullptr);
     start_sse(c, conv, true, -1, "event: connected\ndata: {\"conversation_id\":" + json_quote(conv) + "}\n\n", nullptr);
+    srv_.relay_ensure(conv);
     if (local) {
       ChatRequest r;
       r.conversation_id = conv;
@@ -875,6 +876,7 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
     std::vector<FramePtr> replay;
     srv_.bus().subscribe(conv, sink, after, after >= 0 ? &replay : nullptr);
     start_sse(c, conv, false, after, ": connected to " + conv + "\n\n", &replay);
+    srv_.relay_ensure(conv);
     return;
   }
   if (path.rfind("/publish/", 0) == 0) {
@@ -1090,6 +1092,10 @@ bool Server::start(std::string* err) {
     }
     io_.push_back(std::move(io));
   }
+  if (!cfg_.upstream_url.empty()) {
+    relay_ = std::make_unique<UpstreamRelay>(*bus_, cfg_.upstream_url);
+    if (!relay_->start(err)) return false;
+  }
   running_.store(true);
   for (auto& io : io_) threads_.emplace_back([p = io.get()] { p->run(); });
   housekeeping_ = std::thread([this] {
@@ -1114,6 +1120,8 @@ void Server::stop() {
   for (auto& t : threads_) t.join();
   threads_.clear();
   if (housekeeping_.joinable()) housekeeping_.join();
+  if (relay_) relay_->stop();
+  relay_.reset();
   io_.clear();
 }
 

@@ -31,6 +31,7 @@
 
 #include "bus.h"
 #include "inspector.h"
+#include "relay.h"
 
 namespace dsse {
 
@@ -42,6 +43,7 @@ struct ServerConfig {
   int resp_port = -1;       // < 0 = disabled (6379 for the load-generator producer)
   int io_threads = 4;
   std::string llm_proxy_url;  // edge mode: forward POST /chat here when no local engine is attached
+  std::string upstream_url;   // edge mode: relay conversations from this origin SSE endpoint (relay.h)
   bool local_engine = false;  // POST /chat goes straight into the in-process request queue
   std::string model_name = "mistralai/Mistral-7B-Instruct-v0.3";
   InspectionMode inspection = InspectionMode::kDisabled;
@@ -109,6 +111,10 @@ class Server {
   void note_cancel(const std::string& conv_id);
   bool local_engine() const { return local_engine_.load(); }
   bool ready() const { return ready_.load(); }
+  // Edge without a local engine: start relaying `conv_id` from the upstream origin (no-op otherwise).
+  void relay_ensure(const std::string& conv_id) {
+    if (relay_ && !local_engine_.load()) relay_->ensure(conv_id);
+  }
   void forward_to_proxy(uint64_t conn_id, IoThread* io, const std::string& conv_id, const std::string& message);
 
  private:
@@ -118,6 +124,7 @@ class Server {
   std::vector<std::unique_ptr<IoThread>> io_;
   std::vector<std::thread> threads_;
   std::thread housekeeping_;
+  std::unique_ptr<UpstreamRelay> relay_;
   std::atomic<bool> running_{false};
   std::atomic<bool> local_engine_{false};
   std::atomic<bool> ready_{true};

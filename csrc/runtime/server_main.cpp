@@ -3,10 +3,13 @@
 // generator (STUB_TOKENS > 0) or LLM_PROXY_URL forwarding.  Environment variables follow the reference
 // services (src/sse-adapter/main.go:29-40, src/llm-stream-proxy/main.go:70-96):
 //   SSE_PORT (8080) METRICS_PORT (9090) ORIGIN_PORT (8081, or PORT) RESP_PORT (-1 = off; 6379)
-//   LLM_PROXY_URL INSPECTION_MODE INSPECTION_BUFFER_MS LOG_LEVEL IO_THREADS
-//   STUB_TOKENS (50; 0 = no stub) STUB_TOKEN_DELAY_MS (50) STUB_WORKERS (2)
+//   LLM_PROXY_URL UPSTREAM_URL (edge: relay tokens from the origin's SSE port) INSPECTION_MODE
+//   INSPECTION_BUFFER_MS LOG_LEVEL IO_THREADS
+//   UI_PATH (chat page served at GET /) STUB_TOKENS (50; 0 = no stub) STUB_TOKEN_DELAY_MS (50) STUB_WORKERS (2)
 #include <csignal>
 #include <cstdio>
+#include <fstream>
+#include <sstream>
 #include <thread>
 
 #include "server.h"
@@ -25,6 +28,13 @@ int main() {
   c.resp_port = (int)env_long("RESP_PORT", -1);
   c.io_threads = (int)env_long("IO_THREADS", 4);
   c.llm_proxy_url = env_str("LLM_PROXY_URL", "");
+  c.upstream_url = env_str("UPSTREAM_URL", "");
+  if (const std::string ui = env_str("UI_PATH", ""); !ui.empty()) {  // chat page at GET /
+    std::ifstream f(ui);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    c.ui_html = ss.str();
+  }
   c.inspection = parse_inspection_mode(env_str("INSPECTION_MODE", "disabled"));
   c.inspection_buffer_ms = (int)env_long("INSPECTION_BUFFER_MS", 150);
   const int stub_tokens = (int)env_long("STUB_TOKENS", 50);

@@ -5,6 +5,7 @@ Reference keys (same names, same defaults where they apply here):
   (llm-stream-proxy, src/llm-stream-proxy/main.go:70-96; the origin gets its own port because both
   services default to 8080 and they now share a process), LLM_PROXY_URL, INSPECTION_MODE,
   INSPECTION_BUFFER_MS, LOG_LEVEL, MODEL_NAME, REDIS_ADDR (the RESP ingest port, e.g. ":6379").
+Topology keys (new): UPSTREAM_URL (edge: relay conversations from the origin), UI_PATH.
 Engine keys (new): TP, DP, DP_PREFIX, DP_WORKER_TIMEOUT_MS, MAX_MODEL_LEN, MAX_BATCH, KV_BLOCK (fixed 32), GPU_MEMORY_UTILIZATION,
   SEED, MAX_TOKENS, PREFILL_BUDGET, TOKENIZER_PATH, WEIGHTS_PATH.
 """
@@ -34,6 +35,8 @@ class ServeConfig:
     resp_port: int = -1
     io_threads: int = 4
     llm_proxy_url: str = ""
+    upstream_url: str = ""       # edge: origin SSE endpoint to relay conversations from (csrc/runtime/relay.h)
+    ui_path: str = ""            # chat page served at GET / ("" = the built-in page, "none" = off)
     inspection_mode: str = "disabled"
     inspection_buffer_ms: int = 150
     log_level: str = "info"
@@ -71,6 +74,8 @@ class ServeConfig:
         c.resp_port = _env("RESP_PORT", c.resp_port, int)
         c.io_threads = _env("IO_THREADS", c.io_threads, int)
         c.llm_proxy_url = _env("LLM_PROXY_URL", c.llm_proxy_url)
+        c.upstream_url = _env("UPSTREAM_URL", c.upstream_url)
+        c.ui_path = _env("UI_PATH", c.ui_path)
         c.inspection_mode = _env("INSPECTION_MODE", c.inspection_mode)
         c.inspection_buffer_ms = _env("INSPECTION_BUFFER_MS", c.inspection_buffer_ms, int)
         c.log_level = _env("LOG_LEVEL", c.log_level)
@@ -121,5 +126,13 @@ class ServeConfig:
     def runtime_dict(self) -> dict:
         d = asdict(self)
         keys = ("host", "sse_port", "origin_port", "metrics_port", "resp_port", "io_threads", "llm_proxy_url",
-                "inspection_mode", "inspection_buffer_ms", "model_name", "keepalive_ms", "first_token_timeout_ms")
-        return {k: d[k] for k in keys}
+                "upstream_url", "inspection_mode", "inspection_buffer_ms", "model_name", "keepalive_ms",
+                "first_token_timeout_ms")
+        out = {k: d[k] for k in keys}
+        if self.ui_path != "none":
+            from pathlib import Path
+
+            p = Path(self.ui_path) if self.ui_path else Path(__file__).with_name("static") / "chat.html"
+            if p.exists():
+                out["ui_html"] = p.read_text()
+        return out

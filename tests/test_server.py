@@ -280,3 +280,72 @@ def test_edge_forwards_to_origin_instance():
     finally:
         edge.stop()
         origin.stop()
+
+
+def test_edge_relays_origin_tokens_over_upstream_sse():
+    """Origin -> edge region: the edge forwards POST /chat to the origin API and relays the conversation
+    from the origin's SSE port (one upstream connection, fanned out to every local subscriber)."""
+    origin = make_rt()
+    origin.start_stub(5, 5, 1)
+    edge = make_rt(llm_proxy_url=f"http://127.0.0.1:{origin.bound_port('origin')}",
+                   upstream_url=f"http://127.0.0.1:{origin.bound_port('edge')}")
+    try:
+        ep = edge.bound_port("edge")
+        side = {}
+
+        def watcher():
+            side["r"] = request(H, ep, "GET", "/stream/relay-1", timeout=10)
+
+        t = threading.Thread(target=watcher)
+        t.start()
+        time.sleep(0.2)
+        resp = request(H, ep, "POST", "/chat", {"message": "hi", "conversation_id": "relay-1"}, timeout=10)
+        t.join(10)
+        toks = tokens_of(resp)
+        assert [x["sequence"] for x in toks] == [1, 2, 3, 4, 5, 6]
+        assert toks[-1]["token"] == "[DONE]" and toks[-1]["done"]
+        assert [x["sequence"] for x in tokens_of(side["r"])] == [1, 2, 3, 4, 5, 6]
+        # the origin served the conversation exactly once over its SSE port (the relay)
+        m = request(H, edge.bound_port("metrics"), "GET", "/metrics").body.decode()
+        assert "relay_frames_total 6" in m
+    finally:
+        edge.stop()
+        origin.stop()
+
+
+def test_edge_relay_resumes_with_last_event_id_from_origin_ring(bare_rt):
+    """A conversation already (partly) produced on the origin is replayed to a late edge subscriber."""
+    origin = bare_rt
+    for i in range(1, 4):
+        origin.publish("late-1", f"t{i}", i, False)
+    edge = make_rt(upstream_url=f"http://127.0.0.1:{origin.bound_port('edge')}")
+    try:
+        got = {}
+
+        def watcher():
+            got["r"] = request(H, edge.bound_port("edge"), "GET", "/stream/late-1", timeout=10)
+
+        t = threading.Thread(target=watcher)
+        t.start()
+        time.sleep(0.3)
+        origin.publish("late-1", "t4", 4, False)
+        origin.publish("late-1", "[DONE]", 5, True)
+        t.join(10)
+        assert [x["token"] for x in tokens_of(got["r"])] == ["t1", "t2", "t3", "t4", "[DONE]"]
+    finally:
+        edge.stop()
+
+
+def test_chat_page_served_at_root():
+    from distributed_sse_for_llm_response_amd.serving.config import ServeConfig
+
+    rd = ServeConfig().runtime_dict()
+    assert "<title>MI355X token stream</title>" in rd["ui_html"]
+    r = make_rt(ui_html=rd["ui_html"])
+    try:
+        resp = request(H, r.bound_port("edge"), "GET", "/")
+        assert resp.status == 200
+        assert resp.headers["content-type"].startswith("text/html")
+        assert b"fetch(base + \"/chat\"" in resp.body
+    finally:
+        r.stop()
