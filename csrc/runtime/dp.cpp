@@ -73,6 +73,28 @@ bool DpRouter::start(std::string* err) {
   }
   server_.set_local_engine(true);  // /chat admits into the request queue this router drains
   server_.set_ready(false);
+  // per-GPU series: dp_worker_{up,outstanding,batch_size,kv_blocks_free,active_chats}{worker="g"}
+  metrics().set_extra("dp", [this] {
+    std::string o;
+    const auto ws = workers();
+    const char* names[] = {"dp_worker_up", "dp_worker_outstanding", "dp_worker_batch_size", "dp_worker_kv_blocks_free",
+                           "dp_worker_active_chats"};
+    for (int k = 0; k < 5; ++k) {
+      o += std::string("# TYPE ") + names[k] + " gauge\n";
+      for (size_t w = 0; w < ws.size(); ++w) {
+        const auto& i = ws[w];
+        const double v = k == 0 ? (i.ready && i.alive ? 1.0 : 0.0)
+                         : k == 1 ? (double)i.outstanding
+                         : k == 2 ? i.batch
+                         : k == 3 ? i.kv_free
+                                  : i.active;
+        char b[128];
+        snprintf(b, sizeof b, "%s{worker=\"%zu\"} %.17g\n", names[k], w, v);
+        o += b;
+      }
+    }
+    return o;
+  });
   running_ = true;
   dispatch_ = std::thread([this] { dispatch_loop(); });
   for (int w = 0; w < n_; ++w) drains_.emplace_back([this, w] { drain_loop(w); });
@@ -81,6 +103,7 @@ bool DpRouter::start(std::string* err) {
 
 void DpRouter::stop() {
   if (!running_.exchange(false)) return;
+  metrics().clear_extra("dp");
   {
     dpwire::Writer m;
     m.u8(dpwire::kShutdown);

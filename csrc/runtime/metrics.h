@@ -9,6 +9,8 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -80,8 +82,16 @@ class Metrics {
   Gauge relay_upstream_connections;
   Counter relay_frames_total;
 
+  // Labelled series rendered by their owners (e.g. per-GPU DP worker gauges); appended to render().
+  void set_extra(const std::string& key, std::function<std::string()> fn);
+  void clear_extra(const std::string& key);
+
   std::string render() const;        // full exposition for :9090/metrics
   std::string render_origin() const;  // "active_chats N\n" (origin /metrics)
+
+ private:
+  mutable std::mutex extra_mu_;
+  std::map<std::string, std::function<std::string()>> extra_;
 };
 
 Metrics& metrics();

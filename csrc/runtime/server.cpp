@@ -75,8 +75,12 @@ void RequestQueue::push(ChatRequest r) {
 std::vector<ChatRequest> RequestQueue::pop(size_t max, int timeout_ms) {
   std::vector<ChatRequest> out;
   std::unique_lock<std::mutex> lk(mu_);
+  // system_clock deadline: libstdc++ maps steady-clock waits to pthread_cond_clockwait, which the
+  // ThreadSanitizer runtime of this toolchain does not intercept (it then reports false double locks
+  // and races on everything the mutex protects); pthread_cond_timedwait is understood.
   if (q_.empty() && timeout_ms > 0 && !closed_)
-    cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || closed_; });
+    cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                   [&] { return !q_.empty() || closed_; });
   while (!q_.empty() && out.size() < max) {
     out.push_back(std::move(q_.front()));
     q_.pop_front();

@@ -25,6 +25,7 @@ from ..engine.model_runner import ModelRunner
 from ..models.mistral import TINY, get_config, init_standard_weights
 from ..models.tokenizer import get_tokenizer
 from .config import ServeConfig
+from .faults import FaultPlan, StepTracer, Watchdog
 
 
 def build_engine(cfg: ServeConfig, device=None, comm=None):
@@ -77,6 +78,10 @@ class EngineLoop(threading.Thread):
         self._remote = hasattr(runtime, "observe")
         self._ttft, self._itl = [], []
         self._last_obs = 0.0
+        self.faults = FaultPlan.from_env()
+        self.tracer = StepTracer()
+        self.last_progress = time.monotonic()
+        self.steps = 0
         if self._remote:
             engine.on_ttft = self._ttft.append
             engine.on_itl = self._itl.append
@@ -130,14 +135,26 @@ class EngineLoop(threading.Thread):
                 for conv in self.rt.pop_cancellations():
                     self.engine.abort(conv)
                 if not self.engine.has_work():
+                    self.last_progress = time.monotonic()
                     continue
+                self.tracer.begin(self.steps)
+                t0 = time.perf_counter()
                 events = self.engine.step()
+                if self.faults.active:
+                    events = self.faults.filter_events(events)
                 self.publish(events)
+                self.tracer.end(self.steps, self.engine, events, time.perf_counter() - t0)
+                self.steps += 1
+                self.last_progress = time.monotonic()
                 self._observe()
+                if self.faults.active:
+                    self.faults.after_step()
         except Exception as e:  # noqa: BLE001 - surfaced to the operator, readiness drops
             self.error = e
             self.rt.set_ready(False)
             raise
+        finally:
+            self.tracer.close()
 
 
 class ServingApp:
@@ -148,6 +165,7 @@ class ServingApp:
         rd["local_engine"] = cfg.engine in ("gpu", "cpu", "stub")
         self.rt = mod.Runtime(rd)
         self.loop = None
+        self.watchdog = None
         self.engine = None
         self.tok = None
         if cfg.engine in ("gpu", "cpu"):
@@ -163,12 +181,16 @@ class ServingApp:
             self.loop = EngineLoop(self.rt, self.engine, self.tok, self.cfg)
             self.loop.start()
             self.rt.set_ready(True)
+            self.watchdog = Watchdog(self.loop, self.rt.set_ready)
+            self.watchdog.start()
         return self
 
     def port(self, role: str) -> int:
         return self.rt.bound_port(role)
 
     def stop(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
         if self.loop is not None:
             self.loop.stop_flag.set()
             self.loop.join(timeout=10)

@@ -26,6 +26,7 @@ from ..models.mistral import TINY, get_config
 from ..models.tokenizer import get_tokenizer
 from .app import EngineLoop, build_engine
 from .config import ServeConfig
+from .faults import Watchdog
 
 
 def dp_prefix(cfg: ServeConfig) -> str:
@@ -54,6 +55,8 @@ def run_worker(cfg: ServeConfig, rank: int, device=None):
     loop = EngineLoop(chan, engine, tok, cfg)
     loop.start()
     chan.set_ready(True)
+    # a stalled replica says goodbye (the router stops routing to it) and hello again when it recovers
+    Watchdog(loop, chan.set_ready).start()
     return loop
 
 
