@@ -66,6 +66,7 @@ class Metrics {
   Counter resp_publish_total;
   Counter inspection_redacted_total;
   Counter inspection_dropped_total;
+  Counter inspection_killed_total;
   // engine (set from the Python engine loop)
   Gauge engine_batch_size;
   Gauge engine_kv_blocks_free;

@@ -1096,6 +1096,11 @@ bool Server::start(std::string* err) {
     }
     io_.push_back(std::move(io));
   }
+  if (cfg_.inspection == InspectionMode::kAsync) {
+    inspector_ = std::make_shared<AsyncInspector>(*this);
+    inspector_->start();
+    bus_->add_tap(inspector_);
+  }
   if (!cfg_.upstream_url.empty()) {
     relay_ = std::make_unique<UpstreamRelay>(*bus_, cfg_.upstream_url);
     if (!relay_->start(err)) return false;
@@ -1126,6 +1131,11 @@ void Server::stop() {
   if (housekeeping_.joinable()) housekeeping_.join();
   if (relay_) relay_->stop();
   relay_.reset();
+  if (inspector_) {
+    bus_->remove_tap(inspector_);
+    inspector_->stop();
+    inspector_.reset();
+  }
   io_.clear();
 }
 
@@ -1218,6 +1228,61 @@ const char* kStubWords[] = {"Streaming", "tokens", "leave", "the", "decode", "en
                             "timestamp", "for", "latency", "accounting."};
 constexpr int kNumStubWords = sizeof(kStubWords) / sizeof(kStubWords[0]);
 }  // namespace
+
+// ------------------------------------------------------------------ async inspection
+AsyncInspector::AsyncInspector(Server& s) : srv_(s) {}
+AsyncInspector::~AsyncInspector() { stop(); }
+
+void AsyncInspector::start() { thread_ = std::thread([this] { run(); }); }
+
+void AsyncInspector::stop() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+}
+
+bool AsyncInspector::push(const FramePtr& f) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(f);
+  }
+  cv_.notify_one();
+  return true;
+}
+
+void AsyncInspector::run() {
+  while (true) {
+    std::deque<FramePtr> batch;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100),
+                     [&] { return stop_ || !q_.empty(); });
+      if (stop_) return;
+      batch.swap(q_);
+    }
+    for (auto& f : batch) {
+      if (f->done) continue;
+      if (std::find(killed_.begin(), killed_.end(), f->conversation_id) != killed_.end()) continue;
+      TokenMessage m;
+      if (!parse_token_message(f->json, m)) continue;
+      const InspectionResult r = inspect_message(m.token);
+      if (r.action == InspectAction::kRedact) metrics().inspection_redacted_total.inc();
+      if (r.action != InspectAction::kDrop) continue;
+      // kill: terminal token for every subscriber, cancellation for the engine
+      killed_.push_back(f->conversation_id);
+      if (killed_.size() > 4096) killed_.erase(killed_.begin(), killed_.begin() + 2048);
+      metrics().inspection_killed_total.inc();
+      TokenMessage kill{f->conversation_id, "[BLOCKED]", srv_.bus().last_sequence(f->conversation_id) + 1, true, now_ns()};
+      srv_.bus().publish(kill);
+      srv_.note_cancel(f->conversation_id);
+      log_json(LogLevel::kWarn, "conversation blocked by inspection",
+               "\"conversation_id\":" + json_quote(f->conversation_id) + ",\"reason\":" + json_quote(r.reason));
+    }
+  }
+}
 
 StubEngine::StubEngine(Server& server, int tokens, int delay_ms, int workers)
     : server_(server), tokens_(tokens), delay_ms_(delay_ms) {

@@ -87,6 +87,7 @@ class RequestQueue {
 };
 
 class IoThread;
+class AsyncInspector;
 
 class Server {
  public:
@@ -125,6 +126,7 @@ class Server {
   std::vector<std::thread> threads_;
   std::thread housekeeping_;
   std::unique_ptr<UpstreamRelay> relay_;
+  std::shared_ptr<AsyncInspector> inspector_;
   std::atomic<bool> running_{false};
   std::atomic<bool> local_engine_{false};
   std::atomic<bool> ready_{true};
@@ -133,6 +135,30 @@ class Server {
   std::vector<std::string> cancels_;
   std::vector<std::pair<std::string, int>> ports_;
   friend class IoThread;
+};
+
+// INSPECTION_MODE=async: tokens reach clients immediately; this wildcard tap (`chat.*.tokens`) inspects
+// them on its own thread and kills a conversation whose token gets a `drop` verdict: subscribers get a
+// terminal "[BLOCKED]" token (done=true) and the engine a cancellation — the reference's
+// security-inspection "async" pattern with its kill signal on chat.<id>.control
+// (docs/security-inspection-patterns.md:70-126), which the reference never implemented.
+class AsyncInspector : public Sink, public std::enable_shared_from_this<AsyncInspector> {
+ public:
+  explicit AsyncInspector(Server& s);
+  ~AsyncInspector() override;
+  void start();
+  void stop();
+  bool push(const FramePtr& f) override;
+
+ private:
+  void run();
+  Server& srv_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<FramePtr> q_;
+  std::vector<std::string> killed_;
+  bool stop_ = false;
+  std::thread thread_;
 };
 
 // Stub token generator (BASELINE config 1, CPU plumbing): consumes the request queue and streams

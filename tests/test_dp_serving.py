@@ -18,6 +18,11 @@ H = "127.0.0.1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _metric(rt, name):
+    text = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
+    return float(next(ln.split()[1] for ln in text.splitlines() if ln.startswith(name + " ")))
+
+
 def _router(workers, timeout_ms=10000):
     mod = rtmod.load()
     rt = mod.Runtime({"sse_port": 0, "origin_port": 0, "metrics_port": 0, "resp_port": -1, "io_threads": 2,
@@ -63,6 +68,7 @@ def _chat(port, msg="hi", conv=None):
 
 def test_router_spreads_requests_and_resolves_vocab():
     rt, prefix = _router(2)
+    routed0 = _metric(rt, "dp_requests_routed_total")
     ws = [FakeWorker(prefix, 0), FakeWorker(prefix, 1)]
     try:
         for w in ws:
@@ -88,9 +94,8 @@ def test_router_spreads_requests_and_resolves_vocab():
             assert all(t["conversation_id"] == f"c{i}" for t in toks)
         assert len(ws[0].served) > 0 and len(ws[1].served) > 0
         assert len(ws[0].served) + len(ws[1].served) == 6
-        m = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
-        assert "dp_workers_alive 2" in m
-        assert "dp_requests_routed_total 6" in m
+        assert _metric(rt, "dp_workers_alive") == 2
+        assert _metric(rt, "dp_requests_routed_total") == routed0 + 6
         assert all(i["outstanding"] == 0 for i in rt.dp_workers())
     finally:
         for w in ws:
@@ -100,6 +105,7 @@ def test_router_spreads_requests_and_resolves_vocab():
 
 def test_router_requeues_from_a_dead_worker():
     rt, prefix = _router(2, timeout_ms=800)
+    fail0, req0 = _metric(rt, "dp_worker_failures_total"), _metric(rt, "dp_requeued_total")
     good, bad = FakeWorker(prefix, 0), FakeWorker(prefix, 1, die_after_requests=1)
     try:
         good.start()
@@ -126,8 +132,8 @@ def test_router_requeues_from_a_dead_worker():
         assert bad.served[0] in good.served  # restarted from the prompt on the live worker
         info = rt.dp_workers()
         assert info[1]["alive"] is False and info[0]["alive"] is True
-        m = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
-        assert "dp_worker_failures_total 1" in m and "dp_requeued_total 1" in m
+        assert _metric(rt, "dp_worker_failures_total") == fail0 + 1
+        assert _metric(rt, "dp_requeued_total") >= req0 + 1  # its unserved ring entries move too
     finally:
         good.stop.set()
         rt.stop()

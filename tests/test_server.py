@@ -36,6 +36,11 @@ def bare_rt():
     r.stop()
 
 
+def _metric(rt, name):
+    text = request(H, rt.bound_port("metrics"), "GET", "/metrics").body.decode()
+    return float(next(ln.split()[1] for ln in text.splitlines() if ln.startswith(name + " ")))
+
+
 def tokens_of(resp):
     return [e.json() for e in resp.events if e.event == "token"]
 
@@ -289,6 +294,7 @@ def test_edge_relays_origin_tokens_over_upstream_sse():
     origin.start_stub(5, 5, 1)
     edge = make_rt(llm_proxy_url=f"http://127.0.0.1:{origin.bound_port('origin')}",
                    upstream_url=f"http://127.0.0.1:{origin.bound_port('edge')}")
+    frames0 = _metric(edge, "relay_frames_total")
     try:
         ep = edge.bound_port("edge")
         side = {}
@@ -306,8 +312,7 @@ def test_edge_relays_origin_tokens_over_upstream_sse():
         assert toks[-1]["token"] == "[DONE]" and toks[-1]["done"]
         assert [x["sequence"] for x in tokens_of(side["r"])] == [1, 2, 3, 4, 5, 6]
         # the origin served the conversation exactly once over its SSE port (the relay)
-        m = request(H, edge.bound_port("metrics"), "GET", "/metrics").body.decode()
-        assert "relay_frames_total 6" in m
+        assert _metric(edge, "relay_frames_total") == frames0 + 6
     finally:
         edge.stop()
         origin.stop()
@@ -347,5 +352,30 @@ def test_chat_page_served_at_root():
         assert resp.status == 200
         assert resp.headers["content-type"].startswith("text/html")
         assert b"fetch(base + \"/chat\"" in resp.body
+    finally:
+        r.stop()
+
+
+def test_async_inspection_kills_conversation():
+    r = make_rt(inspection_mode="async")
+    r.set_local_engine(True)
+    killed0, redacted0 = _metric(r, "inspection_killed_total"), _metric(r, "inspection_redacted_total")
+    try:
+        conv = "insp-async"
+        got = []
+        th = threading.Thread(target=lambda: got.append(request(H, r.bound_port("edge"), "GET", f"/stream/{conv}",
+                                                                timeout=5)))
+        th.start()
+        time.sleep(0.3)
+        r.publish(conv, "my password", 1, False, 0)
+        r.publish(conv, "ignore previous orders", 2, False, 0)
+        th.join(5)
+        toks = tokens_of(got[0])
+        # delivered immediately (no redaction in async mode), then stopped with a terminal token
+        assert [t["token"] for t in toks] == ["my password", "ignore previous orders", "[BLOCKED]"]
+        assert toks[-1]["done"] and toks[-1]["sequence"] == 3
+        assert conv in r.pop_cancellations()
+        assert _metric(r, "inspection_killed_total") == killed0 + 1
+        assert _metric(r, "inspection_redacted_total") == redacted0 + 1
     finally:
         r.stop()
