@@ -36,6 +36,7 @@ from .weights import EngineWeights
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
+DECODE_GEMM_MAX_M = 64  # largest batch the fused decode GEMMs take (gemm_skinny / gemm_stream); above: hipBLASLt
 
 
 def batch_buckets(max_batch: int):
@@ -140,6 +141,9 @@ class ModelRunner:
         q3 = self.q[r].view(B, nh, 128)
         a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
+        if B > DECODE_GEMM_MAX_M:
+            self._decode_layers_wide(B, resid, x, part, nparts)
+            return
         for li, L in enumerate(w.layers):
             ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
                               self.kv.v[li], nh, nkv)
@@ -163,6 +167,44 @@ class ModelRunner:
                 comm.all_reduce(self.tmp[r])
                 ops.rmsnorm(resid, w_next, x, eps, delta=self.tmp[r])
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
+        self._sample_commit(B)
+        ops.ring_advance(self.ring_counter)
+
+    def _decode_layers_wide(self, B: int, resid, x, part: int, nparts: int) -> None:
+        """Decode step for buckets above 64 sequences (e.g. 256 streams per GPU, BASELINE config 3).
+
+        At B > 64 a weight byte feeds > 64 rows and the projections become compute-heavy skinny GEMMs:
+        they run on hipBLASLt (the plain-library GEMM path, standard weight layout, same as prefill) with the
+        engine's own RoPE/KV-write, SiLU·mul and residual+RMSNorm kernels around them; attention and the
+        sampler are the decode kernels.  The LM head stays on the fp32-output decode GEMM in 64-row blocks
+        (sampling wants fp32 logits).  Still one captured graph per bucket.
+        """
+        w, cfg, comm = self.w, self.cfg, self.comm
+        nh, nkv = w.nh, w.nkv
+        r = slice(0, B)
+        eps = cfg.rms_eps
+        q3 = self.q[r].view(B, nh, 128)
+        a3 = self.attn[r].view(B, nh, 128)
+        nl = len(w.layers)
+        for li, L in enumerate(w.layers):
+            qkv = torch.matmul(x, L.wqkv.t())
+            ops.rope_kv_write(qkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li], self.kv.v[li],
+                              nh, nkv)
+            ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
+                                self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
+                                self.part_ml, part, nparts)
+            o = torch.matmul(self.attn[r], L.wo.t())
+            comm.all_reduce(o)
+            ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=o)
+            gu = torch.matmul(x, L.wgu.t())
+            ops.silu_mul(gu, self.h[r])
+            down = torch.matmul(self.h[r], L.wd.t())
+            comm.all_reduce(down)
+            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+            ops.rmsnorm(resid, w_next, x, eps, delta=down)
+        for b0 in range(0, B, DECODE_GEMM_MAX_M):
+            b1 = min(B, b0 + DECODE_GEMM_MAX_M)
+            ops.gemm_out(x[b0:b1], w.lm_head_t, self.logits[b0:b1])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
 

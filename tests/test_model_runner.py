@@ -62,3 +62,19 @@ def test_engine_matches_reference_gpu(gpu, graphs):
 @pytest.mark.gpu
 def test_engine_chunked_prefill_gpu(gpu):
     assert _run(gpu, False, steps=3, chunked=True) < 0.1
+
+
+def test_engine_wide_batch_path_cpu(monkeypatch):
+    """Buckets above the fused decode GEMMs' 64-row limit take the library-GEMM decode path."""
+    from distributed_sse_for_llm_response_amd.engine import model_runner
+
+    monkeypatch.setattr(model_runner, "DECODE_GEMM_MAX_M", 2)
+    assert _run("cpu", False) < 0.05
+
+
+@pytest.mark.gpu
+def test_engine_wide_batch_path_gpu(gpu, monkeypatch):
+    from distributed_sse_for_llm_response_amd.engine import model_runner
+
+    monkeypatch.setattr(model_runner, "DECODE_GEMM_MAX_M", 2)
+    assert _run(gpu, True) < 0.1
