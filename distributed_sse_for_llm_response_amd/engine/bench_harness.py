@@ -168,7 +168,11 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     if tp != 1:
         raise ValueError("serving bench: data-parallel replicas only (tp=1); use --delivery frame for TP")
     device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
-    total = steps + warmup
+    # Admission prefills ~max_prefill_tokens of prompts per engine step while the already admitted streams
+    # decode, so the first streams run ahead by up to `skew` steps.  Every stream must stay live through
+    # the whole timed window (full batch on every timed step): budget the tokens and the KV for it.
+    skew = math.ceil(streams * (prompt_len + 16) / 8192) + 4
+    total = steps + warmup + skew
     cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
     if use_graphs and device.type == "cuda":
         r.capture()
@@ -207,6 +211,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
                                arrival_ns=req["arrival_ns"])
 
     # admission + prefill until every stream of this replica is decoding
+    live = lambda: sum(1 for s in engine.slots if s is not None and s.state == "decode")  # noqa: E731
     t_admit = time.time()
     while sum(1 for s in engine.slots if s is not None and s.state == "decode") < streams:
         pump(20 if not engine.has_work() else 0)
@@ -225,6 +230,8 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     _sync(device, world)
     elapsed = time.perf_counter() - t0
     t1_ns = time.time_ns()
+    if live() < streams:
+        raise RuntimeError(f"bench: only {live()} of {streams} streams were still decoding at the end of the window")
     while engine.has_work():
         publish(engine.step())
     res = {"arrivals": [], "errors": []}
@@ -246,7 +253,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     itl = np.array(gaps) if gaps else np.array([elapsed * 1000.0 / max(1, steps)])
     return {"elapsed_s": elapsed, "p50_itl_ms": float(np.percentile(itl, 50)),
             "p99_itl_ms": float(np.percentile(itl, 99)), "delivered_in_window": delivered,
-            "client_errors": res["errors"][:5], "model": cfg.name}
+            "client_errors": res["errors"][:5], "model": cfg.name, "max_context": prompt_len + 16 + total}
 
 
 def _sync(device, world):
