@@ -94,7 +94,7 @@ struct SCfg {
 SCfg pick_stream(int M, int N, int K) {
   SCfg c{};
   c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  c.nt = env_int("DSSE_S_NT", 1);
+  c.nt = M > 64 ? 1 : env_int("DSSE_S_NT", 1);  // row-block mode (M > 64) is instantiated for nt = 1
   // 8 waves per workgroup when that still gives ~one workgroup per CU without split-K (gate_up,
   // LM head), else 4 (narrow O / down / QKV: more, shorter workgroups; measured, profiles/gemm_stream_r1.md)
   c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
@@ -103,10 +103,10 @@ SCfg pick_stream(int M, int N, int K) {
   if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
   if ((N / 16) % c.nw != 0) c.nw = 4;
   c.rd = env_int("DSSE_S_RD", 1);
-  if (c.nt == 2 || c.rd != 2) c.rd = 1;
+  if (c.nt == 2 || c.rd != 2 || M > 64) c.rd = 1;
   c.ok = K % 512 == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
-  const int wgs = N / (16 * c.nt) / c.nw, slices = K / 512;
+  const int wgs = N / (16 * c.nt) / c.nw * ((M + 63) / 64), slices = K / 512;
   int S = env_int("DSSE_S_SPLIT", 0);
   if (S <= 0 || slices % S != 0) {
     // smallest split that gives ~one workgroup per CU (256 CUs), never more than 320 workgroups
@@ -122,11 +122,14 @@ SCfg pick_stream(int M, int N, int K) {
   return c;
 }
 
+constexpr int kMaxDecodeM = 512;  // gemm_stream row-block mode above 64 rows
+
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
 // whole K-slice staged (gemm_xlds.hip), 2 = X streamed through LDS slices (gemm_stream.hip).
 // DSSE_GEMM_IMPL forces one.
 int gemm_impl(int M, int N, int K) {
   const int impl = env_int("DSSE_GEMM_IMPL", -1);
+  if (M > 64) return 2;  // only the X-streaming kernel has a row-block mode
   if (impl >= 0) {
     if (impl == 2 && !pick_stream(M, N, K).ok) return 1;
     return impl;
@@ -144,10 +147,11 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x and w must be 2-D");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch: x ", K, " vs w ", w.size(1));
-  TORCH_CHECK(M >= 1 && M <= 64, "decode GEMM supports 1 <= M <= 64, got ", M);
+  TORCH_CHECK(M >= 1 && M <= kMaxDecodeM, "decode GEMM supports 1 <= M <= ", kMaxDecodeM, ", got ", M);
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
   const int impl = gemm_impl(M, N, K);
+  TORCH_CHECK(M <= 64 || impl == 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
   if (impl == 2) {
     const SCfg c = pick_stream(M, N, K);
     at::Tensor part;
@@ -205,7 +209,8 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   check_gpu(part, "part");
   check_dtype(part, at::kFloat, "part");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
-  const bool shape_ok = M >= 1 && M <= 64 && K % 128 == 0 && N % 16 == 0 && w.size(1) == K;
+  const bool shape_ok = M >= 1 && M <= kMaxDecodeM && K % 128 == 0 && N % 16 == 0 && w.size(1) == K &&
+                        (M <= 64 || pick_stream(M, N, K).ok);
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
   if (impl == 2) {
     const SCfg c = pick_stream(M, N, K);

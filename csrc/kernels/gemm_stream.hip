@@ -24,7 +24,11 @@ namespace dsse {
 
 constexpr int kStreamCPS = 4;  // K-chunks of 128 per LDS slice
 
-template <int MT, int NT, int NW, int RD, int MODE>
+// Row blocks (M > 64, e.g. a 256-sequence decode bucket): the grid is (tile-group workgroups x MB row
+// blocks of 64) and workgroups are renumbered so that the MB row blocks of one tile group are consecutive
+// on the same XCD: they stream the same weight bytes at about the same time, so HBM serves them once and
+// the XCD's L2 the other MB-1 times.  That sharing needs temporal (cached) weight loads (SHARED_W).
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
                    int Kr, GemmEpi ep, float* __restrict__ part) {
@@ -37,12 +41,23 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int tgi = blockIdx.x * NW + w;  // host guarantees N / (16 NT) % NW == 0: every wave is busy
+  int wg = blockIdx.x, rb = 0;
+  if constexpr (SHARED_W) {
+    // bijective XCD-aware renumbering (dispatch puts workgroup i on XCD i % 8)
+    const int nb = gridDim.x, xcd = wg % 8, slot = wg / 8, q = nb / 8, rem = nb % 8;
+    const int id = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
+    const int MB = (M + MP - 1) / MP;
+    wg = id / MB;
+    rb = id % MB;
+    X += (size_t)rb * MP * ldx;
+  }
+  const int m0 = rb * MP;     // first row of this workgroup's row block
+  const int tgi = wg * NW + w;  // host guarantees N / (16 NT) % NW == 0: every wave is busy
   const int ks = blockIdx.y;
   const int k0 = ks * Kr;
   const int nch = Kr >> 7;   // multiple of CPS (host-checked)
   const int nsl = nch / CPS;
-  const int npieces = min(M, MP) * CPS * 16;
+  const int npieces = min(M - m0, MP) * CPS * 16;
   const int KC = K >> 7;
 
   const bf16* wbase = W + ((size_t)tgi * NT * KC + (k0 >> 7)) * kTileChunk + lane * 8;
@@ -51,7 +66,9 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) wf[t][s] = ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
+      for (int s = 0; s < 4; ++s)
+        wf[t][s] = SHARED_W ? ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s)
+                            : ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
   };
 
   bf16x8 xs[PPT];
@@ -127,30 +144,36 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       for (int i = 0; i < 4; ++i) {
         const float v = acc[mt][t][i];
         const float partner = (MODE == kSiluMul || MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
-        epilogue<MODE>(ep, part_ks, M, N, 16 * mt + 4 * g + i, tgi * NT + t, r, v, partner);
+        epilogue<MODE>(ep, part_ks, M, N, m0 + 16 * mt + 4 * g + i, tgi * NT + t, r, v, partner);
       }
 }
 
-template <int MT, int NT, int NW, int RD, int MODE>
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
 static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
   const int TG = N / (16 * NT);
+  const int MB = SHARED_W ? (M + 16 * MT - 1) / (16 * MT) : 1;
   const size_t lds = (size_t)2 * 16 * MT * kStreamCPS * 256;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  dim3 grid(TG / NW, S), block(64 * NW);
-  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep,
-                     part);
+  dim3 grid(TG / NW * MB, S), block(64 * NW);
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>), grid, block, lds, st, X, ldx, M, W, K, N,
+                     K / S, ep, part);
   return hipGetLastError();
 }
 
 template <int MODE>
 static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
                                 int S, const GemmEpi& ep, float* part, hipStream_t st) {
+  if (M > 64) {  // row blocks with L2-shared weights (64-row MFMA tiles, one or eight waves)
+    if (mt == 4 && nt == 1 && nw == 4) return launch_s<4, 1, 4, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
+    if (mt == 4 && nt == 1 && nw == 8) return launch_s<4, 1, 8, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
+    return hipErrorInvalidValue;
+  }
 #define DSSE_S_CASE(MT_, NT_, NW_, RD_)         \
   if (mt == MT_ && nt == NT_ && nw == NW_ && rd == RD_) \
     return launch_s<MT_, NT_, NW_, RD_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
@@ -165,7 +188,8 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
 }  // namespace dsse
 
 // rd: weight-ring depth in LDS slices (1: 4 chunks = 16 KiB per wave in flight, 2: 8 chunks).
-// Shape contract (checked by the caller): K % (512 S) == 0, (N / (16 nt)) % nw == 0, M <= 16 mt <= 64.
+// Shape contract (checked by the caller): K % (512 S) == 0, (N / (16 nt)) % nw == 0, M <= 16 mt <= 64, or
+// M > 64 with mt = 4, nt = 1, rd = 1 (row blocks of 64).
 // part: fp32 [S, M, N] workspace when S > 1.  partial_only: leave the slabs for the consumer (the fused
 // residual + RMSNorm kernel) instead of reducing them here.
 extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X,

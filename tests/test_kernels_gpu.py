@@ -45,7 +45,7 @@ def tiles(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 17, 40, 64])
+@pytest.mark.parametrize("M", [1, 7, 16, 17, 40, 64, 65, 130, 256])
 def test_gemm_out_bf16_f32(gpu, tiles, M):
     g = torch.Generator().manual_seed(M)
     x = _rand(M, 1024, dev=gpu, gen=g)
@@ -70,7 +70,7 @@ def test_gemm_resid(gpu, tiles, M, K):
     _close(r, r0, 1e-3, 1e-3, "gemm_resid")
 
 
-@pytest.mark.parametrize("M,K", [(64, 4096), (40, 14336), (4, 4096)])
+@pytest.mark.parametrize("M,K", [(64, 4096), (40, 14336), (4, 4096), (200, 4096), (256, 14336)])
 def test_gemm_resid_split_then_fused_norm(gpu, M, K):
     """Split-K slabs reduced inside the RMSNorm equal resid += x·wᵀ followed by the norm."""
     g = torch.Generator().manual_seed(M + K)
@@ -80,7 +80,7 @@ def test_gemm_resid_split_then_fused_norm(gpu, M, K):
     nw = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16()
     r0 = torch.randn(M, H, generator=g)
     r = r0.clone().to(gpu)
-    part = torch.zeros(32 * 64 * H, device=gpu)
+    part = torch.zeros(32 * max(64, M) * H, device=gpu)
     y = torch.zeros(M, H, device=gpu, dtype=torch.bfloat16)
     ns = ops.gemm_resid_split(x, w, r, part)
     if M > 16:
@@ -93,7 +93,7 @@ def test_gemm_resid_split_then_fused_norm(gpu, M, K):
     _close(y, yr, 2e-2, 1e-2, "y")
 
 
-@pytest.mark.parametrize("M", [1, 20, 64])
+@pytest.mark.parametrize("M", [1, 20, 64, 150])
 def test_gemm_silu(gpu, tiles, M):
     g = torch.Generator().manual_seed(M + 100)
     x = _rand(M, 2048, dev=gpu, gen=g)
@@ -105,7 +105,7 @@ def test_gemm_silu(gpu, tiles, M):
     _close(out, ref, 2e-2, 2e-2, "gemm_silu")
 
 
-@pytest.mark.parametrize("M", [1, 9, 64])
+@pytest.mark.parametrize("M", [1, 9, 64, 100])
 def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     nh, nkv, H = 8, 2, 1024
     g = torch.Generator().manual_seed(M + 7)
