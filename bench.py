@@ -59,13 +59,15 @@ def main():
 
     from distributed_sse_for_llm_response_amd.parallel.comm import init_distributed
 
-    rank, local, world = init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    n_gpus = world
+    # bind this rank's GPU before the process group exists (RCCL communicators use the current device)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
+    rank, local, world = init_distributed(device=device if device.type == "cuda" else None)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    n_gpus = world
 
     if sse:
         res = bench_harness.run_serving_bench(client, model=args.model, device=device, streams=args.streams,

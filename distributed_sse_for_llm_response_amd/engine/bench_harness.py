@@ -186,7 +186,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
         runtime = mod.Runtime({"host": "127.0.0.1", "sse_port": 0, "origin_port": -1, "metrics_port": -1,
                                "resp_port": -1, "io_threads": 4, "local_engine": True})
         runtime.set_vocab(tok.pieces())
-        runtime.start_dp_router(prefix, world, 16, 600_000)
+        runtime.start_dp_router(prefix, world, 4, 600_000)  # 4 MiB rings: /dev/shm may be small in containers
         runtime.start()
     chan = mod.DpWorker(prefix, rank, 600_000)
     chan.set_ready(True)

@@ -30,11 +30,23 @@ def shapes(tp):
     }
 
 
-def time_op(fn, iters):
+def time_op(fn, iters, graph=False):
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         fn(0)
     torch.cuda.synchronize()
+    if graph:  # the decode step replays its kernels from a hipGraph: time them the same way
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(iters):
+                fn(i)
+        g.replay()
+        torch.cuda.synchronize()
+        st.record()
+        g.replay()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / iters * 1e3
     st.record()
     for i in range(iters):
         fn(i)
@@ -48,6 +60,7 @@ def main():
     ap.add_argument("--M", default="1,16,32,64")
     ap.add_argument("--ops", default="", help="comma-separated subset of qkv,o,gate_up,down,lm_head")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the calls")
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--configs", default="skinny;x;x:DSSE_X_NW=4;x:DSSE_X_NT=2;x:DSSE_X_KS=512",
                     help="';'-separated; 'skinny', 'x' (X-in-LDS) or 's' (X-streaming), optionally ':K=V,K=V' env overrides")
@@ -91,7 +104,7 @@ def main():
                     out = torch.zeros(M, N, device=dev, dtype=torch.float32)
                     fn = (lambda i, out=out, x=x: ops.gemm_resid(x, ws[i % copies], out))
                 try:
-                    us = time_op(fn, args.iters)
+                    us = time_op(fn, args.iters, args.graph)
                 except RuntimeError as e:
                     print(f"{name} M={M} cfg={cfg}: {e}", flush=True)
                     continue
