@@ -210,6 +210,10 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
             engine.add_request(req["conversation_id"], tok.chat_prompt(req["message"]), p,
                                arrival_ns=req["arrival_ns"])
 
+    import gc
+
+    gc.collect()
+    gc.freeze()  # as in the serving loop (serving/app.py EngineLoop.run)
     # admission + prefill until every stream of this replica is decoding
     live = lambda: sum(1 for s in engine.slots if s is not None and s.state == "decode")  # noqa: E731
     t_admit = time.time()

@@ -45,7 +45,7 @@ class SamplingParams:
     ignore_eos: bool = False
 
 
-@dataclass
+@dataclass(slots=True)
 class TokenEvent:
     conversation_id: str
     token_id: int

@@ -2,8 +2,8 @@
 
 Usage: python tools/prof_step.py gpurun_out/prof/run_kernel_trace.csv [--marker sample_pick] [--last 6]
 
-A decode step ends with the sampler's pick kernel; the last `--last` complete steps (after prefill) are
-averaged: per kernel name, calls and GPU time per step, plus the step's wall time (end of one pick to
+A decode step ends with the sampler's pick kernel; the last `--last` steady-state steps (no admission,
+prefill or slot-metadata uploads) are averaged: per kernel name, calls and GPU time per step, plus the step's wall time (end of one pick to
 the end of the next) and the idle share (wall - busy).  Prints a markdown table.
 """
 from __future__ import annotations
@@ -32,12 +32,18 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     ends = [i for i, (_, _, n) in enumerate(rows) if args.marker in n]
-    if len(ends) < args.last + 1:
-        raise SystemExit(f"only {len(ends)} steps found")
-    sel = ends[-(args.last + 1):]
+    # steady-state steps only: no slot-metadata uploads (at most the one token-ring drain copy) and the
+    # most common kernel count (admission / finishing steps carry prefill or upload work)
+    spans = [(a, b) for a, b in zip(ends[:-1], ends[1:])]
+    ncopy = [sum(1 for _, _, n in rows[a + 1:b + 1] if "copyBuffer" in n) for a, b in spans]
+    nk = [b - a for a, b in spans]
+    mode = collections.Counter(k for k, c in zip(nk, ncopy) if c <= 1).most_common(1)
+    steady = [sp for sp, k, c in zip(spans, nk, ncopy) if c <= 1 and mode and k == mode[0][0]]
+    if len(steady) < args.last:
+        raise SystemExit(f"only {len(steady)} steady-state steps found")
     per = collections.defaultdict(lambda: [0, 0.0])
     wall = busy = 0.0
-    for a, b in zip(sel[:-1], sel[1:]):
+    for a, b in steady[-args.last:]:
         wall += (rows[b][1] - rows[a][1]) / 1e3
         for s, e, n in rows[a + 1:b + 1]:
             per[short(n)][0] += 1
