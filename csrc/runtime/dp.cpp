@@ -199,6 +199,7 @@ void DpRouter::dispatch_loop() {
   while (running_) {
     auto reqs = server_.requests().pop(256, 20);
     auto cancels = server_.pop_cancellations();
+    auto flow = server_.pop_flow_events();
     std::lock_guard<std::mutex> g(mu_);
     check_liveness_locked(mono_ms());
     while (!pending_.empty()) {
@@ -214,6 +215,15 @@ void DpRouter::dispatch_loop() {
       dpwire::Writer m;
       m.u8(dpwire::kCancel);
       m.str(c);
+      to_w_[(size_t)it->second.worker]->push_wait(m.data().data(), (uint32_t)m.data().size(), 100);
+    }
+    for (auto& [c, paused] : flow) {  // flow control follows the conversation to its worker
+      auto it = convs_.find(c);
+      if (it == convs_.end() || it->second.worker < 0) continue;
+      dpwire::Writer m;
+      m.u8(dpwire::kFlow);
+      m.str(c);
+      m.u8(paused ? 1 : 0);
       to_w_[(size_t)it->second.worker]->push_wait(m.data().data(), (uint32_t)m.data().size(), 100);
     }
   }
@@ -322,7 +332,8 @@ void DpWorker::heartbeat_if_due() {
   send(m.data());
 }
 
-std::vector<ChatRequest> DpWorker::poll(size_t max, int timeout_ms, std::vector<std::string>* cancels, bool* shutdown) {
+std::vector<ChatRequest> DpWorker::poll(size_t max, int timeout_ms, std::vector<std::string>* cancels, bool* shutdown,
+                                        std::vector<std::pair<std::string, bool>>* flow) {
   std::vector<ChatRequest> out;
   heartbeat_if_due();
   std::string msg;
@@ -335,6 +346,10 @@ std::vector<ChatRequest> DpWorker::poll(size_t max, int timeout_ms, std::vector<
       if (dpwire::decode_request(rd, &r)) out.push_back(std::move(r));
     } else if (type == dpwire::kCancel) {
       cancels->push_back(rd.str());
+    } else if (type == dpwire::kFlow) {
+      std::string c = rd.str();
+      const bool paused = rd.u8() != 0;
+      if (flow) flow->emplace_back(std::move(c), paused);
     } else if (type == dpwire::kShutdown) {
       *shutdown = true;
     }

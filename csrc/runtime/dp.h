@@ -30,7 +30,7 @@
 namespace dsse {
 
 namespace dpwire {
-enum : uint8_t { kRequest = 1, kCancel = 2, kShutdown = 3, kHello = 10, kTokens = 11, kStats = 12, kHeartbeat = 13, kBye = 14 };
+enum : uint8_t { kRequest = 1, kCancel = 2, kShutdown = 3, kFlow = 4, kHello = 10, kTokens = 11, kStats = 12, kHeartbeat = 13, kBye = 14 };
 
 class Writer {
  public:
@@ -143,7 +143,8 @@ class DpWorker {
   bool ok() const { return to_router_ && from_router_; }
   const std::string& error() const { return err_; }
   // Requests routed to this worker; cancellations and shutdown are returned through the out-params.
-  std::vector<ChatRequest> poll(size_t max, int timeout_ms, std::vector<std::string>* cancels, bool* shutdown);
+  std::vector<ChatRequest> poll(size_t max, int timeout_ms, std::vector<std::string>* cancels, bool* shutdown,
+                                std::vector<std::pair<std::string, bool>>* flow = nullptr);
   bool publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
                       const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
                       const std::vector<std::string>& texts);

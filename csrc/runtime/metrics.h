@@ -62,6 +62,8 @@ class Metrics {
   Counter bus_dropped_tokens_total;
   Counter bus_backpressure_events_total;
   Counter bus_replayed_total;
+  Counter bus_backpressure_pauses_total;  // conversations paused by flow control (server.h flow_high_water)
+  Gauge bus_paused_conversations;
   Gauge bus_conversations;
   Counter resp_publish_total;
   Counter inspection_redacted_total;

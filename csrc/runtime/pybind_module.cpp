@@ -61,6 +61,8 @@ class Runtime {
     c.keepalive_ms = geti("keepalive_ms", c.keepalive_ms);
     c.first_token_timeout_ms = geti("first_token_timeout_ms", c.first_token_timeout_ms);
     c.max_pending_bytes = (size_t)geti("max_pending_bytes", (int)c.max_pending_bytes);
+    c.flow_high_water = (size_t)geti("flow_high_water", (int)c.flow_high_water);
+    c.socket_sndbuf = geti("socket_sndbuf", c.socket_sndbuf);
     c.replay_max = (size_t)geti("replay_max", (int)c.replay_max);
     c.retention_s = geti("retention_s", c.retention_s);
     c.ui_html = gets("ui_html", "");
@@ -175,6 +177,7 @@ class Runtime {
     return bus_->publish(m);
   }
   std::vector<std::string> pop_cancellations() { return server_->pop_cancellations(); }
+  std::vector<std::pair<std::string, bool>> pop_flow_events() { return server_->pop_flow_events(); }
   size_t subscriber_count(const std::string& id) { return bus_->subscriber_count(id); }
   int64_t last_sequence(const std::string& id) { return bus_->last_sequence(id); }
   size_t queued_requests() { return server_->requests().size(); }
@@ -209,8 +212,10 @@ class DpWorkerPy {
       py::gil_scoped_release nogil;
       std::vector<std::string> cancels;
       bool sd = false;
-      rs = w_->poll(max, timeout_ms, &cancels, &sd);
+      std::vector<std::pair<std::string, bool>> flow;
+      rs = w_->poll(max, timeout_ms, &cancels, &sd, &flow);
       cancels_.insert(cancels_.end(), cancels.begin(), cancels.end());
+      flow_.insert(flow_.end(), flow.begin(), flow.end());
       if (sd) shutdown_ = true;
     }
     py::list out;
@@ -220,6 +225,11 @@ class DpWorkerPy {
   std::vector<std::string> pop_cancellations() {
     std::vector<std::string> out;
     out.swap(cancels_);
+    return out;
+  }
+  std::vector<std::pair<std::string, bool>> pop_flow_events() {
+    std::vector<std::pair<std::string, bool>> out;
+    out.swap(flow_);
     return out;
   }
   bool shutdown_requested() const { return shutdown_; }
@@ -249,6 +259,7 @@ class DpWorkerPy {
  private:
   std::unique_ptr<DpWorker> w_;
   std::vector<std::string> cancels_;
+  std::vector<std::pair<std::string, bool>> flow_;
   bool shutdown_ = false;
 };
 
@@ -270,6 +281,7 @@ PYBIND11_MODULE(_dsse_runtime, m) {
       .def("publish", &Runtime::publish, py::arg("conversation_id"), py::arg("token"), py::arg("sequence"),
            py::arg("done") = false, py::arg("timestamp_ns") = 0)
       .def("pop_cancellations", &Runtime::pop_cancellations)
+      .def("pop_flow_events", &Runtime::pop_flow_events)
       .def("subscriber_count", &Runtime::subscriber_count)
       .def("last_sequence", &Runtime::last_sequence)
       .def("queued_requests", &Runtime::queued_requests)
@@ -286,6 +298,7 @@ PYBIND11_MODULE(_dsse_runtime, m) {
            py::arg("open_timeout_ms") = 60000)
       .def("poll_requests", &DpWorkerPy::poll_requests, py::arg("max") = 256, py::arg("timeout_ms") = 0)
       .def("pop_cancellations", &DpWorkerPy::pop_cancellations)
+      .def("pop_flow_events", &DpWorkerPy::pop_flow_events)
       .def("shutdown_requested", &DpWorkerPy::shutdown_requested)
       .def("publish_tokens", &DpWorkerPy::publish_tokens, py::arg("conversation_ids"), py::arg("token_ids"),
            py::arg("sequences"), py::arg("dones"), py::arg("timestamp_ns") = 0,

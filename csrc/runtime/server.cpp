@@ -284,6 +284,7 @@ struct Conn {
   bool sse = false;
   bool chat_mode = false;
   bool got_first = false;
+  bool congested = false;  // output queue above flow_high_water (counted in Server::flow_)
   std::string conv_id;
   int64_t sse_start_mono = 0, last_write_mono = 0, first_deadline_mono = 0;
   int64_t after_seq = -1;
@@ -443,6 +444,8 @@ void IoThread::accept_all(int lfd, Role role) {
     if (fd < 0) return;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (srv_.config().socket_sndbuf > 0)
+      setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &srv_.config().socket_sndbuf, sizeof(int));
     Conn c;
     c.fd = fd;
     c.id = ((uint64_t)index_ << 48) | next_id_++;
@@ -488,8 +491,19 @@ void IoThread::flush_out(Conn& c) {
     c.out.erase(0, c.out_off);
     c.out_off = 0;
   }
+  const size_t pend = c.out.size() - c.out_off;
   auto pit = pending_.find(c.id);
-  if (pit != pending_.end()) pit->second->store(c.out.size() - c.out_off, std::memory_order_relaxed);
+  if (pit != pending_.end()) pit->second->store(pend, std::memory_order_relaxed);
+  const size_t hw = srv_.config().flow_high_water;
+  if (hw && c.sse && c.sink) {
+    if (!c.congested && pend > hw) {
+      c.congested = true;
+      srv_.flow_update(c.conv_id, +1);
+    } else if (c.congested && pend < hw / 4) {
+      c.congested = false;
+      srv_.flow_update(c.conv_id, -1);
+    }
+  }
   const bool ww = c.out_off < c.out.size();
   if (ww != c.want_write) {
     c.want_write = ww;
@@ -538,6 +552,8 @@ void IoThread::end_sse(Conn& c, bool write_terminator) {
   c.sse = false;
   if (c.sink) {
     srv_.bus().unsubscribe(c.conv_id, c.sink);
+    srv_.flow_update(c.conv_id, c.congested ? -1 : 0);
+    c.congested = false;
     if (c.chat_mode && !srv_.bus().conversation_done(c.conv_id) && srv_.bus().subscriber_count(c.conv_id) == 0)
       srv_.note_cancel(c.conv_id);
     c.sink.reset();
@@ -834,6 +850,7 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
     sink->cap = srv_.config().max_pending_bytes;
     c.sink = sink;
     srv_.bus().subscribe(conv, sink, -1, nullptr);
+    srv_.flow_update(conv, 0);  // an uncongested subscriber resumes a paused conversation
     start_sse(c, conv, true, -1, "event: connected\ndata: {\"conversation_id\":" + json_quote(conv) + "}\n\n", nullptr);
     srv_.relay_ensure(conv);
     if (local) {
@@ -879,6 +896,7 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
     c.sink = sink;
     std::vector<FramePtr> replay;
     srv_.bus().subscribe(conv, sink, after, after >= 0 ? &replay : nullptr);
+    srv_.flow_update(conv, 0);
     start_sse(c, conv, false, after, ": connected to " + conv + "\n\n", &replay);
     srv_.relay_ensure(conv);
     return;
@@ -1156,6 +1174,40 @@ void Server::note_cancel(const std::string& conv_id) {
   cancels_.push_back(conv_id);
 }
 
+void Server::flow_update(const std::string& conv_id, int delta) {
+  std::lock_guard<std::mutex> g(flow_mu_);  // lock order: flow_mu_ -> bus shard (the bus never calls back)
+  auto it = flow_.find(conv_id);
+  if (it == flow_.end()) {
+    if (delta <= 0) return;
+    it = flow_.emplace(conv_id, std::make_pair(0, false)).first;
+  }
+  int& n = it->second.first;
+  n = std::max(0, n + delta);
+  const bool paused = n > 0 && (size_t)n >= bus_->subscriber_count(conv_id);
+  if (paused != it->second.second) {
+    it->second.second = paused;
+    if (flow_events_.size() < (1u << 16)) flow_events_.emplace_back(conv_id, paused);
+    n_paused_.fetch_add(paused ? 1 : -1);
+    if (paused) metrics().bus_backpressure_pauses_total.inc();
+    metrics().bus_paused_conversations.add(paused ? 1 : -1);
+  }
+  if (n == 0) flow_.erase(it);
+}
+
+bool Server::flow_paused(const std::string& conv_id) {
+  if (n_paused_.load(std::memory_order_relaxed) == 0) return false;
+  std::lock_guard<std::mutex> g(flow_mu_);
+  auto it = flow_.find(conv_id);
+  return it != flow_.end() && it->second.second;
+}
+
+std::vector<std::pair<std::string, bool>> Server::pop_flow_events() {
+  std::lock_guard<std::mutex> g(flow_mu_);
+  std::vector<std::pair<std::string, bool>> out;
+  out.swap(flow_events_);
+  return out;
+}
+
 std::vector<std::string> Server::pop_cancellations() {
   std::lock_guard<std::mutex> g(cancel_mu_);
   std::vector<std::string> out;
@@ -1320,6 +1372,11 @@ void StubEngine::run() {
     int64_t now = mono_ns(), next_due = now + 5000000;
     std::vector<FramePtr> batch;
     for (auto& it : live) {
+      if (!it.finished && it.due_ns <= now && server_.flow_paused(it.req.conversation_id)) {
+        it.due_ns = now + std::max(delay_ms_, 1) * 1000000LL;  // flow control: hold this stream only
+        next_due = std::min(next_due, it.due_ns);
+        continue;
+      }
       while (!it.finished && it.due_ns <= now) {
         TokenMessage m;
         m.conversation_id = it.req.conversation_id;

@@ -27,6 +27,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "bus.h"
@@ -51,6 +52,11 @@ struct ServerConfig {
   int keepalive_ms = 15000;          // sse_handler.go:182
   int first_token_timeout_ms = 30000;  // sse_handler.go:395
   size_t max_pending_bytes = 4 << 20;  // per-connection output cap before token frames are dropped
+  // Per-conversation flow control: when every subscriber of a conversation has more than this many
+  // bytes queued, the engine pauses that sequence's decode (others keep going) until the queues drain
+  // below a quarter of it.  0 disables (slow consumers then only lose frames past max_pending_bytes).
+  size_t flow_high_water = 256 << 10;
+  int socket_sndbuf = 0;  // SO_SNDBUF for accepted sockets (0 = kernel autotuning); smaller = earlier backpressure
   size_t replay_max = 4096;
   int retention_s = 300;
   std::string ui_html;  // served at GET / when non-empty
@@ -104,12 +110,18 @@ class Server {
   void set_ready(bool on) { ready_.store(on); }
   // Conversations whose last subscriber left before completion (engine may abort them).
   std::vector<std::string> pop_cancellations();
+  // Flow-control transitions since the last call: (conversation, paused).
+  std::vector<std::pair<std::string, bool>> pop_flow_events();
   // Actual bound ports (useful with port 0 requests in tests): role -> port.
   int bound_port(const std::string& role) const;
 
   // internal (used by IoThread)
   void submit_chat(ChatRequest r);
   void note_cancel(const std::string& conv_id);
+  // A subscriber of `conv_id` crossed the high-water mark (+1), drained (-1), or the subscriber set
+  // changed (0): re-evaluate whether the conversation is paused.
+  void flow_update(const std::string& conv_id, int delta);
+  bool flow_paused(const std::string& conv_id);
   bool local_engine() const { return local_engine_.load(); }
   bool ready() const { return ready_.load(); }
   // Edge without a local engine: start relaying `conv_id` from the upstream origin (no-op otherwise).
@@ -133,6 +145,10 @@ class Server {
   std::atomic<uint64_t> next_req_{1};
   std::mutex cancel_mu_;
   std::vector<std::string> cancels_;
+  std::mutex flow_mu_;
+  std::unordered_map<std::string, std::pair<int, bool>> flow_;  // congested subscribers, paused
+  std::vector<std::pair<std::string, bool>> flow_events_;  // bounded: consumers also time pauses out
+  std::atomic<int> n_paused_{0};
   std::vector<std::pair<std::string, int>> ports_;
   friend class IoThread;
 };

@@ -4,7 +4,7 @@
 // services (src/sse-adapter/main.go:29-40, src/llm-stream-proxy/main.go:70-96):
 //   SSE_PORT (8080) METRICS_PORT (9090) ORIGIN_PORT (8081, or PORT) RESP_PORT (-1 = off; 6379)
 //   LLM_PROXY_URL UPSTREAM_URL (edge: relay tokens from the origin's SSE port) INSPECTION_MODE
-//   INSPECTION_BUFFER_MS LOG_LEVEL IO_THREADS
+//   INSPECTION_BUFFER_MS LOG_LEVEL IO_THREADS FLOW_HIGH_WATER
 //   UI_PATH (chat page served at GET /) STUB_TOKENS (50; 0 = no stub) STUB_TOKEN_DELAY_MS (50) STUB_WORKERS (2)
 #include <csignal>
 #include <cstdio>
@@ -37,6 +37,7 @@ int main() {
   }
   c.inspection = parse_inspection_mode(env_str("INSPECTION_MODE", "disabled"));
   c.inspection_buffer_ms = (int)env_long("INSPECTION_BUFFER_MS", 150);
+  c.flow_high_water = (size_t)env_long("FLOW_HIGH_WATER", (long)c.flow_high_water);
   const int stub_tokens = (int)env_long("STUB_TOKENS", 50);
   const int stub_delay = (int)env_long("STUB_TOKEN_DELAY_MS", 50);
   c.local_engine = stub_tokens > 0;

@@ -17,6 +17,11 @@ Per ``step()`` (host, a few hundred microseconds of Python):
 5. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
    earlier steps: sequence numbers, EOS / max_tokens stops, TTFT / ITL accounting.
 
+Flow control: a sequence whose subscribers all fall behind is *paused* (``set_paused``): its slot stays
+in the batch with ``active = 0``, so the decode graph neither advances its position nor writes its KV,
+and it resumes exactly where it stopped.  Everyone else keeps decoding.  The reference instead dropped
+frames once a subscriber's 100-slot channel filled (``src/sse-adapter/sse_handler.go:147-156``).
+
 The GPU is never idle waiting for the host: step ``t+1`` is enqueued before row ``t`` is read.  Stops
 discovered late (EOS) cost at most one wasted decode step for that slot, and the slot's pages are
 only reused by work enqueued after the stop, so stream order makes reuse safe.
@@ -72,6 +77,8 @@ class Sequence:
     last_token_ns: int = 0
     aborted: bool = False
     stop_after_enqueue: bool = False
+    paused: bool = False        # flow control: held out of the decode batch (KV and position kept)
+    paused_at: float = 0.0
 
 
 class _Drain:
@@ -107,7 +114,7 @@ class _Drain:
 class LLMEngine:
     def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 2048,
                  idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
-                 pipeline_depth: int = 1):
+                 pipeline_depth: int = 1, max_pause_s: float = 30.0):
         self.r = runner
         self.eos_id = eos_id
         self.alloc = BlockAllocator(runner.kv.num_blocks)
@@ -115,6 +122,7 @@ class LLMEngine:
         self.idle_prefill_budget = idle_prefill_budget or runner.max_prefill_tokens
         self.default_params = default_params or SamplingParams()
         self.depth = pipeline_depth
+        self.max_pause_s = max_pause_s
         self.waiting: deque = deque()
         self.slots: list = [None] * runner.max_batch
         self.by_conv: dict = {}
@@ -124,7 +132,8 @@ class LLMEngine:
         self._rid = itertools.count(1)
         self._dirty_slots: set = set()
         self.ring_head = int(runner.ring_counter.item()) if runner.device.type == "cuda" else int(runner.ring_counter[0])
-        self.stats = {"steps": 0, "decode_steps": 0, "prefill_tokens": 0, "tokens": 0, "last_step_s": 0.0}
+        self.stats = {"steps": 0, "decode_steps": 0, "prefill_tokens": 0, "tokens": 0, "last_step_s": 0.0,
+                      "pauses": 0}
         self.on_ttft = None
         self.on_itl = None
 
@@ -151,8 +160,34 @@ class LLMEngine:
             self._finish(s, [], reason="abort")
         return True
 
+    def set_paused(self, conversation_id: str, paused: bool) -> bool:
+        """Flow control: hold (or release) one sequence's decode.  Returns whether anything changed."""
+        s = self.by_conv.get(conversation_id)
+        if s is None or s.state == "finished" or s.paused == paused:
+            return False
+        s.paused = paused
+        s.paused_at = time.monotonic()
+        if paused:
+            self.stats["pauses"] += 1
+        else:
+            s.last_token_ns = 0  # the held interval is not an inter-token latency sample
+        if s.slot >= 0:
+            self._dirty_slots.add(s.slot)
+        return True
+
+    def expired_pauses(self, now: float | None = None) -> list:
+        """Conversations paused for longer than ``max_pause_s`` (the caller resumes them)."""
+        now = time.monotonic() if now is None else now
+        return [c for c, s in self.by_conv.items() if s.paused and now - s.paused_at > self.max_pause_s]
+
     def has_work(self) -> bool:
         return bool(self.waiting) or any(s is not None for s in self.slots) or bool(self.inflight)
+
+    def runnable(self) -> bool:
+        """Work a step would make progress on (paused decode sequences are not)."""
+        if self.waiting or self.inflight:
+            return True
+        return any(s is not None and (not s.paused or s.aborted or s.state != "decode") for s in self.slots)
 
     def num_running(self) -> int:
         return sum(1 for s in self.slots if s is not None)
@@ -172,7 +207,7 @@ class LLMEngine:
         for i, s in enumerate(self.slots):
             if s is None:
                 continue
-            if s.state == "decode" and not s.aborted and not s.stop_after_enqueue:
+            if s.state == "decode" and not s.aborted and not s.stop_after_enqueue and not s.paused:
                 active[i] = 1
             temp[i] = s.params.temperature
             topk[i] = s.params.top_k
@@ -281,7 +316,7 @@ class LLMEngine:
             producers += [(s.slot, s) for s in prefill_done]
             ran = True
         dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
-               and not s.stop_after_enqueue]
+               and not s.stop_after_enqueue and not s.paused]
         if dec:
             hi = max(s.slot for s in dec) + 1
             B = next(b for b in batch_buckets(r.max_batch) if b >= hi)

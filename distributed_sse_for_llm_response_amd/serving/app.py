@@ -55,7 +55,7 @@ def build_engine(cfg: ServeConfig, device=None, comm=None):
                              device=device, comm=comm)
         runner.capture()
     tok = get_tokenizer(mcfg.vocab_size, cfg.tokenizer_path or None)
-    engine = LLMEngine(runner, eos_id=tok.eos_id, prefill_budget=cfg.prefill_budget,
+    engine = LLMEngine(runner, eos_id=tok.eos_id, prefill_budget=cfg.prefill_budget, max_pause_s=cfg.max_pause_s,
                        default_params=SamplingParams(temperature=cfg.temperature, max_tokens=cfg.max_tokens))
     return engine, tok
 
@@ -98,6 +98,11 @@ class EngineLoop(threading.Thread):
             max_tokens=req["max_tokens"] if req["max_tokens"] > 0 else d.max_tokens,
             seed=req["seed"] if req["seed"] >= 0 else None, ignore_eos=bool(req.get("ignore_eos", False)))
 
+    def flow_events(self) -> list:
+        """Flow-control transitions from the runtime plus pauses that outlived ``max_pause_s``."""
+        ev = list(self.rt.pop_flow_events())
+        return ev + [(c, False) for c in self.engine.expired_pauses()]
+
     def publish(self, events):
         if not events:
             return
@@ -135,13 +140,17 @@ class EngineLoop(threading.Thread):
         gc.freeze()
         try:
             while not self.stop_flag.is_set() and not self._shutdown():
-                busy = self.engine.has_work()
-                for req in self.rt.poll_requests(256, 0 if busy else 20):
+                busy = self.engine.runnable()
+                # only paused streams left: wait briefly so their resume events get through
+                wait = 0 if busy else (2 if self.engine.has_work() else 20)
+                for req in self.rt.poll_requests(256, wait):
                     self.engine.add_request(req["conversation_id"], self.tok.chat_prompt(req["message"]),
                                             self._params(req), arrival_ns=req["arrival_ns"])
                 for conv in self.rt.pop_cancellations():
                     self.engine.abort(conv)
-                if not self.engine.has_work():
+                for conv, paused in self.flow_events():
+                    self.engine.set_paused(conv, paused)
+                if not self.engine.runnable():
                     self.last_progress = time.monotonic()
                     continue
                 self.tracer.begin(self.steps)

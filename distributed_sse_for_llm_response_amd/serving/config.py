@@ -6,6 +6,8 @@ Reference keys (same names, same defaults where they apply here):
   services default to 8080 and they now share a process), LLM_PROXY_URL, INSPECTION_MODE,
   INSPECTION_BUFFER_MS, LOG_LEVEL, MODEL_NAME, REDIS_ADDR (the RESP ingest port, e.g. ":6379").
 Topology keys (new): UPSTREAM_URL (edge: relay conversations from the origin), UI_PATH.
+Flow control (new): FLOW_HIGH_WATER (bytes queued for every subscriber of a conversation before its decode
+  pauses; 0 = off), MAX_PAUSE_S (a paused stream resumes after this long regardless).
 Engine keys (new): TP, DP, DP_PREFIX, DP_WORKER_TIMEOUT_MS, MAX_MODEL_LEN, MAX_BATCH, KV_BLOCK (fixed 32), GPU_MEMORY_UTILIZATION,
   SEED, MAX_TOKENS, PREFILL_BUDGET, TOKENIZER_PATH, WEIGHTS_PATH.
 """
@@ -43,6 +45,8 @@ class ServeConfig:
     model_name: str = "mistralai/Mistral-7B-Instruct-v0.3"
     keepalive_ms: int = 15000
     first_token_timeout_ms: int = 30000
+    flow_high_water: int = 256 << 10   # per-conversation backpressure (csrc/runtime/server.h)
+    max_pause_s: float = 30.0
     # engine
     engine: str = "gpu"          # gpu | cpu (tiny reference-op model) | stub (C++ token generator)
     model: str = "mistral-7b-v0.3"
@@ -76,6 +80,8 @@ class ServeConfig:
         c.llm_proxy_url = _env("LLM_PROXY_URL", c.llm_proxy_url)
         c.upstream_url = _env("UPSTREAM_URL", c.upstream_url)
         c.ui_path = _env("UI_PATH", c.ui_path)
+        c.flow_high_water = _env("FLOW_HIGH_WATER", c.flow_high_water, int)
+        c.max_pause_s = _env("MAX_PAUSE_S", c.max_pause_s, float)
         c.inspection_mode = _env("INSPECTION_MODE", c.inspection_mode)
         c.inspection_buffer_ms = _env("INSPECTION_BUFFER_MS", c.inspection_buffer_ms, int)
         c.log_level = _env("LOG_LEVEL", c.log_level)
@@ -127,7 +133,7 @@ class ServeConfig:
         d = asdict(self)
         keys = ("host", "sse_port", "origin_port", "metrics_port", "resp_port", "io_threads", "llm_proxy_url",
                 "upstream_url", "inspection_mode", "inspection_buffer_ms", "model_name", "keepalive_ms",
-                "first_token_timeout_ms")
+                "first_token_timeout_ms", "flow_high_water")
         out = {k: d[k] for k in keys}
         if self.ui_path != "none":
             from pathlib import Path

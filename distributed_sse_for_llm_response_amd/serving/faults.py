@@ -102,7 +102,7 @@ class Watchdog(threading.Thread):
         while not self._stop.wait(self.period_s):
             if self.loop.error is not None:
                 return  # the loop itself dropped readiness
-            busy = self.loop.engine.has_work()
+            busy = self.loop.engine.runnable()  # streams paused by flow control are not a stall
             idle_for = time.monotonic() - self.loop.last_progress
             stalled = busy and idle_for > self.timeout_s
             if stalled and not self.stalled:

@@ -36,6 +36,8 @@ class TPFollowerLoop:
                 self.engine.add_request(conv, prompt, params, arrival_ns=arrival)
             for conv in plan["abort"]:
                 self.engine.abort(conv)
+            for conv, paused in plan["flow"]:
+                self.engine.set_paused(conv, paused)
             if plan["step"]:
                 self.engine.step()
 
@@ -46,17 +48,21 @@ class TPLeaderLoop(EngineLoop):
     def run(self):
         try:
             while not self.stop_flag.is_set():
-                busy = self.engine.has_work()
+                busy = self.engine.runnable()
                 adds, aborts = [], []
-                for req in self.rt.poll_requests(256, 0 if busy else 20):
+                wait = 0 if busy else (2 if self.engine.has_work() else 20)
+                for req in self.rt.poll_requests(256, wait):
                     p = self._params(req)
                     prompt = self.tok.chat_prompt(req["message"])
                     adds.append((req["conversation_id"], prompt, p, req["arrival_ns"]))
                 aborts = list(self.rt.pop_cancellations())
-                step = bool(adds) or busy
-                if not (adds or aborts or step):
+                flow = self.flow_events()  # pause timeouts are decided here, so all ranks agree
+                for conv, paused in flow:
+                    self.engine.set_paused(conv, paused)
+                step = bool(adds) or self.engine.runnable()
+                if not (adds or aborts or flow or step):
                     continue
-                dist.broadcast_object_list([{"add": adds, "abort": aborts, "step": step}], src=0)
+                dist.broadcast_object_list([{"add": adds, "abort": aborts, "flow": flow, "step": step}], src=0)
                 for conv, prompt, p, arrival in adds:
                     self.engine.add_request(conv, prompt, p, arrival_ns=arrival)
                 for conv in aborts:
