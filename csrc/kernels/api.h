@@ -27,6 +27,8 @@ struct GemmEpi {
   bf16* k_cache;          // [blocks, nkv, kBS, 128]
   bf16* v_cache;          // [blocks, nkv, 128, kBS] (token-permuted inside a page)
   int nh, nkv;
+  int num_slots;          // mode 4: KV slots in the cache (pages * kBS); checked build only
+  int rope_len;           // mode 4: rows of the rope table; checked build only
 };
 
 struct AttnParams {
@@ -35,6 +37,7 @@ struct AttnParams {
   const bf16* v_cache;
   const int* block_tables;  // [B, max_blocks]
   int max_blocks;
+  int num_blocks;           // pages in the KV cache (checked build: block-table entries must be below)
   const int* q_start;       // [B] first query row of the sequence in q / out
   const int* q_len;         // [B] number of query tokens (0 = inactive)
   const int* ctx_len;       // [B] number of keys in the cache including the queries
@@ -66,6 +69,7 @@ struct SampleParams {
   int* positions_inc;        // [B] or null: positions[b] += 1 for active rows
   float2* cand;              // [B, nchunks] (score, index-as-bits) candidates
   int nchunks;               // vocab chunks per row (unfiltered path)
+  int v_global;              // full vocabulary (all TP shards); checked build: sampled ids below it
 };
 
 }  // namespace dsse
@@ -86,12 +90,20 @@ hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::Samp
                             hipStream_t st);
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
                         const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
-                        hipStream_t st);
+                        int vocab, hipStream_t st);
 hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                               const int* slots, const float2* rope, void* q_out, void* k_cache,
-                              void* v_cache, hipStream_t st);
+                              void* v_cache, int num_slots, int rope_len, hipStream_t st);
 hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
 hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
-                            int max_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
+                            int max_blocks, int num_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
 hipError_t dsse_ring_advance(int* counter, hipStream_t st);
+// Checked build: first out-of-range index per kernel file (line, value, bound, count); zeros otherwise.
+hipError_t dsse_check_gemm_skinny(int* out, int clear);
+hipError_t dsse_check_gemm_stream(int* out, int clear);
+hipError_t dsse_check_gemm_xlds(int* out, int clear);
+hipError_t dsse_check_attention(int* out, int clear);
+hipError_t dsse_check_attention_prefill(int* out, int clear);
+hipError_t dsse_check_elementwise(int* out, int clear);
+hipError_t dsse_check_sampler(int* out, int clear);
 }

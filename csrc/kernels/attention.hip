@@ -68,7 +68,7 @@ paged_attention_kernel(AttnParams p) {
 
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   for (int kb = kbeg + 32 * kw; kb < kend; kb += 32 * KWV) {
-    const int page = bt[kb / kPage];
+    const int page = DSSE_IDX(bt[DSSE_IDX(kb / kPage, p.max_blocks, 0)], p.num_blocks, 0);
     const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
     const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
     // K rows for keys kb + r and kb + 16 + r, 64 contiguous bytes per lane each.
@@ -237,3 +237,5 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   }
   return hipGetLastError();
 }
+
+DSSE_CHECK_READER(dsse_check_attention)

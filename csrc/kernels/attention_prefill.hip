@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
       const int v = pc >> 10, off = pc & 1023;
       const int page = off >> 9, o2 = off & 511;
       const int pg = min(2 * j + page, npages - 1);  // pages past the context: harmless re-read, masked
-      const int blk = bt[pg];
+      const int blk = DSSE_IDX(bt[DSSE_IDX(pg, p.max_blocks, 0)], p.num_blocks, 0);
       const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
                                : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
       st[i] = ld_bf16x8(src);
@@ -243,3 +243,5 @@ extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p
   }
   return hipGetLastError();
 }
+
+DSSE_CHECK_READER(dsse_check_attention_prefill)

@@ -276,6 +276,8 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
   ep.v_cache = reinterpret_cast<bf16*>(v_cache.data_ptr());
   ep.nh = (int)nh;
   ep.nkv = (int)nkv;
+  ep.num_slots = (int)(k_cache.size(0) * dsse::kBS);
+  ep.rope_len = (int)rope.size(0);
   run_gemm(dsse::kQkvRope, x, w, ep);
 }
 
@@ -295,6 +297,7 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
   const void* dptr = nullptr;
   const void* eptr = nullptr;
   const int* iptr = nullptr;
+  int vocab = 0;
   if (embed.has_value()) {
     TORCH_CHECK(ids.has_value(), "embedding mode needs ids");
     check_gpu(*embed, "embed");
@@ -304,6 +307,7 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     mode = 2;
     eptr = embed->data_ptr();
     iptr = ids->data_ptr<int>();
+    vocab = (int)embed->size(0);
   } else if (delta.has_value()) {
     check_gpu(*delta, "delta");
     check_dtype(*delta, at::kBFloat16, "delta");
@@ -320,7 +324,7 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     pptr = part->data_ptr<float>();
   }
   DSSE_CHECK_HIP(dsse_rmsnorm(mode, M, resid.data_ptr<float>(), H, dptr, eptr, iptr, w.data_ptr(),
-                              y.data_ptr(), (float)eps, pptr, (int)nsplit, cur_stream()));
+                              y.data_ptr(), (float)eps, pptr, (int)nsplit, vocab, cur_stream()));
 }
 
 void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& rope,
@@ -336,7 +340,7 @@ void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slo
                                     slots.data_ptr<int>(),
                                     reinterpret_cast<const float2*>(rope.data_ptr<float>()),
                                     q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
-                                    cur_stream()));
+                                    (int)(k_cache.size(0) * dsse::kBS), (int)rope.size(0), cur_stream()));
 }
 
 void silu_mul(const Tensor& gu, Tensor& h) {
@@ -348,7 +352,7 @@ void silu_mul(const Tensor& gu, Tensor& h) {
 }
 
 void decode_prep(const Tensor& active, const Tensor& positions, const Tensor& block_tables,
-                 Tensor& slots, Tensor& ctx_len, Tensor& q_len) {
+                 Tensor& slots, Tensor& ctx_len, Tensor& q_len, int64_t num_blocks) {
   for (const Tensor* t : {&active, &positions, &block_tables, (const Tensor*)&slots, (const Tensor*)&ctx_len, (const Tensor*)&q_len}) {
     check_gpu(*t, "decode metadata");
     check_dtype(*t, at::kInt, "decode metadata");
@@ -358,7 +362,7 @@ void decode_prep(const Tensor& active, const Tensor& positions, const Tensor& bl
                   q_len.numel() >= B && block_tables.size(0) >= B, "decode metadata too short");
   DSSE_CHECK_HIP(dsse_decode_prep(B, active.data_ptr<int>(), positions.data_ptr<int>(),
                                   block_tables.data_ptr<int>(), (int)block_tables.size(1),
-                                  slots.data_ptr<int>(), ctx_len.data_ptr<int>(), q_len.data_ptr<int>(),
+                                  (int)std::min<int64_t>(num_blocks, INT32_MAX), slots.data_ptr<int>(), ctx_len.data_ptr<int>(), q_len.data_ptr<int>(),
                                   cur_stream()));
 }
 
@@ -405,6 +409,7 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   p.v_cache = reinterpret_cast<const bf16*>(v_cache.data_ptr());
   p.block_tables = block_tables.data_ptr<int>();
   p.max_blocks = (int)block_tables.size(1);
+  p.num_blocks = (int)k_cache.size(0);
   p.q_start = q_start.data_ptr<int>();
   p.q_len = q_len.data_ptr<int>();
   p.ctx_len = ctx_len.data_ptr<int>();
@@ -473,7 +478,7 @@ void sample_candidates(const Tensor& logits, const Tensor& temperature, const Te
 // Merge pass over cand_all [world, B, nchunks, 2] and commit: next_ids, ring[head], positions += 1.
 void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Tensor& next_ids,
                  const c10::optional<Tensor>& ring, const c10::optional<Tensor>& ring_counter,
-                 const c10::optional<Tensor>& positions_inc) {
+                 const c10::optional<Tensor>& positions_inc, int64_t vocab) {
   check_gpu(cand_all, "cand_all");
   check_gpu(next_ids, "next_ids");
   check_dtype(next_ids, at::kInt, "next_ids");
@@ -482,6 +487,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   TORCH_CHECK(next_ids.numel() >= B, "next_ids too short");
   dsse::SampleParams p{};
   p.nchunks = (int)cand_all.size(2);
+  p.v_global = (int)std::min<int64_t>(vocab, INT32_MAX);
   p.next_ids = next_ids.data_ptr<int>();
   if (active.has_value()) {
     TORCH_CHECK(active->numel() >= B, "active too short");
@@ -503,7 +509,34 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 3; }
+int64_t kernels_abi_version() { return 4; }
+
+#if DSSE_KERNEL_CHECKS
+bool kernels_checked() { return true; }
+#else
+bool kernels_checked() { return false; }
+#endif
+
+// Checked build: [7, 4] int32 (line, value, bound, count) of the first out-of-range index per kernel file,
+// in the order of kCheckFiles; all zeros in the default build.  Synchronises the device.
+const char* const kCheckFiles[7] = {"gemm_skinny.hip", "gemm_stream.hip", "gemm_xlds.hip", "attention.hip",
+                                    "attention_prefill.hip", "elementwise.hip", "sampler.hip"};
+Tensor kernel_checks(bool clear) {
+  using Reader = hipError_t (*)(int*, int);
+  static const Reader readers[7] = {dsse_check_gemm_skinny, dsse_check_gemm_stream, dsse_check_gemm_xlds,
+                                    dsse_check_attention, dsse_check_attention_prefill, dsse_check_elementwise,
+                                    dsse_check_sampler};
+  Tensor out = at::zeros({7, 4}, at::kInt);
+  if (!kernels_checked()) return out;
+  DSSE_CHECK_HIP(hipDeviceSynchronize());
+  for (int i = 0; i < 7; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
+  return out;
+}
+std::string kernel_check_files() {
+  std::string s;
+  for (const char* f : kCheckFiles) s += std::string(s.empty() ? "" : ",") + f;
+  return s;
+}
 
 }  // namespace
 
@@ -520,7 +553,7 @@ TORCH_LIBRARY(dsse, m) {
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("silu_mul(Tensor gu, Tensor(a!) h) -> ()");
   m.def("decode_prep(Tensor active, Tensor positions, Tensor block_tables, Tensor(a!) slots, "
-        "Tensor(b!) ctx_len, Tensor(c!) q_len) -> ()");
+        "Tensor(b!) ctx_len, Tensor(c!) q_len, int num_blocks=2147483647) -> ()");
   m.def("ring_advance(Tensor(a!) counter) -> ()");
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
@@ -528,8 +561,11 @@ TORCH_LIBRARY(dsse, m) {
   m.def("sample_candidates(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
-        "Tensor? ring_counter=None, Tensor(c!)? positions_inc=None) -> ()");
+        "Tensor? ring_counter=None, Tensor(c!)? positions_inc=None, int vocab=2147483647) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
+  m.def("kernels_checked() -> bool", &kernels_checked);
+  m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
+  m.def("kernel_check_files() -> str", &kernel_check_files);
 }
 
 TORCH_LIBRARY_IMPL(dsse, CUDA, m) {

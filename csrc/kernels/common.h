@@ -80,4 +80,41 @@ DEV uint4 philox4x32(uint4 ctr, uint2 key) {
 // Uniform in (0, 1]: never exactly 0 so -log(-log(u)) is finite.
 DEV float u01(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
 
+// ---- checked build (DSSE_KERNEL_CHECKS=1, `_build.py kernels-checked`) -----------------------------
+// Data-dependent indices the host cannot validate without a sync (block-table entries, KV slots, token
+// ids, RoPE positions, sampled ids) go through DSSE_IDX(v, bound, fallback).  In the checked build an
+// out-of-range value is recorded in this translation unit's g_check word (first violation: line, value,
+// bound; plus a count) and replaced by `fallback`, so the kernel never touches memory it does not own
+// and the GPU never faults; the host reads the words back with torch.ops.dsse.kernel_checks().  In the
+// default build DSSE_IDX is the identity and costs nothing.
+#if DSSE_KERNEL_CHECKS
+static __device__ int g_check[4];
+DEV int check_index(int v, int bound, int line, int fallback) {
+  if ((unsigned)v < (unsigned)bound) return v;
+  if (atomicCAS(&g_check[0], 0, line) == 0) {
+    g_check[1] = v;
+    g_check[2] = bound;
+  }
+  atomicAdd(&g_check[3], 1);
+  return fallback;
+}
+#define DSSE_IDX(v, bound, fallback) ::dsse::check_index((v), (bound), __LINE__, (fallback))
+#define DSSE_CHECK_READER(fn)                                                              \
+  extern "C" hipError_t fn(int* out, int clear) {                                          \
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(::dsse::g_check), 4 * sizeof(int)); \
+    if (e == hipSuccess && clear) {                                                        \
+      const int z[4] = {0, 0, 0, 0};                                                       \
+      e = hipMemcpyToSymbol(HIP_SYMBOL(::dsse::g_check), z, sizeof z);                     \
+    }                                                                                      \
+    return e;                                                                              \
+  }
+#else
+#define DSSE_IDX(v, bound, fallback) (v)
+#define DSSE_CHECK_READER(fn)                         \
+  extern "C" hipError_t fn(int* out, int) {           \
+    for (int i = 0; i < 4; ++i) out[i] = 0;           \
+    return hipSuccess;                                \
+  }
+#endif
+
 }  // namespace dsse

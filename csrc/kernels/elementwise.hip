@@ -22,7 +22,7 @@ __global__ void __launch_bounds__(1024)
 rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
                const bf16* __restrict__ embed, const int* __restrict__ ids,
                const bf16* __restrict__ w, bf16* __restrict__ y, float eps,
-               const float* __restrict__ part = nullptr, int nsplit = 0, int M = 0) {
+               const float* __restrict__ part = nullptr, int nsplit = 0, int M = 0, int vocab = 0) {
   const int m = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   float* rrow = resid + (size_t)m * H;
   constexpr int kMaxIt = 2;  // H <= 8192
@@ -35,7 +35,7 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
       const int i = (it * nt + tid) * 4;
       float4 x;
       if constexpr (MODE == 2) {
-        const bf16x4 e = *reinterpret_cast<const bf16x4*>(embed + (size_t)ids[m] * H + i);
+        const bf16x4 e = *reinterpret_cast<const bf16x4*>(embed + (size_t)DSSE_IDX(ids[m], vocab, 0) * H + i);
         x = make_float4(bf2f(e[0]), bf2f(e[1]), bf2f(e[2]), bf2f(e[3]));
       } else {
         x = *reinterpret_cast<const float4*>(rrow + i);
@@ -97,11 +97,13 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
 __global__ void __launch_bounds__(256)
 rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* __restrict__ positions,
                      const int* __restrict__ slots, const float2* __restrict__ rope,
-                     bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache) {
+                     bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
+                     int num_slots, int rope_len) {
   const int t = blockIdx.x;
   const int ncols = (hq + 2 * hkv) * 128;
   const bf16* row = qkv + (size_t)t * ncols;
-  const int pos = positions[t], slot = slots[t];
+  const int pos = DSSE_IDX(positions[t], rope_len, 0);
+  const int slot = slots[t] < 0 ? -1 : DSSE_IDX(slots[t], num_slots, -1);
   const int blk = slot >= 0 ? slot / kPageTok : 0, off = slot >= 0 ? slot % kPageTok : 0;
   // rotary part: (hq + hkv) units × 64 pairs
   for (int idx = threadIdx.x; idx < (hq + hkv) * 64; idx += blockDim.x) {
@@ -150,14 +152,16 @@ silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ h, int F, int T)
 // ---- decode-step metadata (runs first inside the captured graph) -----------------------------
 // For slot b: live sequences process the token at positions[b]; dead slots write nothing.
 __global__ void decode_prep_kernel(int B, const int* __restrict__ active, const int* __restrict__ positions,
-                                   const int* __restrict__ block_tables, int max_blocks,
+                                   const int* __restrict__ block_tables, int max_blocks, int num_blocks,
                                    int* __restrict__ slots, int* __restrict__ ctx_len,
                                    int* __restrict__ q_len) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   if (active[b]) {
     const int pos = positions[b];
-    slots[b] = block_tables[(size_t)b * max_blocks + pos / kPageTok] * kPageTok + pos % kPageTok;
+    const int page = DSSE_IDX(block_tables[(size_t)b * max_blocks + DSSE_IDX(pos / kPageTok, max_blocks, 0)],
+                              num_blocks, 0);
+    slots[b] = page * kPageTok + pos % kPageTok;
     ctx_len[b] = pos + 1;
     q_len[b] = 1;
   } else {
@@ -176,7 +180,7 @@ using namespace dsse;
 
 extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta,
                                    const void* embed, const int* ids, const void* w, void* y,
-                                   float eps, const float* part, int nsplit, hipStream_t st) {
+                                   float eps, const float* part, int nsplit, int vocab, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   const bf16* d = reinterpret_cast<const bf16*>(delta);
   const bf16* e = reinterpret_cast<const bf16*>(embed);
@@ -184,10 +188,10 @@ extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const v
   bf16* yp = reinterpret_cast<bf16*>(y);
   const int nt = std::min(1024, H / 4);  // host-checked: H % 256 == 0, H <= 8192
   switch (mode) {
-    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
-    case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M); break;
+    case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
+    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
+    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
+    case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -195,12 +199,13 @@ extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const v
 
 extern "C" hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                                          const int* slots, const float2* rope, void* q_out,
-                                         void* k_cache, void* v_cache, hipStream_t st) {
+                                         void* k_cache, void* v_cache, int num_slots, int rope_len,
+                                         hipStream_t st) {
   if (T <= 0) return hipSuccess;
   hipLaunchKernelGGL(rope_kv_write_kernel, dim3(T), dim3(256), 0, st,
                      reinterpret_cast<const bf16*>(qkv), hq, hkv, positions, slots, rope,
                      reinterpret_cast<bf16*>(q_out), reinterpret_cast<bf16*>(k_cache),
-                     reinterpret_cast<bf16*>(v_cache));
+                     reinterpret_cast<bf16*>(v_cache), num_slots, rope_len);
   return hipGetLastError();
 }
 
@@ -214,10 +219,10 @@ extern "C" hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipSt
 }
 
 extern "C" hipError_t dsse_decode_prep(int B, const int* active, const int* positions,
-                                       const int* block_tables, int max_blocks, int* slots,
+                                       const int* block_tables, int max_blocks, int num_blocks, int* slots,
                                        int* ctx_len, int* q_len, hipStream_t st) {
   hipLaunchKernelGGL(decode_prep_kernel, dim3((B + 255) / 256), dim3(256), 0, st, B, active,
-                     positions, block_tables, max_blocks, slots, ctx_len, q_len);
+                     positions, block_tables, max_blocks, num_blocks, slots, ctx_len, q_len);
   return hipGetLastError();
 }
 
@@ -225,3 +230,5 @@ extern "C" hipError_t dsse_ring_advance(int* counter, hipStream_t st) {
   hipLaunchKernelGGL(ring_advance_kernel, dim3(1), dim3(1), 0, st, counter);
   return hipGetLastError();
 }
+
+DSSE_CHECK_READER(dsse_check_elementwise)

@@ -26,19 +26,19 @@ DEV void epilogue(const GemmEpi& ep, float* part, int M, int N, int m, int tile,
     const int unit = tile >> 3, j = tile & 7;
     const int d = (r < 8) ? (8 * j + r) : (64 + 8 * j + (r - 8));
     if (unit < ep.nh + ep.nkv) {
-      const float2 cs = ep.rope[(size_t)ep.positions[m] * 64 + 8 * j + (r & 7)];
+      const float2 cs = ep.rope[(size_t)DSSE_IDX(ep.positions[m], ep.rope_len, 0) * 64 + 8 * j + (r & 7)];
       const float rot = (r < 8) ? (v * cs.x - partner * cs.y) : (v * cs.x + partner * cs.y);
       if (unit < ep.nh) {
         ep.q_out[(size_t)m * ep.nh * 128 + unit * 128 + d] = f2bf(rot);
       } else {
-        const int s = ep.slots[m];
+        const int s = ep.slots[m] < 0 ? -1 : DSSE_IDX(ep.slots[m], ep.num_slots, -1);
         if (s >= 0) {
           const int h = unit - ep.nh, blk = s / kBS, off = s % kBS;
           ep.k_cache[(((size_t)blk * ep.nkv + h) * kBS + off) * 128 + d] = f2bf(rot);
         }
       }
     } else {
-      const int s = ep.slots[m];
+      const int s = ep.slots[m] < 0 ? -1 : DSSE_IDX(ep.slots[m], ep.num_slots, -1);
       if (s >= 0) {
         const int h = unit - ep.nh - ep.nkv, blk = s / kBS, off = s % kBS;
         ep.v_cache[(((size_t)blk * ep.nkv + h) * 128 + d) * kBS + vperm_tok(off)] = f2bf(v);

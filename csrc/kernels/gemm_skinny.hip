@@ -141,20 +141,20 @@ skinny_gemm_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
           const int d = (r < 8) ? (8 * j + r) : (64 + 8 * j + (r - 8));
           if (m < M) {
             if (unit < ep.nh + ep.nkv) {
-              const float2 cs = ep.rope[(size_t)ep.positions[m] * 64 + 8 * j + (r & 7)];
+              const float2 cs = ep.rope[(size_t)DSSE_IDX(ep.positions[m], ep.rope_len, 0) * 64 + 8 * j + (r & 7)];
               // r < 8: v = x1, partner = x2 -> x1 cos - x2 sin ; r >= 8: v = x2 -> x2 cos + x1 sin
               const float rot = (r < 8) ? (v * cs.x - partner * cs.y) : (v * cs.x + partner * cs.y);
               if (unit < ep.nh) {
                 ep.q_out[(size_t)m * ep.nh * 128 + unit * 128 + d] = f2bf(rot);
               } else {
-                const int s = ep.slots[m];
+                const int s = ep.slots[m] < 0 ? -1 : DSSE_IDX(ep.slots[m], ep.num_slots, -1);
                 if (s >= 0) {
                   const int h = unit - ep.nh, blk = s / kBS, off = s % kBS;
                   ep.k_cache[(((size_t)blk * ep.nkv + h) * kBS + off) * 128 + d] = f2bf(rot);
                 }
               }
             } else {
-              const int s = ep.slots[m];
+              const int s = ep.slots[m] < 0 ? -1 : DSSE_IDX(ep.slots[m], ep.num_slots, -1);
               if (s >= 0) {
                 const int h = unit - ep.nh - ep.nkv, blk = s / kBS, off = s % kBS;
                 ep.v_cache[(((size_t)blk * ep.nkv + h) * 128 + d) * kBS + vperm(off)] = f2bf(v);
@@ -210,3 +210,5 @@ extern "C" hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const v
   }
   return hipErrorInvalidValue;
 }
+
+DSSE_CHECK_READER(dsse_check_gemm_skinny)

@@ -212,3 +212,5 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }
+
+DSSE_CHECK_READER(dsse_check_gemm_stream)

@@ -193,3 +193,5 @@ extern "C" hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth
   if (e != hipSuccess) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }
+
+DSSE_CHECK_READER(dsse_check_gemm_xlds)

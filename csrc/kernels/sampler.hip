@@ -179,6 +179,7 @@ __global__ void sample_pick_kernel(const float2* __restrict__ cand, int world, i
       const float2 v = cand[((size_t)w * B + b) * p.nchunks + c];
       better(best, bidx, v.x, __float_as_int(v.y));
     }
+  bidx = DSSE_IDX(bidx, p.v_global, 0);  // no candidate (all logits NaN / -inf) is a bug upstream
   p.next_ids[b] = bidx;
   if (p.ring) p.ring[(size_t)(p.ring_counter[0] % p.ring_size) * p.ring_stride + b] = bidx;
   if (p.positions_inc) p.positions_inc[b] += 1;
@@ -203,3 +204,5 @@ extern "C" hipError_t dsse_sample_pick(int B, int world, const void* cand, const
                      reinterpret_cast<const float2*>(cand), world, B, *p);
   return hipGetLastError();
 }
+
+DSSE_CHECK_READER(dsse_check_sampler)

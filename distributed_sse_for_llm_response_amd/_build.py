@@ -68,7 +68,10 @@ def _parallel(jobs, verbose):
             f.result()
 
 
-KERNEL_VARIANTS = {"nt": ["-DDSSE_W_NT=1"]}  # experiment builds: libdsse_kernels_<variant>.so
+KERNEL_VARIANTS = {
+    "nt": ["-DDSSE_W_NT=1"],           # experiment build (non-temporal weight loads everywhere)
+    "checked": ["-DDSSE_KERNEL_CHECKS=1"],  # debug build: device-side index checks (common.h DSSE_IDX)
+}  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
 
 def kernels_so(variant: str | None = None) -> Path:

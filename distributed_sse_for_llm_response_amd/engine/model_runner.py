@@ -134,7 +134,7 @@ class ModelRunner:
         r = slice(0, B)
         eps = cfg.rms_eps
         ops.decode_prep(self.active[r], self.positions[r], self.block_tables[r], self.slots[r], self.ctx_len[r],
-                        self.q_len[r])
+                        self.q_len[r], self.kv.num_blocks)
         resid, x = self.resid[r], self.x[r]
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=self.ids[r])
         part, nparts = decode_partitioning(B, nkv, self.max_model_len)
@@ -219,7 +219,8 @@ class ModelRunner:
         else:
             cand_all = self._cand_all[B]
             self.comm.all_gather_into(cand_all, cand)
-        ops.sample_pick(cand_all, self.active[r], self.ids[r], self.ring, self.ring_counter, self.positions[r])
+        ops.sample_pick(cand_all, self.active[r], self.ids[r], self.ring, self.ring_counter, self.positions[r],
+                        vocab=self.cfg.vocab_size)
 
     def bucket_for(self, n_active_max_slot: int) -> int:
         for b in batch_buckets(self.max_batch):
@@ -367,7 +368,7 @@ class ModelRunner:
         else:
             cand_all = torch.zeros(comm.size, nL, nch, 2, **f32)
             comm.all_gather_into(cand_all, cand)
-        ops.sample_pick(cand_all, None, new_ids)
+        ops.sample_pick(cand_all, None, new_ids, vocab=cfg.vocab_size)
         self.ids.index_copy_(0, slot_idx, new_ids)
         self.ring[ring_row].index_copy_(0, slot_idx, new_ids)
         self.positions.index_copy_(0, slot_idx, last_pos + 1)

@@ -17,7 +17,7 @@ import torch
 
 from . import reference as ref
 
-_VARIANT = os.environ.get("DSSE_KERNELS_VARIANT", "")  # experiment builds (e.g. "nt"), see _build.py
+_VARIANT = os.environ.get("DSSE_KERNELS_VARIANT", "")  # "checked" (device index checks) or "nt", see _build.py
 _LIB = Path(__file__).resolve().parent.parent / "_lib" / (
     f"libdsse_kernels_{_VARIANT}.so" if _VARIANT else "libdsse_kernels.so")
 _loaded = False
@@ -33,7 +33,7 @@ def load_library(required: bool = False) -> bool:
         try:
             from .._build import build_kernels
 
-            build_kernels()
+            build_kernels(variant=_VARIANT or None)
         except Exception as e:  # noqa: BLE001 - reported below
             _load_error = f"build failed: {e}"
     if _LIB.exists():
@@ -123,9 +123,9 @@ def silu_mul(gu, h):
         ref.silu_mul(gu, h)
 
 
-def decode_prep(active, positions, block_tables, slots, ctx_len, q_len):
+def decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_blocks: int = 2**31 - 1):
     if _hip(active):
-        torch.ops.dsse.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
+        torch.ops.dsse.decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_blocks)
     else:
         ref.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
 
@@ -158,10 +158,11 @@ def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, activ
         ref.sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset)
 
 
-def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None):
+def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None,
+                vocab: int = 2**31 - 1):
     """Merge cand_all [world, B, C, 2] and commit: next_ids[b], ring[head][b], positions[b] += 1."""
     if _hip(cand_all):
-        torch.ops.dsse.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc)
+        torch.ops.dsse.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc, vocab)
     else:
         ref.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc)
 
@@ -173,3 +174,26 @@ def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids
     cand = torch.empty(B, nchunks if logits.is_cuda else 1, 2, device=logits.device, dtype=torch.float32)
     sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, 0)
     sample_pick(cand.unsqueeze(0), active, next_ids, ring, ring_counter, positions_inc)
+
+
+class KernelCheckError(RuntimeError):
+    """An out-of-range device index caught by the checked kernel build."""
+
+
+def kernel_checks(clear: bool = True, raise_on_error: bool = True) -> list:
+    """Read the checked build's violation words (``_build.py kernels-checked``, DSSE_KERNELS_VARIANT=checked).
+
+    Returns ``[(file, line, value, bound, count)]`` for every kernel file that recorded an out-of-range
+    index since the last clear; raises KernelCheckError when ``raise_on_error`` and any were found.  The
+    default build records nothing (empty list).  Synchronises the device.
+    """
+    load_library(required=True)
+    if not torch.ops.dsse.kernels_checked():
+        return []
+    words = torch.ops.dsse.kernel_checks(clear).tolist()
+    files = torch.ops.dsse.kernel_check_files().split(",")
+    bad = [(f, *w) for f, w in zip(files, words) if w[3] > 0]
+    if bad and raise_on_error:
+        raise KernelCheckError("; ".join(f"{f}:{ln} index {v} not below {b} ({n} times)" for f, ln, v, b, n in bad))
+    return bad
+

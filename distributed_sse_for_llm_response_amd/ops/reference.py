@@ -150,7 +150,7 @@ def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nspli
 
 
 # ---------------------------------------------------------------- decode metadata
-def decode_prep(active, positions, block_tables, slots, ctx_len, q_len):
+def decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_blocks: int = 2**31 - 1):
     B = active.numel()
     for b in range(B):
         if int(active[b]):
@@ -283,7 +283,7 @@ def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, activ
         cand[b, 0, 1] = float(idx)  # CPU encoding: the index as a float value (GPU: its bit pattern)
 
 
-def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None):
+def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positions_inc=None, vocab: int = 2**31 - 1):
     world, B, C, _ = cand_all.shape
     for b in range(B):
         if active is not None and not int(active[b]):

@@ -327,4 +327,21 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 3
+    assert torch.ops.dsse.kernels_abi_version() == 4
+    assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
+
+
+def test_checked_build_catches_bad_indices(gpu):
+    """The checked build (DSSE_KERNELS_VARIANT=checked) runs the model with no false positives and attributes
+    corrupted block tables / token ids / KV slots / RoPE positions to the right kernel without faulting."""
+    import subprocess
+    import sys
+
+    from distributed_sse_for_llm_response_amd import _build
+
+    _build.build_kernels(variant="checked")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "check_kernels.py")], capture_output=True,
+                       text=True, timeout=600, env={**os.environ, "DSSE_KERNELS_VARIANT": "checked"})
+    assert r.returncode == 0 and "CHECKS-OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
