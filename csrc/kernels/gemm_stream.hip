@@ -20,6 +20,10 @@
 // stored (MFMA output rows depend only on the same A row).
 #include "gemm_epilogue.h"
 
+#ifndef DSSE_W_DEFAULT
+#define DSSE_W_DEFAULT 0  // experiment build "wdef": default cache policy on the weight stream
+#endif
+
 namespace dsse {
 
 constexpr int kStreamCPS = 4;  // K-chunks of 128 per LDS slice
@@ -67,7 +71,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        wf[t][s] = SHARED_W ? ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s)
+        wf[t][s] = (SHARED_W || DSSE_W_DEFAULT) ? ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s)
                             : ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
   };
 

@@ -70,7 +70,8 @@ def _parallel(jobs, verbose):
 
 KERNEL_VARIANTS = {
     "nt": ["-DDSSE_W_NT=1"],           # experiment build (non-temporal weight loads everywhere)
-    "checked": ["-DDSSE_KERNEL_CHECKS=1"],  # debug build: device-side index checks (common.h DSSE_IDX)
+    "checked": ["-DDSSE_KERNEL_CHECKS=1"],
+    "wdef": ["-DDSSE_W_DEFAULT=1"],     # experiment build (default cache policy on gemm_stream weights)  # debug build: device-side index checks (common.h DSSE_IDX)
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
 

@@ -69,3 +69,36 @@ def test_configmap_env_keys_are_read_by_the_code():
                 if k == "HSA_ENABLE_IPC_MODE_LEGACY":
                     continue  # consumed by the ROCm runtime
                 assert f'"{k}"' in code, f"{os.path.relpath(f, ROOT)}: {k} is not read anywhere"
+
+
+def test_run_loadtest_renders_the_job():
+    import subprocess
+
+    out = subprocess.run(["bash", os.path.join(ROOT, "scripts", "run-loadtest.sh"), "--k8s", "-conversations", "100",
+                          "-tokens", "200", "-duration", "5m", "-chat"], env={**os.environ, "DRY_RUN": "1"},
+                         capture_output=True, text=True, check=True).stdout
+    job = yaml.safe_load(out)
+    assert job["kind"] == "Job"
+    args = job["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert args[args.index("-conversations") + 1] == "100" and args[args.index("-tokens") + 1] == "200"
+    assert "-chat" in args and args[-1] == "-json" and args[args.index("-sse") + 1] == "http://dsse-edge:80"
+
+
+def test_run_loadtest_local_against_a_stub_server():
+    """The wrapper's local mode drives the native load generator (RESP producers + SSE consumers)."""
+    import subprocess
+
+    r = rtmod.load().Runtime({"sse_port": 0, "origin_port": -1, "metrics_port": -1, "resp_port": 0,
+                              "host": "127.0.0.1", "io_threads": 2})
+    r.start()
+    try:
+        out = subprocess.run(["bash", os.path.join(ROOT, "scripts", "run-loadtest.sh"),
+                              "-sse", f"http://127.0.0.1:{r.bound_port('edge')}",
+                              "-redis", f"127.0.0.1:{r.bound_port('resp')}", "-conversations", "4", "-tokens", "6",
+                              "-token-delay", "5", "-duration", "10s", "-json"],
+                             capture_output=True, text=True, timeout=60)
+    finally:
+        r.stop()
+    assert out.returncode == 0, out.stderr
+    stats = json.loads(out.stdout.strip().splitlines()[-1])
+    assert stats["tokens_received"] == stats["tokens_published"] == 4 * 6, stats

@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--configs", default="skinny;x;x:DSSE_X_NW=4;x:DSSE_X_NT=2;x:DSSE_X_KS=512",
                     help="';'-separated; 'skinny', 'x' (X-in-LDS) or 's' (X-streaming), optionally ':K=V,K=V' env overrides")
+    ap.add_argument("--hot", action="store_true", help="one weight copy (Infinity-Cache resident when it fits)")
     ap.add_argument("--out", default="")
     ap.add_argument("--grid", action="store_true", help="sweep the X-in-LDS parameter grid")
     args = ap.parse_args()
@@ -82,7 +83,7 @@ def main():
         if args.ops and name not in args.ops.split(","):
             continue
         nbytes = N * K * 2
-        copies = max(2, (600 << 20) // nbytes + 1)
+        copies = 1 if args.hot else max(2, (600 << 20) // nbytes + 1)
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
         for M in [int(m) for m in args.M.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
