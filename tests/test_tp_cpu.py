@@ -10,7 +10,7 @@ import torch.multiprocessing as mp
 
 from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
 from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
-from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights, reference_forward
+from distributed_sse_for_llm_response_amd.models.mistral import SMALL, TINY, init_standard_weights, reference_forward
 from distributed_sse_for_llm_response_amd.parallel.comm import TPComm
 
 PROMPTS = [[5, 17, 99, 3, 8, 1000, 42], list(range(100, 150)), [7] * 33]
@@ -18,8 +18,7 @@ BTS = [[0, 1, 2], [10, 4, 5, 6], [20, 21, 22]]
 STEPS = 5
 
 
-def _generate(rank, world, temperature):
-    cfg = TINY
+def _generate(rank, world, temperature, cfg=TINY):
     std = init_standard_weights(cfg, seed=3)
     comm = TPComm(rank=rank, size=world, group=None) if world > 1 else TPComm()
     w = convert_standard(cfg, std, tp_rank=rank, tp_size=world)
@@ -38,11 +37,11 @@ def _generate(rank, world, temperature):
     return gen
 
 
-def _worker(rank, world, port, temperature, out):
+def _worker(rank, world, port, temperature, out, cfg=TINY):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out[rank] = _generate(rank, world, temperature)
+        out[rank] = _generate(rank, world, temperature, cfg)
     finally:
         dist.destroy_process_group()
 
@@ -55,10 +54,10 @@ def _port():
     return p
 
 
-def _tp_run(world, temperature):
+def _tp_run(world, temperature, cfg=TINY):
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, _port(), temperature, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _port(), temperature, out, cfg), nprocs=world, join=True)
         return [out[r] for r in range(world)]
 
 
@@ -85,6 +84,15 @@ def test_tp2_stochastic_sampling_is_tp_invariant():
     res = _tp_run(2, 1.0)
     assert res[0] == res[1]
     assert res[0] == _generate(0, 1, 1.0)
+
+
+@pytest.mark.timeout(900)
+def test_tp4_matches_tp1():
+    """TP=4 (4 KV heads -> one per rank, vocab in four shards): greedy and sampled tokens equal TP=1."""
+    for temperature in (0.0, 1.0):
+        res = _tp_run(4, temperature, SMALL)
+        assert all(r == res[0] for r in res), "TP ranks disagree on the sampled tokens"
+        assert res[0] == _generate(0, 1, temperature, SMALL)
 
 
 def _free_port():
