@@ -55,6 +55,8 @@ class Metrics {
   Counter sse_total_connections;
   Counter sse_messages_delivered_total;
   Histogram sse_connection_duration_seconds;
+  // token timestamp (engine drain / producer publish) -> written to the subscriber's socket
+  Histogram sse_delivery_latency_seconds;
   // origin proxy
   Gauge active_chats;
   // bus / delivery

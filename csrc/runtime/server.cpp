@@ -602,6 +602,10 @@ void IoThread::deliver_token(Conn& c, const FramePtr& f) {
   append_chunk(c.out, out->bytes.data(), out->bytes.size());
   c.last_write_mono = mono_ns();
   metrics().sse_messages_delivered_total.inc();
+  if (out->timestamp > 0) {  // producers may send ms timestamps (run-demo.sh): keep plausible values only
+    const double d = (now_ns() - out->timestamp) * 1e-9;
+    if (d >= 0 && d < 60) metrics().sse_delivery_latency_seconds.observe(d);
+  }
   if (out->done) {
     end_sse(c, true);
     return;

@@ -170,6 +170,9 @@ def test_health_ready_metrics(stub_rt):
     for name in ("sse_active_connections", "sse_total_connections", "sse_messages_delivered_total",
                  'sse_connection_duration_seconds_bucket{le="600"}', "bus_published_total"):
         assert name in m
+    # every delivered token frame carries a fresh ns timestamp: the delivery-latency histogram saw them
+    assert _metric(stub_rt, "sse_delivery_latency_seconds_count") >= 7
+    assert _metric(stub_rt, 'sse_delivery_latency_seconds_bucket{le="0.5"}') >= 7
 
 
 def test_origin_api(stub_rt):
