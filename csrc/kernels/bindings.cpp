@@ -91,10 +91,12 @@ struct SCfg {
   int mt, nt, nw, rd, S;
   bool ok;
 };
+// 64 < M <= 256: one workgroup holds all rows (mt 8 / 16, X slices of 256 / 128 columns); M > 256: row
+// blocks of 64 (mt 4, L2-shared weights).
 SCfg pick_stream(int M, int N, int K) {
   SCfg c{};
-  c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  c.nt = M > 64 ? 1 : env_int("DSSE_S_NT", 1);  // row-block mode (M > 64) is instantiated for nt = 1
+  c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : (M <= 256 ? 16 : 4))));
+  c.nt = M > 64 ? 1 : env_int("DSSE_S_NT", 1);  // the M > 64 kernels are instantiated for nt = 1
   // 8 waves per workgroup when that still gives ~one workgroup per CU without split-K (gate_up,
   // LM head), else 4 (narrow O / down / QKV: more, shorter workgroups; measured, profiles/gemm_stream_r1.md)
   c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
@@ -104,9 +106,12 @@ SCfg pick_stream(int M, int N, int K) {
   if ((N / 16) % c.nw != 0) c.nw = 4;
   c.rd = env_int("DSSE_S_RD", 1);
   if (c.nt == 2 || c.rd != 2 || M > 64) c.rd = 1;
-  c.ok = K % 512 == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
+  if (c.mt == 8) c.rd = 2;
+  if (c.mt == 16) c.rd = 4;
+  const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
+  c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
-  const int wgs = N / (16 * c.nt) / c.nw * ((M + 63) / 64), slices = K / 512;
+  const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
   int S = env_int("DSSE_S_SPLIT", 0);
   if (S <= 0 || slices % S != 0) {
     // smallest split that gives ~one workgroup per CU (256 CUs), never more than 320 workgroups
@@ -122,7 +127,7 @@ SCfg pick_stream(int M, int N, int K) {
   return c;
 }
 
-constexpr int kMaxDecodeM = 512;  // gemm_stream row-block mode above 64 rows
+constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
 // whole K-slice staged (gemm_xlds.hip), 2 = X streamed through LDS slices (gemm_stream.hip).

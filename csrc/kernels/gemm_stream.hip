@@ -1,4 +1,4 @@
-// X-streaming decode GEMM:  Y[M, N] = X[M, K] · W[N, K]ᵀ, 16 < M <= 64 (any M <= 64 works).
+// X-streaming decode GEMM:  Y[M, N] = X[M, K] · W[N, K]ᵀ, 16 < M <= 256.
 //
 // Successor of gemm_xlds.hip for the batched decode step.  gemm_xlds stages a whole K-slice of X
 // (up to 128 KiB) into LDS before its waves start streaming weights, and splits K across
@@ -26,7 +26,9 @@
 
 namespace dsse {
 
-constexpr int kStreamCPS = 4;  // K-chunks of 128 per LDS slice
+// K-chunks of 128 per LDS slice: two slices of 16·MT rows stay within 128 KiB of LDS (MT <= 4: 512 columns,
+// MT = 8 (128 rows): 256, MT = 16 (256 rows): 128 — one barrier per 2048 MFMA cycles per SIMD there).
+constexpr int stream_cps(int mt) { return mt <= 4 ? 4 : (mt <= 8 ? 2 : 1); }
 
 // Row blocks (M > 64, e.g. a 256-sequence decode bucket): the grid is (tile-group workgroups x MB row
 // blocks of 64) and workgroups are renumbered so that the MB row blocks of one tile group are consecutive
@@ -36,7 +38,7 @@ template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
                    int Kr, GemmEpi ep, float* __restrict__ part) {
-  constexpr int CPS = kStreamCPS;
+  constexpr int CPS = stream_cps(MT);
   constexpr int MP = 16 * MT;
   constexpr int ROWB = CPS * 256;                        // bytes of one X row in a slice
   constexpr int BUF = MP * ROWB;                         // bytes per slice buffer
@@ -157,7 +159,7 @@ static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, 
                            float* part, hipStream_t st) {
   const int TG = N / (16 * NT);
   const int MB = SHARED_W ? (M + 16 * MT - 1) / (16 * MT) : 1;
-  const size_t lds = (size_t)2 * 16 * MT * kStreamCPS * 256;
+  const size_t lds = (size_t)2 * 16 * MT * stream_cps(MT) * 256;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>),
@@ -173,11 +175,16 @@ static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, 
 template <int MODE>
 static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
                                 int S, const GemmEpi& ep, float* part, hipStream_t st) {
-  if (M > 64) {  // row blocks with L2-shared weights (64-row MFMA tiles, one or eight waves)
+  if (M > 16 * mt) {  // row blocks with L2-shared weights (64-row MFMA tiles, one or eight waves)
     if (mt == 4 && nt == 1 && nw == 4) return launch_s<4, 1, 4, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
     if (mt == 4 && nt == 1 && nw == 8) return launch_s<4, 1, 8, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
     return hipErrorInvalidValue;
   }
+  // 128 / 256 rows in one workgroup: the weight ring stays 4 chunks deep (rd slices of 2 / 1 chunks)
+  if (mt == 8 && nt == 1 && nw == 8 && rd == 2) return launch_s<8, 1, 8, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  if (mt == 8 && nt == 1 && nw == 4 && rd == 2) return launch_s<8, 1, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  if (mt == 16 && nt == 1 && nw == 8 && rd == 4) return launch_s<16, 1, 8, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  if (mt == 16 && nt == 1 && nw == 4 && rd == 4) return launch_s<16, 1, 4, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
 #define DSSE_S_CASE(MT_, NT_, NW_, RD_)         \
   if (mt == MT_ && nt == NT_ && nw == NW_ && rd == RD_) \
     return launch_s<MT_, NT_, NW_, RD_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
@@ -191,9 +198,10 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
 
 }  // namespace dsse
 
-// rd: weight-ring depth in LDS slices (1: 4 chunks = 16 KiB per wave in flight, 2: 8 chunks).
-// Shape contract (checked by the caller): K % (512 S) == 0, (N / (16 nt)) % nw == 0, M <= 16 mt <= 64, or
-// M > 64 with mt = 4, nt = 1, rd = 1 (row blocks of 64).
+// rd: weight-ring depth in LDS slices (mt <= 4: 1 = 4 chunks = 16 KiB per wave in flight, 2 = 8 chunks;
+// mt = 8: 2, mt = 16: 4, i.e. 4 chunks).
+// Shape contract (checked by the caller): K % (128 stream_cps(mt) S) == 0, (N / (16 nt)) % nw == 0,
+// M <= 16 mt with mt in {1, 2, 4, 8, 16}, or M > 64 with mt = 4, nt = 1, rd = 1 (row blocks of 64).
 // part: fp32 [S, M, N] workspace when S > 1.  partial_only: leave the slabs for the consumer (the fused
 // residual + RMSNorm kernel) instead of reducing them here.
 extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X,

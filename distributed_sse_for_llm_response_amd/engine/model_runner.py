@@ -23,6 +23,7 @@ batch bucket into a torch.cuda.CUDAGraph (a hipGraph on ROCm).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -36,14 +37,18 @@ from .weights import EngineWeights
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
-DECODE_GEMM_MAX_M = 64  # largest batch the fused decode GEMMs take (gemm_skinny / gemm_stream); above: hipBLASLt
+# Largest decode bucket on the engine's own GEMMs (gemm_skinny / gemm_stream with fused epilogues); larger
+# buckets use hipBLASLt + separate RoPE / SiLU / norm kernels.  Measured per layer (qkv + o + gate_up + down,
+# profiles/gemm_mid_m_r1.md): 128 rows 156 vs 185 us, 192 rows 207 vs 236, 256 rows 241 vs 194.
+DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "192"))
 
 
 def batch_buckets(max_batch: int):
+    """Captured decode batch sizes: powers of two up to 64, then every 64 (less padding at 65-256 streams)."""
     out, b = [], 1
     while b < max_batch:
         out.append(b)
-        b *= 2
+        b = b * 2 if b < 64 else b + 64
     out.append(max_batch)
     return sorted(set(out))
 
@@ -171,12 +176,12 @@ class ModelRunner:
         ops.ring_advance(self.ring_counter)
 
     def _decode_layers_wide(self, B: int, resid, x, part: int, nparts: int) -> None:
-        """Decode step for buckets above 64 sequences (e.g. 256 streams per GPU, BASELINE config 3).
+        """Decode step for buckets above DECODE_GEMM_MAX_M sequences (256 streams per GPU, BASELINE config 3).
 
-        At B > 64 a weight byte feeds > 64 rows and the projections become compute-heavy skinny GEMMs:
+        At B > 192 a weight byte feeds > 192 rows and the projections become compute-heavy skinny GEMMs:
         they run on hipBLASLt (the plain-library GEMM path, standard weight layout, same as prefill) with the
         engine's own RoPE/KV-write, SiLU·mul and residual+RMSNorm kernels around them; attention and the
-        sampler are the decode kernels.  The LM head stays on the fp32-output decode GEMM in 64-row blocks
+        sampler are the decode kernels.  The LM head stays on the fp32-output decode GEMM in 256-row blocks
         (sampling wants fp32 logits).  Still one captured graph per bucket.
         """
         w, cfg, comm = self.w, self.cfg, self.comm
@@ -202,8 +207,9 @@ class ModelRunner:
             comm.all_reduce(down)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             ops.rmsnorm(resid, w_next, x, eps, delta=down)
-        for b0 in range(0, B, DECODE_GEMM_MAX_M):
-            b1 = min(B, b0 + DECODE_GEMM_MAX_M)
+        step = 256 if DECODE_GEMM_MAX_M > 2 else DECODE_GEMM_MAX_M  # one 256-row call streams the head once
+        for b0 in range(0, B, step):
+            b1 = min(B, b0 + step)
             ops.gemm_out(x[b0:b1], w.lm_head_t, self.logits[b0:b1])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
