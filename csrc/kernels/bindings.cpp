@@ -96,18 +96,19 @@ struct SCfg {
 SCfg pick_stream(int M, int N, int K) {
   SCfg c{};
   c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : (M <= 256 ? 16 : 4))));
-  c.nt = M > 64 ? 1 : env_int("DSSE_S_NT", 1);  // the M > 64 kernels are instantiated for nt = 1
+  c.nt = M > 256 ? 1 : env_int("DSSE_S_NT", 1);  // row blocks (M > 256) are instantiated for nt = 1
   // 8 waves per workgroup when that still gives ~one workgroup per CU without split-K (gate_up,
   // LM head), else 4 (narrow O / down / QKV: more, shorter workgroups; measured, profiles/gemm_stream_r1.md)
   c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
-  if (c.nt == 2) c.nw = 8;  // instantiated (nt, nw): (1, 8), (2, 8), (1, 4) — gemm_stream.hip
+  if (c.nt == 2 && c.mt <= 4) c.nw = 8;  // instantiated (nt, nw): (1, 8), (2, 8), (1, 4) — gemm_stream.hip
+  if (c.nt == 2 && c.mt >= 8) c.nw = 4;   // mt 8 / 16: (1, 8), (1, 4), (2, 4)
   if (c.nw != 4) c.nw = 8;
   if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
   if ((N / 16) % c.nw != 0) c.nw = 4;
   c.rd = env_int("DSSE_S_RD", 1);
   if (c.nt == 2 || c.rd != 2 || M > 64) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
-  if (c.mt == 16) c.rd = 4;
+  if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
   const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
   c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;

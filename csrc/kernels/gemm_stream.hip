@@ -185,6 +185,9 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
   if (mt == 8 && nt == 1 && nw == 4 && rd == 2) return launch_s<8, 1, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   if (mt == 16 && nt == 1 && nw == 8 && rd == 4) return launch_s<16, 1, 8, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   if (mt == 16 && nt == 1 && nw == 4 && rd == 4) return launch_s<16, 1, 4, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  // two column tiles per wave: every X fragment read from LDS feeds two MFMAs
+  if (mt == 8 && nt == 2 && nw == 4 && rd == 2) return launch_s<8, 2, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  if (mt == 16 && nt == 2 && nw == 4 && rd == 2) return launch_s<16, 2, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
 #define DSSE_S_CASE(MT_, NT_, NW_, RD_)         \
   if (mt == MT_ && nt == NT_ && nw == NW_ && rd == RD_) \
     return launch_s<MT_, NT_, NW_, RD_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
