@@ -93,7 +93,8 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
 // ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
 // qkv: [T, (hq + 2 hkv) * 128] bf16 in the engine's permuted column order (inside each 16-column
 // tile j of a head: columns 0..7 = dims 8j..8j+7, columns 8..15 = dims 64+8j..64+8j+7).
-// One workgroup per token, one thread per (unit, pair) for rotary units and per column for V.
+// One workgroup per token; a thread rotates 8 pairs of one (unit, tile j) with 16-byte loads and stores,
+// or moves 8 V columns into the transposed, token-permuted V page.
 __global__ void __launch_bounds__(256)
 rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* __restrict__ positions,
                      const int* __restrict__ slots, const float2* __restrict__ rope,
@@ -105,31 +106,35 @@ rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* _
   const int pos = DSSE_IDX(positions[t], rope_len, 0);
   const int slot = slots[t] < 0 ? -1 : DSSE_IDX(slots[t], num_slots, -1);
   const int blk = slot >= 0 ? slot / kPageTok : 0, off = slot >= 0 ? slot % kPageTok : 0;
-  // rotary part: (hq + hkv) units × 64 pairs
-  for (int idx = threadIdx.x; idx < (hq + hkv) * 64; idx += blockDim.x) {
-    const int u = idx >> 6, pr = idx & 63;  // pr = rotary pair index = dim of the first half
-    const int j = pr >> 3, rr = pr & 7;
-    const float x1 = bf2f(row[u * 128 + 16 * j + rr]);
-    const float x2 = bf2f(row[u * 128 + 16 * j + 8 + rr]);
-    const float2 cs = rope[(size_t)pos * 64 + pr];
-    const float o1 = x1 * cs.x - x2 * cs.y, o2 = x2 * cs.x + x1 * cs.y;
-    if (u < hq) {
-      bf16* qp = q_out + ((size_t)t * hq + u) * 128;
-      qp[pr] = f2bf(o1);
-      qp[64 + pr] = f2bf(o2);
-    } else if (slot >= 0) {
-      bf16* kp = k_cache + (((size_t)blk * hkv + (u - hq)) * kPageTok + off) * 128;
-      kp[pr] = f2bf(o1);
-      kp[64 + pr] = f2bf(o2);
+  const int nrot = (hq + hkv) * 8, nv = slot >= 0 ? hkv * 16 : 0;
+  for (int idx = threadIdx.x; idx < nrot + nv; idx += blockDim.x) {
+    if (idx < nrot) {
+      const int u = idx >> 3, j = idx & 7;
+      bf16* dst = u < hq ? q_out + ((size_t)t * hq + u) * 128
+                         : (slot >= 0 ? k_cache + (((size_t)blk * hkv + (u - hq)) * kPageTok + off) * 128 : nullptr);
+      if (dst == nullptr) continue;
+      const bf16x8 x1 = ld_bf16x8(row + u * 128 + 16 * j);
+      const bf16x8 x2 = ld_bf16x8(row + u * 128 + 16 * j + 8);
+      const float4* cs4 = reinterpret_cast<const float4*>(rope + (size_t)pos * 64 + 8 * j);
+      bf16x8 o1, o2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 cs = cs4[e];  // (cos, sin) of pairs 2e and 2e + 1
+        const float a0 = bf2f(x1[2 * e]), b0 = bf2f(x2[2 * e]), a1 = bf2f(x1[2 * e + 1]), b1 = bf2f(x2[2 * e + 1]);
+        o1[2 * e] = f2bf(a0 * cs.x - b0 * cs.y);
+        o2[2 * e] = f2bf(b0 * cs.x + a0 * cs.y);
+        o1[2 * e + 1] = f2bf(a1 * cs.z - b1 * cs.w);
+        o2[2 * e + 1] = f2bf(b1 * cs.z + a1 * cs.w);
+      }
+      *reinterpret_cast<bf16x8*>(dst + 8 * j) = o1;
+      *reinterpret_cast<bf16x8*>(dst + 64 + 8 * j) = o2;
+    } else {
+      const int vi = idx - nrot, h = vi >> 4, j = (vi >> 1) & 7, half = vi & 1;
+      const bf16x8 v = ld_bf16x8(row + (hq + hkv + h) * 128 + 16 * j + 8 * half);
+      bf16* vp = v_cache + (((size_t)blk * hkv + h) * 128 + (half ? 64 : 0) + 8 * j) * kPageTok + vperm_tok(off);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vp[(size_t)e * kPageTok] = v[e];
     }
-  }
-  if (slot < 0) return;
-  for (int idx = threadIdx.x; idx < hkv * 128; idx += blockDim.x) {
-    const int h = idx >> 7, c = idx & 127;
-    const int j = c >> 4, rr = c & 15;
-    const int d = rr < 8 ? 8 * j + rr : 64 + 8 * j + (rr - 8);
-    v_cache[(((size_t)blk * hkv + h) * 128 + d) * kPageTok + vperm_tok(off)] =
-        row[(hq + hkv + h) * 128 + c];
   }
 }
 
