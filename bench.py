@@ -61,7 +61,8 @@ def main():
 
     # bind this rank's GPU before the process group exists (RCCL communicators use the current device)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    # (local % count: a multi-rank rehearsal may put several ranks on one GPU, with DSSE_DIST_BACKEND=gloo)
+    device = torch.device("cuda", local % torch.cuda.device_count()) if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     rank, local, world = init_distributed(device=device if device.type == "cuda" else None)

@@ -102,11 +102,18 @@ SCfg pick_stream(int M, int N, int K) {
   c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
   if (c.nt == 2 && c.mt <= 4) c.nw = 8;  // instantiated (nt, nw): (1, 8), (2, 8), (1, 4) — gemm_stream.hip
   if (c.nt == 2 && c.mt >= 8) c.nw = 4;   // mt 8 / 16: (1, 8), (1, 4), (2, 4)
-  if (c.nw != 4) c.nw = 8;
+  // 7 waves when that puts exactly one workgroup on each CU where 8 leaves CUs idle (gate_up at TP = 1:
+  // 1792 tile groups -> 256 instead of 224 workgroups; 51.1 vs 56.0 us at M = 64, profiles/gemm_nw_r1.md)
+  const int tg1 = N / 16;
+  if (env_int("DSSE_S_NW", 0) == 0 && c.mt == 4 && c.nt == 1 && M <= 64 && c.nw == 8 && tg1 % 8 == 0 &&
+      tg1 / 8 < 256 && tg1 % 7 == 0 && tg1 / 7 <= 256)
+    c.nw = 7;
+  const bool odd_nw = c.mt == 4 && c.nt == 1 && M <= 64 && c.nw >= 2 && c.nw <= 7;  // (4, 1, 2..7, rd 1)
+  if (c.nw != 4 && !odd_nw) c.nw = 8;
   if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
   if ((N / 16) % c.nw != 0) c.nw = 4;
   c.rd = env_int("DSSE_S_RD", 1);
-  if (c.nt == 2 || c.rd != 2 || M > 64) c.rd = 1;
+  if (c.nt == 2 || c.rd != 2 || M > 64 || (c.nw != 4 && c.nw != 8)) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
   if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
   const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps

@@ -43,6 +43,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
   constexpr int ROWB = CPS * 256;                        // bytes of one X row in a slice
   constexpr int BUF = MP * ROWB;                         // bytes per slice buffer
   constexpr int PPT = (MP * CPS * 16 + 64 * NW - 1) / (64 * NW);  // 16-byte pieces per thread
+  constexpr int XG = MT * NT <= 4 ? 4 : 2;  // k-steps whose X fragments are read at once (MT * NT <= 8)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -126,15 +127,39 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
         const int slot = h * CPS + d;
         load_w(sl * CPS + d + DEPTH - 1, ring[(slot + DEPTH - 1) % DEPTH]);
         const char* xb = xb0 + (d << 8);
+        // All X fragments of a group of k-steps are read from LDS before its MFMAs (the sched_barrier
+        // keeps the compiler from sinking each ds_read next to its MFMA behind an lgkmcnt(0): that
+        // schedule paid one LDS latency per MFMA and issued the weight loads late, draining the ring).
+        if constexpr (MT * NT > 8) {  // 256 rows: VGPR-bound, the compiler's interleaved schedule is faster
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int ch = ((4 * g + s) ^ swz(r)) << 4;
+          for (int s = 0; s < 4; ++s) {
+            const int ch = ((4 * g + s) ^ swz(r)) << 4;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
+            for (int mt = 0; mt < MT; ++mt) {
+              const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
 #pragma unroll
-            for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf, ring[slot][t][s], acc[mt][t]);
+              for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf, ring[slot][t][s], acc[mt][t]);
+            }
           }
+          continue;
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < 4; s0 += XG) {
+          bf16x8 xf[XG][MT];
+#pragma unroll
+          for (int s = 0; s < XG; ++s) {
+            const int ch = ((4 * g + s0 + s) ^ swz(r)) << 4;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              xf[s][mt] = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * ROWB + ch);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 0; s < XG; ++s)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(xf[s][mt], ring[slot][t][s0 + s], acc[mt][t]);
         }
       }
       if (more) store_x((sl + 1) & 1);
@@ -194,6 +219,10 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
 #define DSSE_S_MT(MT_) \
   DSSE_S_CASE(MT_, 1, 8, 1) DSSE_S_CASE(MT_, 2, 8, 1) DSSE_S_CASE(MT_, 1, 4, 1) DSSE_S_CASE(MT_, 1, 4, 2) DSSE_S_CASE(MT_, 1, 8, 2)
   DSSE_S_MT(1) DSSE_S_MT(2) DSSE_S_MT(4)
+  // odd wave counts so that N / 16 / nw x S lands on the 256 CUs (qkv 384 tile groups: nw 3 x S 2; gate_up
+  // 1792: nw 7; 36 MB-class narrow layers: nw 6)
+  DSSE_S_CASE(4, 1, 3, 1) DSSE_S_CASE(4, 1, 5, 1) DSSE_S_CASE(4, 1, 6, 1) DSSE_S_CASE(4, 1, 7, 1)
+  DSSE_S_CASE(4, 1, 2, 1)
 #undef DSSE_S_MT
 #undef DSSE_S_CASE
   return hipErrorInvalidValue;

@@ -64,8 +64,8 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
         return rank, local, world
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # DSSE_DIST_BACKEND=gloo: several ranks sharing one GPU (RCCL rejects duplicate devices)
+        backend = os.environ.get("DSSE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     kwargs = {}
     if backend == "nccl" and device is not None:
         kwargs["device_id"] = device

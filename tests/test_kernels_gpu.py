@@ -105,6 +105,43 @@ def test_gemm_silu(gpu, tiles, M):
     _close(out, ref, 2e-2, 2e-2, "gemm_silu")
 
 
+@pytest.mark.parametrize("nw", [2, 3, 5, 6, 7])
+@pytest.mark.parametrize("M", [33, 64])
+def test_gemm_stream_odd_wave_counts(gpu, monkeypatch, nw, M):
+    """X-streaming kernel with 2..7 waves per workgroup (N / 16 a multiple of nw), plain and split-K."""
+    g = torch.Generator().manual_seed(nw * 100 + M)
+    N, K = 16 * nw * 6, 2048
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / 45, gen=g))
+    monkeypatch.setenv("DSSE_GEMM_IMPL", "2")
+    monkeypatch.setenv("DSSE_S_NW", str(nw))
+    for split in ("1", "2"):
+        monkeypatch.setenv("DSSE_S_SPLIT", split)
+        out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+        ref = torch.zeros(M, N, dtype=torch.float32)
+        ops.gemm_out(x, w, out)
+        R.gemm_out(x.cpu(), w.cpu(), ref)
+        _close(out, ref, 1e-3, 1e-2, f"gemm_out nw={nw} S={split}")
+        h = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+        hr = torch.zeros(M, N // 2, dtype=torch.bfloat16)
+        ops.gemm_silu(x, w, h)
+        R.gemm_silu(x.cpu(), w.cpu(), hr)
+        _close(h, hr, 2e-2, 2e-2, f"gemm_silu nw={nw} S={split}")
+
+
+def test_gemm_silu_full_gate_up(gpu):
+    """Mistral-7B gate_up at the bench batch (64 rows: the 7-wave, 256-workgroup configuration)."""
+    g = torch.Generator().manual_seed(7)
+    M, N, K = 64, 28672, 4096
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / 64, gen=g))
+    out = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+    ref = torch.zeros(M, N // 2, dtype=torch.bfloat16)
+    ops.gemm_silu(x, w, out)
+    R.gemm_silu(x.cpu(), w.cpu(), ref)
+    _close(out, ref, 2e-2, 2e-2, "gate_up")
+
+
 @pytest.mark.parametrize("M", [1, 9, 64, 100])
 def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     nh, nkv, H = 8, 2, 1024
