@@ -17,6 +17,8 @@
 // in LDS; grid.z splits the key range into partitions of `part` keys (flash-decoding), merged
 // by attn_combine_kernel.  Online softmax in base 2 with a finite initial max, so fully masked
 // columns stay finite and produce zeros.
+#include <cstdlib>
+
 #include "api.h"
 
 namespace dsse {
@@ -25,7 +27,7 @@ constexpr int kPage = 32;
 constexpr int kD = 128;
 
 
-template <int QW, int KWV>
+template <int QW, int KWV, bool PF = false>
 __global__ void __launch_bounds__(64 * QW * KWV)
 paged_attention_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -52,13 +54,14 @@ paged_attention_kernel(AttnParams p) {
   const int kend = min(kmax, kbeg + p.part);
   if (kbeg >= kend) return;  // uniform for the whole workgroup
 
-  // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32g + 8s + j].
+  // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32s + 8g + j] in k-step s — the same head-dim
+  // order as the K fragments, so each K load instruction reads 64 contiguous bytes of 16 key rows.
   bf16x8 qf[4];
   {
     const int qrow = p.q_start[b] + (col_valid ? qi : 0);
-    const bf16* qp = p.q + ((size_t)qrow * p.hq + h * G + (r % G)) * kD + 32 * g;
+    const bf16* qp = p.q + ((size_t)qrow * p.hq + h * G + (r % G)) * kD + 8 * g;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = col_valid ? ld_bf16x8(qp + 8 * s) : zero_bf16x8();
+    for (int s = 0; s < 4; ++s) qf[s] = col_valid ? ld_bf16x8(qp + 32 * s) : zero_bf16x8();
   }
 
   float m_run = -1e30f, l_run = 0.f;
@@ -67,21 +70,22 @@ paged_attention_kernel(AttnParams p) {
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
-  for (int kb = kbeg + 32 * kw; kb < kend; kb += 32 * KWV) {
+  // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
+  // while the current one is computed (measured slower for decode: VGPRs 100 -> 140 cost occupancy).
+  auto load_page = [&](int kb, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
     const int page = DSSE_IDX(bt[DSSE_IDX(kb / kPage, p.max_blocks, 0)], p.num_blocks, 0);
     const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
     const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
-    // K rows for keys kb + r and kb + 16 + r, 64 contiguous bytes per lane each.
-    bf16x8 k0[4], k1[4];
+    // K rows for keys kb + r and kb + 16 + r; k-step s of the 4 lane groups = 64 contiguous bytes of a row.
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * g + 8 * s);
-      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * g + 8 * s);
+      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * s + 8 * g);
+      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * s + 8 * g);
     }
-    bf16x8 vf[8];
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_bf16x8(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
-
+  };
+  auto compute_page = [&](int kb, const bf16x8 (&k0)[4], const bf16x8 (&k1)[4], const bf16x8 (&vf)[8]) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -116,6 +120,30 @@ paged_attention_kernel(AttnParams p) {
     for (int dt = 0; dt < 8; ++dt) {
       f32x4 acc = o[dt] * alpha;
       o[dt] = mfma16x16x32(vf[dt], pf, acc);
+    }
+  };
+  constexpr int kStep = 32 * KWV;
+  int kb = kbeg + 32 * kw;
+  if constexpr (!PF) {
+    for (; kb < kend; kb += kStep) {
+      bf16x8 k0[4], k1[4], vf[8];
+      load_page(kb, k0, k1, vf);
+      compute_page(kb, k0, k1, vf);
+    }
+  } else if (kb < kend) {
+    bf16x8 ka0[4], ka1[4], va[8], kc0[4], kc1[4], vc[8];
+    load_page(kb, ka0, ka1, va);
+    while (true) {
+      const bool more = kb + kStep < kend;
+      if (more) load_page(kb + kStep, kc0, kc1, vc);
+      compute_page(kb, ka0, ka1, va);
+      kb += kStep;
+      if (!more) break;
+      const bool more2 = kb + kStep < kend;
+      if (more2) load_page(kb + kStep, ka0, ka1, va);
+      compute_page(kb, kc0, kc1, vc);
+      kb += kStep;
+      if (!more2) break;
     }
   }
   // l_run is a per-lane partial over this lane's keys: sum the 4 lane groups of the column.
@@ -225,8 +253,29 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
   if (mode == 0) {
-    hipLaunchKernelGGL((paged_attention_kernel<1, 4>), dim3(num_work, p->hkv, p->nparts), dim3(256),
-                       0, st, *p);
+    // decode: DSSE_ATTN_KWV = waves per workgroup splitting the keys (4 / 8), DSSE_ATTN_PF = 0 / 1 next-page
+    // register prefetch (tools/bench_attn.py)
+    // Measured (profiles/attention_decode_r1.md): the prefetch costs 2-10 %; 4 key-split waves are best
+    // up to ~1k workgroups (64 streams x 8 kv heads: 29 us at 560 keys, 5.1 TB/s), one wave per
+    // (sequence, kv head) above (256 streams: 100 vs 109 us, 5.9 TB/s).
+    const dim3 grid(num_work, p->hkv, p->nparts);
+    const char* e1 = getenv("DSSE_ATTN_KWV");
+    const char* e2 = getenv("DSSE_ATTN_PF");
+    const int kwv = e1 ? atoi(e1) : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
+    const bool pf = e2 ? atoi(e2) != 0 : false;
+    if (kwv == 8) {
+      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 8, true>), grid, dim3(512), 0, st, *p);
+      else hipLaunchKernelGGL((paged_attention_kernel<1, 8, false>), grid, dim3(512), 0, st, *p);
+    } else if (kwv == 1) {
+      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 1, true>), grid, dim3(64), 0, st, *p);
+      else hipLaunchKernelGGL((paged_attention_kernel<1, 1, false>), grid, dim3(64), 0, st, *p);
+    } else if (kwv == 2) {
+      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 2, true>), grid, dim3(128), 0, st, *p);
+      else hipLaunchKernelGGL((paged_attention_kernel<1, 2, false>), grid, dim3(128), 0, st, *p);
+    } else {
+      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 4, true>), grid, dim3(256), 0, st, *p);
+      else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false>), grid, dim3(256), 0, st, *p);
+    }
     if (p->nparts > 1)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else {
