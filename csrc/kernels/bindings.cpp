@@ -135,6 +135,36 @@ SCfg pick_stream(int M, int N, int K) {
   return c;
 }
 
+// Wide-batch kernel configuration (gemm_wide.hip, 32x32x16 MFMAs, 128 columns per workgroup).  Env
+// overrides: DSSE_W_SPLIT, DSSE_W_RD.
+struct WCfg {
+  int mb, rd, S;
+  bool ok;
+};
+WCfg pick_wide(int M, int N, int K) {
+  WCfg c{};
+  c.mb = M <= 128 ? 4 : 8;
+  const int cps = c.mb == 8 ? 1 : 2;
+  c.rd = env_int("DSSE_W_RD", c.mb == 8 ? 2 : 1);
+  if (c.mb == 8 && c.rd != 3) c.rd = 2;
+  if (c.mb == 4 && c.rd != 2) c.rd = 1;
+  c.ok = M <= 256 && N % 128 == 0 && K % (128 * cps) == 0;
+  if (!c.ok) return c;
+  const int wgs = N / 128, slices = K / (128 * cps);
+  int S = env_int("DSSE_W_SPLIT", 0);
+  if (S <= 0 || slices % S != 0) {
+    S = 1;
+    for (int d = 1; d <= slices; ++d) {
+      if (slices % d) continue;
+      if (wgs * d > 320) break;
+      S = d;
+      if (wgs * d >= 192) break;
+    }
+  }
+  c.S = S;
+  return c;
+}
+
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
@@ -142,8 +172,14 @@ constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group u
 // DSSE_GEMM_IMPL forces one.
 int gemm_impl(int M, int N, int K) {
   const int impl = env_int("DSSE_GEMM_IMPL", -1);
-  if (M > 64) return 2;  // only the X-streaming kernel has a row-block mode
+  if (M > 64) {  // 3 = gemm_wide (32x32 MFMAs, M <= 256) above DSSE_WIDE_MIN_M rows, else gemm_stream
+    const bool wide_ok = pick_wide(M, N, K).ok;
+    if (impl == 3 && wide_ok) return 3;
+    if (impl == 2) return 2;
+    return (wide_ok && M > env_int("DSSE_WIDE_MIN_M", 64)) ? 3 : 2;
+  }
   if (impl >= 0) {
+    if (impl == 3 && !pick_wide(M, N, K).ok) return pick_stream(M, N, K).ok ? 2 : 1;
     if (impl == 2 && !pick_stream(M, N, K).ok) return 1;
     return impl;
   }
@@ -164,7 +200,15 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
   const int impl = gemm_impl(M, N, K);
-  TORCH_CHECK(M <= 64 || impl == 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
+  TORCH_CHECK(M <= 64 || impl >= 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
+  if (impl == 3) {
+    const WCfg c = pick_wide(M, N, K);
+    at::Tensor part;
+    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
+    DSSE_CHECK_HIP(dsse_gemm_wide(mode, c.mb, c.rd, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                  c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    return;
+  }
   if (impl == 2) {
     const SCfg c = pick_stream(M, N, K);
     at::Tensor part;
@@ -225,7 +269,17 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   const bool shape_ok = M >= 1 && M <= kMaxDecodeM && K % 128 == 0 && N % 16 == 0 && w.size(1) == K &&
                         (M <= 64 || pick_stream(M, N, K).ok);
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
-  if (impl == 2) {
+  if (impl == 3) {
+    const WCfg c = pick_wide(M, N, K);
+    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      dsse::GemmEpi ep{};
+      DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kResidAdd, c.mb, c.rd, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                    part.data_ptr<float>(), cur_stream()));
+      return c.S;
+    }
+  } else if (impl == 2) {
     const SCfg c = pick_stream(M, N, K);
     if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
       check_dtype(x, at::kBFloat16, "x");

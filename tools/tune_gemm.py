@@ -91,7 +91,7 @@ def main():
                 for k in [k for k in os.environ if k.startswith(("DSSE_X_", "DSSE_S_", "DSSE_GEMM_"))]:
                     os.environ.pop(k, None)
                 impl, _, kv = cfg.partition(":")
-                os.environ["DSSE_GEMM_IMPL"] = {"skinny": "0", "x": "1", "s": "2"}[impl]
+                os.environ["DSSE_GEMM_IMPL"] = {"skinny": "0", "x": "1", "s": "2", "w": "3"}[impl]
                 for item in filter(None, kv.split(",")):
                     k, v = item.split("=")
                     os.environ[k] = v
