@@ -384,3 +384,44 @@ def test_checked_build_catches_bad_indices(gpu):
                        text=True, timeout=600, env={**os.environ, "DSSE_KERNELS_VARIANT": "checked"})
     assert r.returncode == 0 and "CHECKS-OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
+
+
+def _mistral_shards(tp):
+    """(name, N, K) of every Mistral-7B decode projection as one TP rank holds it (Megatron split)."""
+    H, F, V, nh, nkv = 4096, 14336, 32768, 32 // tp, 8 // tp
+    return [("qkv", (nh + 2 * nkv) * 128, H), ("o", H, nh * 128), ("gate_up", 2 * F // tp, H),
+            ("down", H, F // tp), ("lm_head", V // tp, H)]
+
+
+@pytest.mark.parametrize("tp", [1, 2, 4, 8])
+@pytest.mark.parametrize("M", [1, 16, 64, 128, 192])
+def test_decode_gemms_at_tp_shard_shapes(gpu, tp, M):
+    """Every rank-local projection shape of TP = 1/2/4/8 at the decode bucket sizes, through the kernel the
+    engine picks for it (skinny / X-streaming / wide, split-K or not), against an fp32 reference on the GPU.
+    The 8-GPU TP path cannot run on a one-GPU box; this pins its kernels' shapes."""
+    g = torch.Generator().manual_seed(tp * 1000 + M)
+    for name, N, K in _mistral_shards(tp):
+        x = _rand(M, K, dev=gpu, gen=g)
+        w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
+        if name == "gate_up":
+            out = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+            ref = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+            ops.gemm_silu(x, w, out)
+            R.gemm_silu(x, w, ref)
+            _close(out, ref, 2e-2, 2e-2, f"{name} tp={tp} M={M}")
+        elif name in ("o", "down"):
+            r0 = torch.randn(M, N, generator=g).to(gpu)
+            r = r0.clone()
+            part = torch.zeros(32 * M * N, device=gpu)
+            y = torch.zeros(M, N, device=gpu, dtype=torch.bfloat16)
+            nw = torch.ones(N, device=gpu, dtype=torch.bfloat16)
+            ns = ops.gemm_resid_split(x, w, r, part)
+            ops.rmsnorm(r, nw, y, 1e-5, part=part, nsplit=ns)
+            R.gemm_resid(x, w, r0)
+            _close(r, r0, 1e-3, 1e-3, f"{name} tp={tp} M={M}")
+        else:
+            out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+            ref = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+            ops.gemm_out(x, w, out)
+            R.gemm_out(x, w, ref)
+            _close(out, ref, 1e-3, 1e-2, f"{name} tp={tp} M={M}")
