@@ -25,13 +25,28 @@ class TPComm:
     size: int = 1
     group: object = None
 
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        # gloo with GPU tensors (several TP ranks sharing one GPU in a rehearsal, DSSE_DIST_BACKEND=gloo):
+        # run the collective on a host copy; never taken on the RCCL path
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def all_reduce(self, t: torch.Tensor) -> None:
         if self.size > 1:
-            dist.all_reduce(t, group=self.group)
+            if self._host_staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, group=self.group)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         """out: [size * numel(inp)] contiguous."""
         if self.size > 1:
+            if self._host_staged(out):
+                h = torch.empty(out.numel(), dtype=out.dtype)
+                dist.all_gather_into_tensor(h, inp.contiguous().view(-1).cpu(), group=self.group)
+                out.view(-1).copy_(h)
+                return
             # flat views: RCCL accepts stacked outputs, gloo only the dim-0 concatenation
             dist.all_gather_into_tensor(out.view(-1), inp.contiguous().view(-1), group=self.group)
         else:
