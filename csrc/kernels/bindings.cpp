@@ -116,19 +116,24 @@ SCfg pick_stream(int M, int N, int K) {
   if (c.nt == 2 || c.rd != 2 || M > 64 || (c.nw != 4 && c.nw != 8)) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
   if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
-  const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
+  // half-width X slices (64 KiB of LDS: two workgroups per CU) for 33-64 rows, flagged as rd = 16 + 2
+  const bool half = c.mt == 4 && c.nt == 1 && M <= 64 && (c.nw == 4 || c.nw == 8 || c.nw == 2) &&
+                    env_int("DSSE_S_HALF", 0) == 1;
+  if (half) c.rd = 18;
+  const int cps = c.mt <= 4 ? (half ? 2 : 4) : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
   c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
   const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
+  const int per_cu = half ? 2 : 1;
   int S = env_int("DSSE_S_SPLIT", 0);
   if (S <= 0 || slices % S != 0) {
-    // smallest split that gives ~one workgroup per CU (256 CUs), never more than 320 workgroups
+    // smallest split that gives ~one workgroup per CU slot (256 CUs x per_cu), never more than 1.25x that
     S = 1;
     for (int d = 1; d <= slices; ++d) {
       if (slices % d) continue;
-      if (wgs * d > 320) break;
+      if (wgs * d > 320 * per_cu) break;
       S = d;
-      if (wgs * d >= 192) break;
+      if (wgs * d >= 192 * per_cu) break;
     }
   }
   c.S = S;

@@ -20,6 +20,10 @@
 // stored (MFMA output rows depend only on the same A row).
 #include "gemm_epilogue.h"
 
+#ifndef DSSE_X_TOUCH
+#define DSSE_X_TOUCH 1  // L2 warm-up loads of the next X slice (see the kernel)
+#endif
+
 #ifndef DSSE_W_DEFAULT
 #define DSSE_W_DEFAULT 0  // experiment build "wdef": default cache policy on the weight stream
 #endif
@@ -34,11 +38,12 @@ constexpr int stream_cps(int mt) { return mt <= 4 ? 4 : (mt <= 8 ? 2 : 1); }
 // blocks of 64) and workgroups are renumbered so that the MB row blocks of one tile group are consecutive
 // on the same XCD: they stream the same weight bytes at about the same time, so HBM serves them once and
 // the XCD's L2 the other MB-1 times.  That sharing needs temporal (cached) weight loads (SHARED_W).
-template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false, bool HALF = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
                    int Kr, GemmEpi ep, float* __restrict__ part) {
-  constexpr int CPS = stream_cps(MT);
+  // HALF: X slices of half the columns (64 KiB of LDS for 64 rows): two workgroups fit on a CU
+  constexpr int CPS = HALF ? stream_cps(MT) / 2 : stream_cps(MT);
   constexpr int MP = 16 * MT;
   constexpr int ROWB = CPS * 256;                        // bytes of one X row in a slice
   constexpr int BUF = MP * ROWB;                         // bytes per slice buffer
@@ -99,11 +104,33 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     }
   };
 
+  // L2 warm-up of the NEXT X slice: X is usually written by the kernel just before (RMSNorm / SiLU) on other
+  // XCDs, so every XCD's L2 misses on it; one dword per 128-B line, touched a slice ahead, turns the real
+  // (register-staged) X loads into L2 hits.  The touched words are folded into `touch`, consumed by a store
+  // that never executes (M >= 0), so the loads stay.
+  // Only for the wide-N launches (7-8 waves, no split-K: gate_up, LM head): the split-K narrow projections,
+  // with 2-7 slices per workgroup, measured slower with it (+140 us per 64-stream step).
+  constexpr bool TOUCH = DSSE_X_TOUCH && NW >= 7;
+  constexpr int LPR = CPS * 2;                 // 128-B lines per X row of a slice
+  constexpr int TOUCH_PT = (MP * LPR + 64 * NW - 1) / (64 * NW);
+  const int touch_last_row = min(M - m0, MP) - 1;
+  uint32_t touch = 0;
+  auto touch_x = [&](int sl) {
+    const char* src = reinterpret_cast<const char*>(X + k0 + sl * (CPS * 128));
+#pragma unroll
+    for (int i = 0; i < TOUCH_PT; ++i) {
+      const int li = min(threadIdx.x + i * 64 * NW, MP * LPR - 1);
+      touch ^= *reinterpret_cast<const uint32_t*>(src + (size_t)min(li / LPR, touch_last_row) * ldx * 2 +
+                                                  (li % LPR) * 128);
+    }
+  };
+
   constexpr int DEPTH = CPS * RD;  // weight ring: RD slices of chunks in flight
   bf16x8 ring[DEPTH][NT][4];
 #pragma unroll
   for (int d = 0; d < DEPTH - 1; ++d) load_w(d, ring[d]);
   load_x(0);
+  if (TOUCH) touch_x(min(1, nsl - 1));
   store_x(0);
 
   f32x4 acc[MT][NT];
@@ -120,6 +147,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       if (h > 0 && sl >= nsl) break;
       __syncthreads();  // slice sl visible; everyone is done reading slice sl - 1's buffer
       const bool more = sl + 1 < nsl;
+      if (TOUCH) touch_x(min(sl + 2, nsl - 1));
       if (more) load_x(sl + 1);
       const char* xb0 = smem + (sl & 1) * BUF;
 #pragma unroll
@@ -166,6 +194,8 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     }
   }
 
+  if (TOUCH && M < 0) part[touch & 1] = (float)touch;  // never runs: keeps the warm-up loads
+
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -179,27 +209,33 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       }
 }
 
-template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false, bool HALF = false>
 static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
   const int TG = N / (16 * NT);
   const int MB = SHARED_W ? (M + 16 * MT - 1) / (16 * MT) : 1;
-  const size_t lds = (size_t)2 * 16 * MT * stream_cps(MT) * 256;
+  const size_t lds = (size_t)2 * 16 * MT * (HALF ? stream_cps(MT) / 2 : stream_cps(MT)) * 256;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W, HALF>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   dim3 grid(TG / NW * MB, S), block(64 * NW);
-  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>), grid, block, lds, st, X, ldx, M, W, K, N,
-                     K / S, ep, part);
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W, HALF>), grid, block, lds, st, X, ldx, M, W, K,
+                     N, K / S, ep, part);
   return hipGetLastError();
 }
 
 template <int MODE>
 static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
                                 int S, const GemmEpi& ep, float* part, hipStream_t st) {
+  if (rd >= 16) {  // rd = 16 + ring slices: HALF-width X slices (two workgroups per CU), mt 4 only
+    if (mt == 4 && nt == 1 && nw == 4 && rd == 18) return launch_s<4, 1, 4, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
+    if (mt == 4 && nt == 1 && nw == 8 && rd == 18) return launch_s<4, 1, 8, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
+    if (mt == 4 && nt == 1 && nw == 2 && rd == 18) return launch_s<4, 1, 2, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
+    return hipErrorInvalidValue;
+  }
   if (M > 16 * mt) {  // row blocks with L2-shared weights (64-row MFMA tiles, one or eight waves)
     if (mt == 4 && nt == 1 && nw == 4) return launch_s<4, 1, 4, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
     if (mt == 4 && nt == 1 && nw == 8) return launch_s<4, 1, 8, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
