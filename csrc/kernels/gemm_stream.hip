@@ -24,6 +24,10 @@
 #define DSSE_X_TOUCH 1  // L2 warm-up loads of the next X slice (see the kernel)
 #endif
 
+#ifndef DSSE_XCD_SPLITK
+#define DSSE_XCD_SPLITK 1  // XCD-grouped split-K workgroup mapping (see the kernel)
+#endif
+
 #ifndef DSSE_W_DEFAULT
 #define DSSE_W_DEFAULT 0  // experiment build "wdef": default cache policy on the weight stream
 #endif
@@ -63,9 +67,16 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     rb = id % MB;
     X += (size_t)rb * MP * ldx;
   }
+  int ks = blockIdx.y;
+  if (!SHARED_W && DSSE_XCD_SPLITK && gridDim.y > 1 && 8 % gridDim.y == 0 && (gridDim.x * gridDim.y) % 8 == 0) {
+    // Split-K: keep each K range on 8/S XCDs (dispatch deals workgroup i, x-fastest, to XCD i % 8), so an
+    // XCD's L2 fetches only its K range of X (1/S of it) instead of all of X.  Bijective, speed only.
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x, xcd = lin % 8, slot = lin / 8, per = 8 / gridDim.y;
+    ks = xcd / per;
+    wg = slot * per + xcd % per;
+  }
   const int m0 = rb * MP;     // first row of this workgroup's row block
   const int tgi = wg * NW + w;  // host guarantees N / (16 NT) % NW == 0: every wave is busy
-  const int ks = blockIdx.y;
   const int k0 = ks * Kr;
   const int nch = Kr >> 7;   // multiple of CPS (host-checked)
   const int nsl = nch / CPS;

@@ -46,8 +46,14 @@ gemm_wide_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n32 = lane & 31, h = lane >> 5;
-  const int strip = blockIdx.x * NW + w;  // host guarantees N % (32 NW) == 0
-  const int ks = blockIdx.y;
+  int cg = blockIdx.x, ks = blockIdx.y;
+  if (gridDim.y > 1 && 8 % gridDim.y == 0 && (gridDim.x * gridDim.y) % 8 == 0) {
+    // split-K: each K range on 8/S XCDs (as gemm_stream.hip), so an XCD's L2 fetches only its range of X
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x, xcd = lin % 8, slot = lin / 8, per = 8 / gridDim.y;
+    ks = xcd / per;
+    cg = slot * per + xcd % per;
+  }
+  const int strip = cg * NW + w;  // host guarantees N % (32 NW) == 0
   const int k0 = ks * Kr;
   const int nch = Kr >> 7;  // multiple of CPS (host-checked)
   const int nsl = nch / CPS;

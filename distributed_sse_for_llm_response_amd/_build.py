@@ -71,6 +71,7 @@ def _parallel(jobs, verbose):
 KERNEL_VARIANTS = {
     "nt": ["-DDSSE_W_NT=1"],           # experiment build (non-temporal weight loads everywhere)
     "checked": ["-DDSSE_KERNEL_CHECKS=1"],
+    "noxcd": ["-DDSSE_XCD_SPLITK=0"],  # experiment build (split-K workgroups in plain dispatch order)
     "wdef": ["-DDSSE_W_DEFAULT=1"],     # experiment build (default cache policy on gemm_stream weights)  # debug build: device-side index checks (common.h DSSE_IDX)
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
