@@ -34,7 +34,13 @@ def load(sanitizer: str | None = None):
 
 
 def server_binary() -> Path:
-    return _LIB_DIR / "dsse-server"
+    """The standalone server (csrc/runtime/server_main.cpp), built on demand."""
+    p = _LIB_DIR / "dsse-server"
+    if not p.exists() and os.environ.get("DSSE_AUTOBUILD", "1") == "1":
+        from .._build import build_runtime
+
+        build_runtime()
+    return p
 
 
 def loadgen_binary() -> Path:
