@@ -131,19 +131,20 @@ paged_attention_kernel(AttnParams p) {
       compute_page(kb, k0, k1, vf);
     }
   } else if (kb < kend) {
+    // The next-page loads are unconditional (the last page is re-read once at the end): a branch around
+    // them made hipcc wait vmcnt(0) at the join, which serialised the prefetch away.
     bf16x8 ka0[4], ka1[4], va[8], kc0[4], kc1[4], vc[8];
+    const int n = (kend - kb + kStep - 1) / kStep;  // pages of this wave
+    const int kb_last = kb + (n - 1) * kStep;
     load_page(kb, ka0, ka1, va);
-    while (true) {
-      const bool more = kb + kStep < kend;
-      if (more) load_page(kb + kStep, kc0, kc1, vc);
+    for (int i = 0; i < n; i += 2) {
+      load_page(min(kb + kStep, kb_last), kc0, kc1, vc);
       compute_page(kb, ka0, ka1, va);
       kb += kStep;
-      if (!more) break;
-      const bool more2 = kb + kStep < kend;
-      if (more2) load_page(kb + kStep, ka0, ka1, va);
+      if (i + 1 >= n) break;
+      load_page(min(kb + kStep, kb_last), ka0, ka1, va);
       compute_page(kb, kc0, kc1, vc);
       kb += kStep;
-      if (!more2) break;
     }
   }
   // l_run is a per-lane partial over this lane's keys: sum the 4 lane groups of the column.
