@@ -30,6 +30,7 @@ std::string encode_request(const ChatRequest& r) {
   w.i64(r.seed);
   w.u8(r.ignore_eos ? 1 : 0);
   w.u8(r.from_edge ? 1 : 0);
+  w.str(r.messages_json);
   return w.data();
 }
 
@@ -45,6 +46,7 @@ bool decode_request(Reader& rd, ChatRequest* r) {
   r->seed = rd.i64();
   r->ignore_eos = rd.u8() != 0;
   r->from_edge = rd.u8() != 0;
+  r->messages_json = rd.str();
   return rd.good();
 }
 }  // namespace dpwire

@@ -222,6 +222,7 @@ struct Parser {
     if (p >= t.size()) return false;
     bool ok = true;
     char c = t[p];
+    const size_t s0 = p;
     if (c == '"') { v.kind = JsonValue::kString; ok = string(v.str); }
     else if (c == '{') { v.kind = JsonValue::kObject; std::map<std::string, JsonValue> skip; ok = object(skip); }
     else if (c == '[') { v.kind = JsonValue::kArray; ok = array(); }
@@ -229,6 +230,7 @@ struct Parser {
     else if (c == 'f') { v.kind = JsonValue::kBool; v.b = false; ok = lit("false"); }
     else if (c == 'n') { v.kind = JsonValue::kNull; ok = lit("null"); }
     else ok = number(v);
+    if (ok && (c == '{' || c == '[')) v.raw = std::string(t.substr(s0, p - s0));
     --depth;
     return ok;
   }
@@ -272,6 +274,26 @@ struct Parser {
 };
 
 }  // namespace
+
+bool parse_json_array_of_objects(std::string_view text, std::vector<std::map<std::string, JsonValue>>& out) {
+  Parser ps{text};
+  ps.ws();
+  if (ps.p >= text.size() || text[ps.p] != '[') return false;
+  ++ps.p;
+  ps.ws();
+  if (ps.p < text.size() && text[ps.p] == ']') return true;
+  while (true) {
+    ps.ws();
+    std::map<std::string, JsonValue> o;
+    if (!ps.object(o)) return false;
+    out.push_back(std::move(o));
+    ps.ws();
+    if (ps.p >= text.size()) return false;
+    if (text[ps.p] == ',') { ++ps.p; continue; }
+    if (text[ps.p] == ']') return true;
+    return false;
+  }
+}
 
 bool parse_json_object(std::string_view text, std::map<std::string, JsonValue>& out, size_t* consumed) {
   Parser ps{text};

@@ -11,6 +11,7 @@
 #include <optional>
 #include <string>
 #include <string_view>
+#include <vector>
 
 namespace dsse {
 
@@ -38,12 +39,17 @@ struct JsonValue {
   int64_t i64 = 0;
   bool is_int = false;
   std::string str;
+  std::string raw;  // exact JSON text of an object / array value
 };
 
 // Parse the first JSON value of `text` as an object of scalar fields.  Keys are stored lower-cased
 // (encoding/json matches struct fields case-insensitively).  Returns false on malformed JSON or when
 // the top-level value is not an object.
 bool parse_json_object(std::string_view text, std::map<std::string, JsonValue>& out, size_t* consumed = nullptr);
+
+// Parse a JSON array whose elements are all objects (e.g. OpenAI chat `messages`).  Returns false on
+// malformed JSON or a non-object element.
+bool parse_json_array_of_objects(std::string_view text, std::vector<std::map<std::string, JsonValue>>& out);
 
 // Parse a TokenMessage (as published by the proxy / load generator).  Missing fields keep defaults.
 bool parse_token_message(std::string_view text, TokenMessage& m);

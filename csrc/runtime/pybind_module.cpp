@@ -37,6 +37,7 @@ py::dict request_dict(const ChatRequest& r) {
   d["seed"] = r.seed;
   d["ignore_eos"] = r.ignore_eos;
   d["from_edge"] = r.from_edge;
+  d["messages"] = r.messages_json;
   return d;
 }
 

@@ -290,6 +290,12 @@ struct Conn {
   int64_t after_seq = -1;
   SinkPtr sink;
   std::deque<std::pair<int64_t, FramePtr>> held;  // hybrid inspection delay queue (release time, frame)
+  // OpenAI chat completions (vLLM-compatible): frames are re-encoded as chat.completion chunks
+  bool openai = false;
+  bool oa_stream = true;
+  std::string oa_model, oa_text;
+  int64_t oa_created = 0;
+  int oa_count = 0, oa_max_tokens = -1;
   // RESP
   bool resp_pubsub = false;
   std::vector<std::string> resp_channels, resp_patterns;
@@ -367,6 +373,9 @@ class IoThread {
   void write_raw(Conn& c, const std::string& data);
   void write_sse_bytes(Conn& c, const std::string& data);
   void deliver_token(Conn& c, const FramePtr& f);
+  void handle_openai(Conn& c, HttpRequest& req);
+  void deliver_openai(Conn& c, const FramePtr& f);
+  void finish_openai(Conn& c, const char* finish_reason);
   void flush_out(Conn& c);
   void close_conn(Conn& c);
   void drain_outbox();
@@ -559,6 +568,7 @@ void IoThread::end_sse(Conn& c, bool write_terminator) {
     c.sink.reset();
   }
   c.held.clear();
+  c.openai = false;
   metrics().sse_active_connections.add(-1);
   metrics().sse_connection_duration_seconds.observe((mono_ns() - c.sse_start_mono) / 1e9);
   if (write_terminator) {
@@ -572,6 +582,10 @@ void IoThread::deliver_token(Conn& c, const FramePtr& f) {
   if (!c.sse) return;
   // Last-Event-ID filter (strictly greater: fixes the reference's off-by-one)
   if (c.after_seq >= 0 && f->seq <= c.after_seq && !f->done) return;
+  if (c.openai) {
+    deliver_openai(c, f);
+    return;
+  }
   const InspectionMode mode = srv_.config().inspection;
   if (mode == InspectionMode::kHybrid) {
     c.held.emplace_back(mono_ns() + (int64_t)srv_.config().inspection_buffer_ms * 1000000LL, f);
@@ -611,6 +625,187 @@ void IoThread::deliver_token(Conn& c, const FramePtr& f) {
     return;
   }
   flush_out(c);
+}
+
+// ---- OpenAI-compatible chat completions (the vLLM surface the reference proxy consumes) ----------------
+// POST /v1/chat/completions {"model","messages":[{"role","content"}..],"stream",...} -> either an SSE stream of
+// chat.completion.chunk objects ending with `data: [DONE]` (stream: true; the exact lines the reference's
+// llm-stream-proxy parses, src/llm-stream-proxy/main.go:34-52,192-227) or one chat.completion object.  The
+// request goes to the same engine queue as POST /chat; the engine's TokenMessages for the conversation are
+// re-encoded per connection.  GET /v1/models lists the served model.
+namespace {
+std::string openai_error(int code, const std::string& msg, const char* type) {
+  return "{\"object\":\"error\",\"message\":" + json_quote(msg) + ",\"type\":\"" + type + "\",\"param\":null,\"code\":" +
+         std::to_string(code) + "}";
+}
+}  // namespace
+
+void IoThread::handle_openai(Conn& c, HttpRequest& req) {
+  const bool ka = req.keep_alive;
+  const std::string& model = srv_.config().model_name;
+  if (req.path == "/v1/models") {
+    const std::string body = "{\"object\":\"list\",\"data\":[{\"id\":" + json_quote(model) +
+                             ",\"object\":\"model\",\"created\":" + std::to_string((long long)time(nullptr)) +
+                             ",\"owned_by\":\"dsse\",\"root\":" + json_quote(model) + ",\"parent\":null}]}";
+    write_raw(c, simple_response(200, body, "application/json", ka));
+    return;
+  }
+  auto bad = [&](int code, const std::string& m) {
+    write_raw(c, simple_response(code, openai_error(code, m, code == 404 ? "NotFoundError" : "BadRequestError"),
+                                 "application/json", ka));
+  };
+  if (req.method != "POST") {
+    write_raw(c, http_error(405, "Method not allowed", ka));
+    return;
+  }
+  if (!srv_.local_engine()) {
+    write_raw(c, simple_response(503, openai_error(503, "no engine attached", "ServiceUnavailableError"),
+                                 "application/json", ka));
+    return;
+  }
+  std::map<std::string, JsonValue> o;
+  if (!parse_json_object(req.body, o)) return bad(400, "Invalid JSON body");
+  auto mi = o.find("messages");
+  std::vector<std::map<std::string, JsonValue>> msgs;
+  if (mi == o.end() || mi->second.kind != JsonValue::kArray || !parse_json_array_of_objects(mi->second.raw, msgs) ||
+      msgs.empty())
+    return bad(400, "messages must be a non-empty array of {role, content} objects");
+  std::string norm = "[", last_user;
+  for (size_t i = 0; i < msgs.size(); ++i) {
+    auto& m = msgs[i];
+    auto r = m.find("role");
+    auto ct = m.find("content");
+    if (r == m.end() || r->second.kind != JsonValue::kString) return bad(400, "every message needs a string role");
+    std::string text;
+    if (ct != m.end() && ct->second.kind == JsonValue::kString) {
+      text = ct->second.str;
+    } else if (ct != m.end() && ct->second.kind == JsonValue::kArray) {  // [{"type":"text","text":..}]
+      std::vector<std::map<std::string, JsonValue>> parts;
+      if (!parse_json_array_of_objects(ct->second.raw, parts)) return bad(400, "invalid content parts");
+      for (auto& pt : parts) {
+        auto tx = pt.find("text");
+        if (tx != pt.end() && tx->second.kind == JsonValue::kString) text += tx->second.str;
+      }
+    } else if (!(ct != m.end() && ct->second.kind == JsonValue::kNull)) {
+      return bad(400, "every message needs string content");
+    }
+    if (r->second.str == "user") last_user = text;
+    norm += (i ? ",{\"role\":" : "{\"role\":") + json_quote(r->second.str) + ",\"content\":" + json_quote(text) + "}";
+  }
+  norm += "]";
+  auto num = [&](const char* k, double dflt) {
+    auto it2 = o.find(k);
+    return (it2 != o.end() && it2->second.kind == JsonValue::kNumber) ? it2->second.num : dflt;
+  };
+  if (num("n", 1) != 1) return bad(400, "only n = 1 is supported");
+  auto st = o.find("stream");
+  const bool stream = st != o.end() && st->second.kind == JsonValue::kBool && st->second.b;
+  std::string id = uuid4();
+  id.erase(std::remove(id.begin(), id.end(), '-'), id.end());
+  const std::string conv = "chatcmpl-" + id;
+  ChatRequest r;
+  r.conversation_id = conv;
+  r.message = last_user;
+  r.messages_json = norm;
+  r.max_tokens = (int)num("max_tokens", num("max_completion_tokens", -1));
+  r.temperature = num("temperature", -1);
+  r.top_p = num("top_p", -1);
+  r.top_k = (int)num("top_k", -1);
+  r.seed = (int64_t)num("seed", -1);
+  {
+    auto ie = o.find("ignore_eos");
+    r.ignore_eos = ie != o.end() && ie->second.kind == JsonValue::kBool && ie->second.b;
+  }
+  r.from_edge = true;
+  auto mo = o.find("model");
+  c.openai = true;
+  c.oa_stream = stream;
+  c.oa_model = (mo != o.end() && mo->second.kind == JsonValue::kString && !mo->second.str.empty()) ? mo->second.str : model;
+  c.oa_created = (int64_t)time(nullptr);
+  c.oa_count = 0;
+  c.oa_max_tokens = r.max_tokens;
+  c.oa_text.clear();
+  // subscribe before submitting, as POST /chat does
+  auto sink = std::make_shared<ConnSink>();
+  sink->io = this;
+  sink->conn = c.id;
+  sink->pending = pending_[c.id].get();
+  sink->cap = srv_.config().max_pending_bytes;
+  c.sink = sink;
+  srv_.bus().subscribe(conv, sink, -1, nullptr);
+  srv_.flow_update(conv, 0);
+  if (stream) {
+    const std::string first = "data: {\"id\":" + json_quote(conv) + ",\"object\":\"chat.completion.chunk\",\"created\":" +
+                              std::to_string(c.oa_created) + ",\"model\":" + json_quote(c.oa_model) +
+                              ",\"choices\":[{\"index\":0,\"delta\":{\"role\":\"assistant\",\"content\":\"\"},"
+                              "\"logprobs\":null,\"finish_reason\":null}]}\n\n";
+    start_sse(c, conv, true, -1, first, nullptr);
+  } else {  // buffered: no HTTP response until the completion is done
+    c.sse = true;
+    c.chat_mode = true;
+    c.got_first = false;
+    c.conv_id = conv;
+    c.after_seq = -1;
+    c.sse_start_mono = c.last_write_mono = mono_ns();
+    c.first_deadline_mono = c.sse_start_mono + (int64_t)srv_.config().first_token_timeout_ms * 1000000LL;
+    metrics().sse_active_connections.add(1);
+    metrics().sse_total_connections.inc();
+  }
+  srv_.submit_chat(std::move(r));
+}
+
+void IoThread::deliver_openai(Conn& c, const FramePtr& f) {
+  TokenMessage m;
+  if (!parse_token_message(f->json, m)) return;
+  if (f->done) {
+    if (m.token == "[ERROR]") return finish_openai(c, "abort");
+    // the engine ends a completion at EOS or at max_tokens; the count tells which (vLLM's finish_reason)
+    return finish_openai(c, c.oa_max_tokens > 0 && c.oa_count >= c.oa_max_tokens ? "length" : "stop");
+  }
+  c.got_first = true;
+  ++c.oa_count;
+  metrics().sse_messages_delivered_total.inc();
+  if (!c.oa_stream) {
+    c.oa_text += m.token;
+    return;
+  }
+  const size_t pend = c.out.size() - c.out_off;
+  if (pend > srv_.config().max_pending_bytes) {
+    metrics().bus_dropped_tokens_total.inc();
+    return;
+  }
+  std::string ev = "data: {\"id\":";
+  json_append_string(ev, c.conv_id);
+  ev += ",\"object\":\"chat.completion.chunk\",\"created\":" + std::to_string(c.oa_created) + ",\"model\":";
+  json_append_string(ev, c.oa_model);
+  ev += ",\"choices\":[{\"index\":0,\"delta\":{\"content\":";
+  json_append_string(ev, m.token);
+  ev += "},\"logprobs\":null,\"finish_reason\":null}]}\n\n";
+  write_sse_bytes(c, ev);
+}
+
+void IoThread::finish_openai(Conn& c, const char* finish_reason) {
+  if (!c.sse) return;
+  const std::string head = "{\"id\":" + json_quote(c.conv_id) + ",\"object\":\"chat.completion" +
+                           std::string(c.oa_stream ? ".chunk" : "") + "\",\"created\":" + std::to_string(c.oa_created) +
+                           ",\"model\":" + json_quote(c.oa_model) + ",\"choices\":[{\"index\":0,";
+  const std::string usage = "\"usage\":{\"prompt_tokens\":0,\"total_tokens\":" + std::to_string(c.oa_count) +
+                            ",\"completion_tokens\":" + std::to_string(c.oa_count) + "}";
+  if (c.oa_stream) {
+    std::string ev = "data: " + head + "\"delta\":{},\"logprobs\":null,\"finish_reason\":\"" + finish_reason +
+                     "\",\"stop_reason\":null}]}\n\ndata: [DONE]\n\n";
+    append_chunk(c.out, ev.data(), ev.size());
+    end_sse(c, true);
+    return;
+  }
+  const bool ka = c.keep_alive;
+  std::string body = head + "\"message\":{\"role\":\"assistant\",\"content\":" + json_quote(c.oa_text) +
+                     ",\"tool_calls\":[]},\"logprobs\":null,\"finish_reason\":\"" + finish_reason +
+                     "\",\"stop_reason\":null}]," + usage + "}";
+  // buffered mode never wrote headers: close the pseudo-SSE session, then send one JSON response
+  end_sse(c, false);
+  c.oa_text.clear();
+  write_raw(c, simple_response(200, body, "application/json", ka));
 }
 
 void IoThread::drain_outbox() {
@@ -686,6 +881,12 @@ void IoThread::timers() {
       else flush_out(c);
     }
     if (!c.sse) continue;
+    if (c.openai) {
+      if (!c.got_first && now >= c.first_deadline_mono) finish_openai(c, "abort");
+      else if (c.oa_stream && now - c.last_write_mono >= ka) write_sse_bytes(c, ": keep-alive\n\n");
+      if (c.close_after_write && c.out_off >= c.out.size()) to_close.push_back(c.fd);
+      continue;
+    }
     if (c.chat_mode && !c.got_first && now >= c.first_deadline_mono) {
       const std::string e = "event: error\ndata: {\"error\":\"timeout waiting for response\"}\n\n";
       append_chunk(c.out, e.data(), e.size());
@@ -750,6 +951,10 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
   if (c.role == Role::kMetrics) {
     if (path == "/metrics") write_raw(c, simple_response(200, metrics().render(), "text/plain; version=0.0.4", ka));
     else write_raw(c, http_error(404, "404 page not found", ka));
+    return;
+  }
+  if (path == "/v1/chat/completions" || path == "/v1/models") {  // vLLM's OpenAI surface, both HTTP roles
+    handle_openai(c, req);
     return;
   }
   if (c.role == Role::kOrigin) {

@@ -75,6 +75,9 @@ struct ChatRequest {
   int64_t seed = -1;
   bool ignore_eos = false;
   bool from_edge = false;    // submitted by the edge /chat (a subscriber exists)
+  // OpenAI chat (POST /v1/chat/completions): the conversation as normalised JSON
+  // [{"role":..,"content":..},..]; empty = `message` is a single user turn
+  std::string messages_json;
 };
 
 class RequestQueue {

@@ -162,7 +162,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     import os
 
     from .. import runtime as rt_mod
-    from ..models.tokenizer import SyntheticTokenizer
+    from ..models.tokenizer import SyntheticTokenizer, prompt_for_request
     from .engine import LLMEngine, SamplingParams
 
     if tp != 1:
@@ -207,7 +207,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     def pump(block_ms=0):
         for req in chan.poll_requests(1024, block_ms):
             p = SamplingParams(temperature=1.0, top_p=1.0, max_tokens=req["max_tokens"], ignore_eos=True)
-            engine.add_request(req["conversation_id"], tok.chat_prompt(req["message"]), p,
+            engine.add_request(req["conversation_id"], prompt_for_request(tok, req), p,
                                arrival_ns=req["arrival_ns"])
 
     import gc

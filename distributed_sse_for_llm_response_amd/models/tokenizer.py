@@ -9,6 +9,7 @@ id maps to a printable, valid-UTF-8 piece (so streamed deltas are well-formed JS
 """
 from __future__ import annotations
 
+import json
 import re
 import zlib
 
@@ -66,6 +67,21 @@ class SyntheticTokenizer:
         """[INST] message [/INST] framing of the Mistral instruct template (synthetic ids)."""
         return self.encode("[INST] " + message + " [/INST]")
 
+    def messages_prompt(self, messages: list) -> list:
+        """Multi-turn Mistral framing: <s>[INST] u1 [/INST] a1</s>[INST] u2 [/INST] (system text joins the
+        first user turn, as the v0.3 template folds it into a user message)."""
+        ids = [self.bos_id]
+        system = " ".join(m["content"] for m in messages if m["role"] == "system")
+        first = True
+        for m in messages:
+            if m["role"] == "user":
+                text = (system + "\n\n" + m["content"]) if (first and system) else m["content"]
+                ids += self.encode("[INST] " + text + " [/INST]", add_bos=False)
+                first = False
+            elif m["role"] == "assistant":
+                ids += self.encode(m["content"], add_bos=False) + [self.eos_id]
+        return ids
+
 
 class HFTokenizer:
     """Local HuggingFace tokenizer directory (no network access)."""
@@ -92,6 +108,18 @@ class HFTokenizer:
 
     def chat_prompt(self, message: str) -> list:
         return self.tok.apply_chat_template([{"role": "user", "content": message}], add_generation_prompt=True)
+
+    def messages_prompt(self, messages: list) -> list:
+        return self.tok.apply_chat_template(messages, add_generation_prompt=True)
+
+
+def prompt_for_request(tok, req: dict) -> list:
+    """Prompt ids of a queued chat request: the OpenAI `messages` conversation when the request came from
+    POST /v1/chat/completions, else the single `message` of POST /chat."""
+    msgs = req.get("messages")
+    if msgs:
+        return tok.messages_prompt(json.loads(msgs))
+    return tok.chat_prompt(req["message"])
 
 
 def get_tokenizer(vocab_size: int, path: str | None = None):

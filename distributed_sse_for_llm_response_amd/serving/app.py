@@ -23,7 +23,7 @@ from ..engine.engine import LLMEngine, SamplingParams
 from ..engine.kv_cache import KVCache
 from ..engine.model_runner import ModelRunner
 from ..models.mistral import TINY, get_config, init_standard_weights
-from ..models.tokenizer import get_tokenizer
+from ..models.tokenizer import get_tokenizer, prompt_for_request
 from .config import ServeConfig
 from .faults import FaultPlan, StepTracer, Watchdog
 
@@ -144,7 +144,7 @@ class EngineLoop(threading.Thread):
                 # only paused streams left: wait briefly so their resume events get through
                 wait = 0 if busy else (2 if self.engine.has_work() else 20)
                 for req in self.rt.poll_requests(256, wait):
-                    self.engine.add_request(req["conversation_id"], self.tok.chat_prompt(req["message"]),
+                    self.engine.add_request(req["conversation_id"], prompt_for_request(self.tok, req),
                                             self._params(req), arrival_ns=req["arrival_ns"])
                 for conv in self.rt.pop_cancellations():
                     self.engine.abort(conv)

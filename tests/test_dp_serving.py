@@ -185,6 +185,13 @@ def test_serve_dp2_cpu_engines_end_to_end():
         # greedy + same seed on both replicas: the same prompt gives the same text on either GPU
         texts = {"".join(t["token"] for t in toks[:-1]) for _, toks in outs}
         assert len(texts) == 1
+        # the OpenAI surface goes through the router too (the conversation rides the shm ring to a worker)
+        expected = texts.pop()  # a single user turn is framed exactly like POST /chat's message
+        for _ in range(2):
+            r = request(H, sse, "POST", "/v1/chat/completions",
+                        {"messages": [{"role": "user", "content": "hello there"}], "max_tokens": 6}, timeout=120)
+            assert r.status == 200
+            assert json.loads(r.body)["choices"][0]["message"]["content"] == expected
     finally:
         p.terminate()
         try:

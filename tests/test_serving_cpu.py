@@ -82,3 +82,58 @@ def test_loadgen_twin_chat_mode_against_stub():
         assert st.errors == 0 and st.received == 50 * 6
     finally:
         app.stop()
+
+
+def _reference_proxy_parse(events):
+    """The reference llm-stream-proxy's reading of a vLLM stream (src/llm-stream-proxy/main.go:192-227):
+    `data: ` lines, `[DONE]` terminates, each chunk's choices[].delta.content is a token, a non-null
+    finish_reason ends the stream."""
+    deltas, finish = [], None
+    for e in events:
+        if e.data == "[DONE]":
+            break
+        chunk = json.loads(e.data)
+        assert chunk["object"] == "chat.completion.chunk" and chunk["id"].startswith("chatcmpl-")
+        for ch in chunk["choices"]:
+            if ch["delta"].get("content"):
+                deltas.append(ch["delta"]["content"])
+            if ch["finish_reason"] is not None:
+                finish = ch["finish_reason"]
+    return deltas, finish
+
+
+def test_openai_chat_completions_stream_as_the_reference_proxy_reads_it(cpu_app):
+    body = {"model": "mistralai/Mistral-7B-Instruct-v0.3", "stream": True, "max_tokens": 5,
+            "messages": [{"role": "user", "content": "Why stream tokens?"}]}
+    for port in (cpu_app.port("origin"), cpu_app.port("edge")):
+        r = request(H, port, "POST", "/v1/chat/completions", body, timeout=60, stop_on_done=False)
+        assert r.status == 200 and r.headers.get("content-type", "").startswith("text/event-stream")
+        assert r.events[0].json()["choices"][0]["delta"] == {"role": "assistant", "content": ""}
+        assert r.events[-1].data == "[DONE]"
+        deltas, finish = _reference_proxy_parse(r.events)
+        assert len(deltas) == 5 and finish == "length"
+        pieces = set(cpu_app.tok.pieces())
+        assert all(d in pieces for d in deltas)
+
+
+def test_openai_chat_completions_non_stream_multi_turn_and_models(cpu_app):
+    msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hello"},
+            {"role": "assistant", "content": "hi there"}, {"role": "user", "content": [{"type": "text", "text": "and?"}]}]
+    outs = []
+    for _ in range(2):
+        r = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions", {"messages": msgs, "max_tokens": 4},
+                    timeout=60)
+        assert r.status == 200
+        d = json.loads(r.body)
+        assert d["object"] == "chat.completion" and d["choices"][0]["message"]["role"] == "assistant"
+        assert d["choices"][0]["finish_reason"] in ("stop", "length") and d["usage"]["completion_tokens"] <= 4
+        outs.append(d["choices"][0]["message"]["content"])
+    assert outs[0] == outs[1] and outs[0]  # greedy: the same conversation gives the same completion
+    # the conversation (not just the last user turn) is the prompt
+    r = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions",
+                {"messages": [{"role": "user", "content": "and?"}], "max_tokens": 4}, timeout=60)
+    assert json.loads(r.body)["choices"][0]["message"]["content"] != outs[0]
+    m = json.loads(request(H, cpu_app.port("origin"), "GET", "/v1/models").body)
+    assert m["object"] == "list" and m["data"][0]["object"] == "model"
+    bad = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions", {"messages": []})
+    assert bad.status == 400 and json.loads(bad.body)["object"] == "error"
