@@ -93,7 +93,7 @@ struct SCfg {
 };
 // 64 < M <= 256: one workgroup holds all rows (mt 8 / 16, X slices of 256 / 128 columns); M > 256: row
 // blocks of 64 (mt 4, L2-shared weights).
-SCfg pick_stream(int M, int N, int K) {
+SCfg pick_stream(int M, int N, int K, int mode = -1) {
   SCfg c{};
   c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : (M <= 256 ? 16 : 4))));
   c.nt = M > 256 ? 1 : env_int("DSSE_S_NT", 1);  // row blocks (M > 256) are instantiated for nt = 1
@@ -120,12 +120,21 @@ SCfg pick_stream(int M, int N, int K) {
   const bool half = c.mt == 4 && c.nt == 1 && M <= 64 && (c.nw == 4 || c.nw == 8 || c.nw == 2) &&
                     env_int("DSSE_S_HALF", 0) == 1;
   if (half) c.rd = 18;
-  const int cps = c.mt <= 4 ? (half ? 2 : 4) : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
-  c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
+  // in-workgroup split-K by two (KS2, flagged as rd = 32 + 2): the two K halves meet in LDS, no slabs
+  // Opt-in (DSSE_S_KS2=1; DSSE_S_KS2=2 = only the QKV + RoPE projection, with S = 1): measured slower in situ
+  // for QKV at 64 rows (4.86 vs 4.73 ms per decode step, profiles/experiments_r1.md) although it removes the
+  // split-K reduce launch.
+  const int ks2_env = env_int("DSSE_S_KS2", 0);
+  const bool ks2 = !half && c.mt == 4 && c.nt == 1 && M <= 64 && (c.nw == 4 || c.nw == 8) &&
+                   (ks2_env == 1 || (ks2_env == 2 && mode == dsse::kQkvRope && c.nw == 4));
+  if (ks2) c.rd = 34;
+  const int cps = c.mt <= 4 ? ((half || ks2) ? 2 : 4) : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
+  const int kdiv = ks2 ? 2 : 1, tgw = ks2 ? c.nw / 2 : c.nw;
+  c.ok = K % (128 * cps * kdiv) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % tgw == 0;
   if (!c.ok) return c;
-  const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
+  const int wgs = N / (16 * c.nt) / tgw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps * kdiv);
   const int per_cu = half ? 2 : 1;
-  int S = env_int("DSSE_S_SPLIT", 0);
+  int S = env_int("DSSE_S_SPLIT", (ks2 && ks2_env < 0) ? 1 : 0);
   if (S <= 0 || slices % S != 0) {
     // smallest split that gives ~one workgroup per CU slot (256 CUs x per_cu), never more than 1.25x that
     S = 1;
@@ -215,7 +224,7 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
     return;
   }
   if (impl == 2) {
-    const SCfg c = pick_stream(M, N, K);
+    const SCfg c = pick_stream(M, N, K, mode);
     at::Tensor part;
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
     DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,

@@ -32,6 +32,8 @@ GEMM_CONFIGS = {
     "stream-default": {"DSSE_GEMM_IMPL": "2"},
     "stream-nt2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NT": "2"},
     "stream-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
+    "stream-ks2-nw8": {"DSSE_GEMM_IMPL": "2", "DSSE_S_KS2": "1", "DSSE_S_NW": "8"},
+    "stream-ks2-nw4-s1": {"DSSE_GEMM_IMPL": "2", "DSSE_S_KS2": "1", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "1"},
     "wide-default": {"DSSE_GEMM_IMPL": "3"},
     "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
