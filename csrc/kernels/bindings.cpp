@@ -134,7 +134,7 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
   if (!c.ok) return c;
   const int wgs = N / (16 * c.nt) / tgw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps * kdiv);
   const int per_cu = half ? 2 : 1;
-  int S = env_int("DSSE_S_SPLIT", (ks2 && ks2_env < 0) ? 1 : 0);
+  int S = env_int("DSSE_S_SPLIT", (ks2 && ks2_env == 2) ? 1 : 0);
   if (S <= 0 || slices % S != 0) {
     // smallest split that gives ~one workgroup per CU slot (256 CUs x per_cu), never more than 1.25x that
     S = 1;
