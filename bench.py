@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--delivery", default="sse", choices=["sse", "frame", "none"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--stub-step-ms", type=float, default=0.0,
+                    help="host-path rehearsal only: paced stub replicas emitting one token per stream every "
+                         "STUB_STEP_MS instead of the model (router/bus/SSE/client at N GPUs' token rate)")
     args = ap.parse_args()
 
     from distributed_sse_for_llm_response_amd.engine import bench_harness
@@ -73,7 +76,8 @@ def main():
     if sse:
         res = bench_harness.run_serving_bench(client, model=args.model, device=device, streams=args.streams,
                                               prompt_len=args.prompt_len, steps=args.steps, warmup=args.warmup,
-                                              tp=args.tp, use_graphs=not args.no_graph, rank=rank, world=world)
+                                              tp=args.tp, use_graphs=not args.no_graph, rank=rank, world=world,
+                                              stub_step_ms=args.stub_step_ms)
     else:
         res = bench_harness.run_decode_bench(model=args.model, device=device, streams=args.streams,
                                              prompt_len=args.prompt_len, steps=args.steps, warmup=args.warmup,
@@ -105,7 +109,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic prompts, random-init weights",
+            "data": "synthetic prompts, random-init weights" if not args.stub_step_ms else
+                    f"REHEARSAL: paced stub replicas at {args.stub_step_ms} ms/step, no model",
             "concurrent_streams": total_streams,
             "p50_itl_ms": round(res["p50_itl_ms"], 4),
             "p99_itl_ms": round(res.get("p99_itl_ms", 0.0), 4),

@@ -44,6 +44,59 @@ class _Drain:
         return self.host[row]
 
 
+class PacedStubEngine:
+    """Host-path rehearsal engine: the LLMEngine surface the serving bench drives (add_request / step /
+    slots / has_work), emitting one token per live stream every `step_ms`, like a GPU replica decoding
+    at that step time.  Lets the N-replica router + bus + SSE server + client path be driven at the
+    token rate of N real GPUs (N x streams / step_ms) on a host without them."""
+
+    class _Seq:
+        __slots__ = ("conversation_id", "state", "sequence", "max_tokens")
+
+        def __init__(self, cid, max_tokens):
+            self.conversation_id, self.state, self.sequence, self.max_tokens = cid, "decode", 0, max_tokens
+
+    def __init__(self, streams: int, step_ms: float, vocab: int):
+        from .engine import TokenEvent
+
+        self.TokenEvent = TokenEvent
+        self.slots: list = [None] * streams
+        self.step_s = step_ms / 1000.0
+        self.vocab = vocab
+        self.next_t = 0.0
+        self.started = False
+
+    def add_request(self, conversation_id, prompt, params, arrival_ns=0):
+        free = self.slots.index(None)
+        self.slots[free] = self._Seq(conversation_id, params.max_tokens)
+
+    def has_work(self) -> bool:
+        return any(s is not None for s in self.slots)
+
+    def step(self, block: bool = True) -> list:
+        if not self.started:  # hold tokens until every stream is admitted (the stub has no prefill to bound skew)
+            if any(s is None for s in self.slots):
+                time.sleep(0.001)
+                return []
+            self.started = True
+        now = time.perf_counter()
+        if self.next_t > now:
+            time.sleep(self.next_t - now)
+        self.next_t = max(now, self.next_t) + self.step_s
+        ev = []
+        for i, s in enumerate(self.slots):
+            if s is None:
+                continue
+            s.sequence += 1
+            if s.sequence > s.max_tokens:
+                ev.append(self.TokenEvent(s.conversation_id, 0, s.sequence, True, "[DONE]"))
+                self.slots[i] = None
+            else:
+                ev.append(self.TokenEvent(s.conversation_id, 3 + (s.sequence * 7919 + i) % (self.vocab - 3),
+                                          s.sequence, False))
+        return ev
+
+
 def _build_runner(model: str, device, streams: int, prompt_len: int, total_steps: int, tp: int, use_graphs: bool,
                   rank: int, world: int):
     cfg = get_config(model) if device.type == "cuda" else TINY
@@ -149,7 +202,7 @@ def spawn_client():
 
 
 def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, prompt_len=512, steps=64, warmup=8,
-                      tp=1, use_graphs=True, rank=0, world=1, seed=0):
+                      tp=1, use_graphs=True, rank=0, world=1, seed=0, stub_step_ms=0.0):
     """Full serving path: `streams` real POST /chat SSE connections per engine replica (one client process on
     rank 0) -> native runtime + data-parallel router on rank 0 -> shared-memory ring -> this rank's LLMEngine
     (scheduler, hipGraph decode, token-ring drain) -> ring -> router -> bus -> epoll writers -> sockets.
@@ -173,12 +226,17 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     # the whole timed window (full batch on every timed step): budget the tokens and the KV for it.
     skew = math.ceil(streams * (prompt_len + 16) / 8192) + 4
     total = steps + warmup + skew
-    cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
-    if use_graphs and device.type == "cuda":
-        r.capture()
-    tok = SyntheticTokenizer(cfg.vocab_size)
-    engine = LLMEngine(r, eos_id=tok.eos_id, prefill_budget=r.max_prefill_tokens,
-                       default_params=SamplingParams(temperature=1.0, top_p=1.0, max_tokens=total + 2))
+    if stub_step_ms > 0:  # host-path rehearsal: paced stub replicas, no model
+        cfg = get_config(model)
+        tok = SyntheticTokenizer(cfg.vocab_size)
+        engine = PacedStubEngine(streams, stub_step_ms, cfg.vocab_size)
+    else:
+        cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
+        if use_graphs and device.type == "cuda":
+            r.capture()
+        tok = SyntheticTokenizer(cfg.vocab_size)
+        engine = LLMEngine(r, eos_id=tok.eos_id, prefill_budget=r.max_prefill_tokens,
+                           default_params=SamplingParams(temperature=1.0, top_p=1.0, max_tokens=total + 2))
     mod = rt_mod.load()
     prefix = f"/dsse-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid() if world > 1 else os.getpid()}"
     runtime = None

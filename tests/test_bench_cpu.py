@@ -48,3 +48,21 @@ def test_bench_contract(world):
     assert d["config"]["global_batch"] == 3 * world and d["config"]["parallelism"] == f"dp{world}"
     assert d["value"] > 0 and d["client_errors"] == []
     assert d["tokens_delivered_in_window"] >= 3 * world * 2
+
+
+@pytest.mark.timeout(600)
+def test_bench_host_path_rehearsal_with_paced_stubs():
+    """--stub-step-ms: 4 stub replicas at 5 ms/step through router + bus + SSE + native client; the measured
+    step time tracks the stub pace and every stream's tokens arrive (profiles/host_path_rehearsal_r1.md)."""
+    args = ["bench.py", "--gpus", "4", "--steps", "32", "--warmup", "4", "--streams", "16", "--stub-step-ms", "5"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    assert d["data"].startswith("REHEARSAL")
+    assert d["config"]["global_batch"] == 64 and d["client_errors"] == []
+    assert 4.5 < d["ms_per_step"] < 8.0, d
+    assert d["tokens_delivered_in_window"] >= 0.9 * 64 * 32, d
