@@ -246,7 +246,20 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
                                   cur_stream()));
 }
 
-void gemm_out(const Tensor& x, const Tensor& w, Tensor& out) {
+// Deferred-norm input (rmsnorm with row_ss): scale row m of the product by rsqrt(sum(row_ss[m]) / K + eps).
+void set_rowss(dsse::GemmEpi& ep, const c10::optional<Tensor>& row_ss, const Tensor& x, double eps) {
+  if (!row_ss.has_value()) return;
+  check_gpu(*row_ss, "row_ss");
+  check_dtype(*row_ss, at::kFloat, "row_ss");
+  TORCH_CHECK(row_ss->dim() == 2 && row_ss->size(0) >= x.size(0) && row_ss->is_contiguous(),
+              "row_ss must be a contiguous [>= M, G] fp32 tensor");
+  ep.rowss = row_ss->data_ptr<float>();
+  ep.nss = (int)row_ss->size(1);
+  ep.inv_k = 1.f / (float)x.size(1);
+  ep.eps = (float)eps;
+}
+
+void gemm_out(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& row_ss, double eps) {
   check_gpu(out, "out");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) == w.size(0),
               "out must be [M, N]");
@@ -257,6 +270,7 @@ void gemm_out(const Tensor& x, const Tensor& w, Tensor& out) {
   if (out.scalar_type() == at::kBFloat16) mode = dsse::kStoreBf16;
   else if (out.scalar_type() == at::kFloat) mode = dsse::kStoreF32;
   else TORCH_CHECK(false, "out must be bf16 or fp32");
+  set_rowss(ep, row_ss, x, eps);
   run_gemm(mode, x, w, ep);
 }
 
@@ -318,7 +332,7 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   return 0;
 }
 
-void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out) {
+void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& row_ss, double eps) {
   check_gpu(out, "out");
   check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) * 2 == w.size(0),
@@ -326,12 +340,13 @@ void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out) {
   dsse::GemmEpi ep{};
   ep.out = out.data_ptr();
   ep.ldo = (int)out.size(1);
+  set_rowss(ep, row_ss, x, eps);
   run_gemm(dsse::kSiluMul, x, w, ep);
 }
 
 void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
                    const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
-                   int64_t nkv) {
+                   int64_t nkv, const c10::optional<Tensor>& row_ss, double eps) {
   for (auto* t : {&positions, &slots, &rope}) check_gpu(*t, "metadata");
   check_gpu(q_out, "q_out");
   check_gpu(k_cache, "k_cache");
@@ -359,12 +374,13 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
   ep.nkv = (int)nkv;
   ep.num_slots = (int)(k_cache.size(0) * dsse::kBS);
   ep.rope_len = (int)rope.size(0);
+  set_rowss(ep, row_ss, x, eps);
   run_gemm(dsse::kQkvRope, x, w, ep);
 }
 
 void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
              const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids,
-             const c10::optional<Tensor>& part, int64_t nsplit) {
+             const c10::optional<Tensor>& part, int64_t nsplit, const c10::optional<Tensor>& row_ss) {
   check_gpu(resid, "resid");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -395,6 +411,26 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     TORCH_CHECK(delta->size(0) >= M && delta->size(1) == H, "delta shape mismatch");
     mode = 1;
     dptr = delta->data_ptr();
+  }
+  if (row_ss.has_value()) {  // deferred norm: split-K slabs (or nothing) added, scale left to the GEMM
+    TORCH_CHECK(mode == 0, "row_ss (deferred norm) takes no delta / embed");
+    check_gpu(*row_ss, "row_ss");
+    check_dtype(*row_ss, at::kFloat, "row_ss");
+    const int G = (int)row_ss->size(1);
+    TORCH_CHECK(row_ss->dim() == 2 && row_ss->size(0) >= M && row_ss->is_contiguous() && G > 0 && H % (4 * G) == 0 &&
+                    (H / (4 * G)) % 64 == 0 && H / (4 * G) <= 1024,
+                "row_ss must be [>= M, G] with H / (4 G) a multiple of 64 threads, <= 1024");
+    const float* pp = nullptr;
+    if (nsplit > 0) {
+      TORCH_CHECK(part.has_value(), "nsplit > 0 needs part");
+      check_gpu(*part, "part");
+      check_dtype(*part, at::kFloat, "part");
+      TORCH_CHECK(part->numel() >= nsplit * M * H, "part too small for ", nsplit, " slabs");
+      pp = part->data_ptr<float>();
+    }
+    DSSE_CHECK_HIP(dsse_rmsnorm_deferred(M, resid.data_ptr<float>(), H, w.data_ptr(), y.data_ptr(), pp, (int)nsplit,
+                                         row_ss->data_ptr<float>(), G, cur_stream()));
+    return;
   }
   const float* pptr = nullptr;
   if (part.has_value() && nsplit > 0 && mode == 0) {
@@ -590,7 +626,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 4; }
+int64_t kernels_abi_version() { return 5; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -622,13 +658,13 @@ std::string kernel_check_files() {
 }  // namespace
 
 TORCH_LIBRARY(dsse, m) {
-  m.def("gemm_out(Tensor x, Tensor w, Tensor(a!) out) -> ()");
+  m.def("gemm_out(Tensor x, Tensor w, Tensor(a!) out, Tensor? row_ss=None, float eps=0.0) -> ()");
   m.def("gemm_resid(Tensor x, Tensor w, Tensor(a!) resid) -> ()");
-  m.def("gemm_silu(Tensor x, Tensor w, Tensor(a!) out) -> ()");
+  m.def("gemm_silu(Tensor x, Tensor w, Tensor(a!) out, Tensor? row_ss=None, float eps=0.0) -> ()");
   m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
-        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor? row_ss=None, float eps=0.0) -> ()");
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
-        "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
+        "Tensor? ids=None, Tensor? part=None, int nsplit=0, Tensor(c!)? row_ss=None) -> ()");
   m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");

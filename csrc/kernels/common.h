@@ -62,6 +62,24 @@ DEV T wave_sum(T v) {
 // K tiles of the flash prefill).  Apply as chunk ^ swz(row & 15) on both the write and the read.
 DEV int swz(int row) { return row ^ ((((row >> 2) ^ (row >> 3)) & 1) << 2); }
 
+// Max / sum over the four 16-lane rows of a wave (lanes r, r+16, r+32, r+48: the xor-16 and xor-32 partners)
+// with the gfx950 row swaps v_permlane16_swap / v_permlane32_swap -- VALU, no ds_bpermute round trip.
+DEV float rows4_max(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  float a = __uint_as_float(p[0]), b = __uint_as_float(p[1]);
+  v = a > b ? a : b;
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(q[0]);
+  b = __uint_as_float(q[1]);
+  return a > b ? a : b;
+}
+DEV float rows4_sum(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 DEV float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 // Philox4x32-10 counter-based RNG (one 32-bit output used per call site).

@@ -61,12 +61,13 @@ def _hip(t: torch.Tensor) -> bool:
     return False
 
 
-def gemm_out(x, w, out):
-    """out[M, N] = x[M, K] · w[N, K]ᵀ (bf16 or fp32 out)."""
+def gemm_out(x, w, out, row_ss=None, eps=0.0):
+    """out[M, N] = x[M, K] · w[N, K]ᵀ (bf16 or fp32 out).  With `row_ss` (from rmsnorm(..., row_ss=)) row m
+    of the product is scaled by rsqrt(sum(row_ss[m]) / K + eps): the deferred RMSNorm scale."""
     if _hip(x):
-        torch.ops.dsse.gemm_out(x, w, out)
+        torch.ops.dsse.gemm_out(x, w, out, row_ss, eps)
     else:
-        ref.gemm_out(x, w, out)
+        ref.gemm_out(x, w, out, row_ss, eps)
 
 
 def gemm_resid(x, w, resid):
@@ -77,20 +78,20 @@ def gemm_resid(x, w, resid):
         ref.gemm_resid(x, w, resid)
 
 
-def gemm_silu(x, w, out):
-    """out[M, N/2] = silu(gate) * up with the interleaved gate/up weight rows."""
+def gemm_silu(x, w, out, row_ss=None, eps=0.0):
+    """out[M, N/2] = silu(gate) * up with the interleaved gate/up weight rows (row_ss: as gemm_out)."""
     if _hip(x):
-        torch.ops.dsse.gemm_silu(x, w, out)
+        torch.ops.dsse.gemm_silu(x, w, out, row_ss, eps)
     else:
-        ref.gemm_silu(x, w, out)
+        ref.gemm_silu(x, w, out, row_ss, eps)
 
 
-def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
-    """Fused QKV projection + RoPE + paged KV write (decode)."""
+def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss=None, eps=0.0):
+    """Fused QKV projection + RoPE + paged KV write (decode; row_ss: as gemm_out)."""
     if _hip(x):
-        torch.ops.dsse.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+        torch.ops.dsse.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss, eps)
     else:
-        ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+        ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss, eps)
 
 
 def gemm_resid_split(x, w, resid, part) -> int:
@@ -102,11 +103,16 @@ def gemm_resid_split(x, w, resid, part) -> int:
     return 0
 
 
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0, row_ss=None):
+    """resid (+= delta | sum of `nsplit` split-K slabs in `part` | = embed[ids]); y = rmsnorm(resid) * w.
+
+    With `row_ss` [M, G] (fp32; split-K slab or no-delta mode only) the norm is deferred to the consuming
+    decode GEMM: y = bf16(resid * w) and row_ss[m, g] = sum of squares of chunk g of row m, so the kernel
+    spreads every row over G workgroups with no row-wide reduction; pass row_ss (and eps) to the GEMM."""
     if _hip(resid):
-        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
+        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit, row_ss)
     else:
-        ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
+        ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit, row_ss)
 
 
 def rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
