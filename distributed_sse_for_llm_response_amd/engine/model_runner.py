@@ -49,6 +49,12 @@ DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "192"))
 DEFERRED_NORM = os.environ.get("DSSE_DEFERRED_NORM", "0") == "1"  # measured slower (profiles/experiments_r1.md)
 
 
+# Decode buckets above DECODE_GEMM_MAX_M (<= 256 rows): projections that run on the engine's 32x32-MFMA decode GEMM
+# (gemm_wide) instead of hipBLASLt -- QKV with its fused RoPE + KV-write epilogue (no separate rope kernel) and,
+# at TP=1, down with its split-K slabs reduced inside the next norm (profiles/experiments_r1.md).
+WIDE_ENGINE_OPS = frozenset(x for x in os.environ.get("DSSE_WIDE_ENGINE_OPS", "qkv,down").split(",") if x)
+
+
 def norm_chunks(H: int) -> int:
     """Column chunks per row of the deferred norm: 128 threads x float4 per workgroup (H = 4096 -> 8)."""
     return max(1, H // 512) if H % 512 == 0 else 1
@@ -211,10 +217,16 @@ class ModelRunner:
         q3 = self.q[r].view(B, nh, 128)
         a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
+        eng_qkv = "qkv" in WIDE_ENGINE_OPS and B <= 256
+        eng_down = "down" in WIDE_ENGINE_OPS and B <= 256 and comm.size == 1
         for li, L in enumerate(w.layers):
-            qkv = torch.matmul(x, L.wqkv.t())
-            ops.rope_kv_write(qkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li], self.kv.v[li],
-                              nh, nkv)
+            if eng_qkv:
+                ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+                                  self.kv.v[li], nh, nkv)
+            else:
+                qkv = torch.matmul(x, L.wqkv.t())
+                ops.rope_kv_write(qkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+                                  self.kv.v[li], nh, nkv)
             ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
                                 self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
                                 self.part_ml, part, nparts)
@@ -223,10 +235,14 @@ class ModelRunner:
             ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=o)
             gu = torch.matmul(x, L.wgu.t())
             ops.silu_mul(gu, self.h[r])
-            down = torch.matmul(self.h[r], L.wd.t())
-            comm.all_reduce(down)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-            ops.rmsnorm(resid, w_next, x, eps, delta=down)
+            if eng_down:
+                ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
+                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
+            else:
+                down = torch.matmul(self.h[r], L.wd.t())
+                comm.all_reduce(down)
+                ops.rmsnorm(resid, w_next, x, eps, delta=down)
         step = 256 if DECODE_GEMM_MAX_M > 2 else DECODE_GEMM_MAX_M  # one 256-row call streams the head once
         for b0 in range(0, B, step):
             b1 = min(B, b0 + step)
