@@ -95,6 +95,20 @@ def test_tp4_matches_tp1():
         assert res[0] == _generate(0, 1, temperature, SMALL)
 
 
+@pytest.mark.timeout(1200)
+def test_tp8_matches_tp1():
+    """TP=8, the degree of BASELINE config 4 (one KV head and a 1/8 vocab shard per rank; 16 q / 8 kv heads so
+    that eight ranks each hold a whole GQA group): greedy and sampled tokens equal TP=1 on every rank."""
+    from distributed_sse_for_llm_response_amd.models.mistral import MistralConfig
+
+    cfg = MistralConfig(name="mistral-tp8-test", vocab_size=2048, hidden_size=2048, intermediate_size=2048,
+                        num_layers=2, num_heads=16, num_kv_heads=8, max_position=4096)
+    for temperature in (0.0, 1.0):
+        res = _tp_run(8, temperature, cfg)
+        assert all(r == res[0] for r in res), "TP ranks disagree on the sampled tokens"
+        assert res[0] == _generate(0, 1, temperature, cfg)
+
+
 def _free_port():
     return _port()
 
