@@ -19,14 +19,24 @@ BTS = [[0, 1, 2], [10, 4, 5, 6], [20, 21, 22]]
 STEPS = 6
 
 
-def _generate(rank, world, device):
+def _cfg(name):
+    from distributed_sse_for_llm_response_amd.models.mistral import MistralConfig
+
+    if name == "small":
+        return SMALL
+    # 16 q / 8 kv heads: eight ranks each hold one KV head (a whole GQA group), as at TP=8 for Mistral-7B
+    return MistralConfig(name="mistral-tp8-test", vocab_size=2048, hidden_size=2048, intermediate_size=2048,
+                         num_layers=2, num_heads=16, num_kv_heads=8, max_position=4096)
+
+
+def _generate(rank, world, device, cfg=SMALL):
     from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
     from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
     from distributed_sse_for_llm_response_amd.parallel.comm import TPComm
 
-    std = init_standard_weights(SMALL, seed=3)
+    std = init_standard_weights(cfg, seed=3)
     comm = TPComm(rank=rank, size=world, group=None) if world > 1 else TPComm()
-    w = convert_standard(SMALL, std, tp_rank=rank, tp_size=world, device=device)
+    w = convert_standard(cfg, std, tp_rank=rank, tp_size=world, device=device)
     r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device=device, comm=comm, use_graphs=False)
     for i, bt in enumerate(BTS):
         r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
@@ -41,17 +51,19 @@ def _generate(rank, world, device):
     return gen
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, cfg_name="small"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out[rank] = _generate(rank, world, torch.device("cuda", 0))
+        out[rank] = _generate(rank, world, torch.device("cuda", 0), _cfg(cfg_name))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_tp2_on_gpu_kernels_matches_reference():
+@pytest.mark.parametrize("world,cfg_name", [(2, "small"), (4, "small"), (8, "tp8")])
+def test_tp_on_gpu_kernels_matches_reference(world, cfg_name):
+    """TP = 2 / 4 / 8 ranks time-sharing the one GPU (8 ranks: one KV head and a 1/8 vocab shard each)."""
     import socket
 
     s = socket.socket()
@@ -61,13 +73,14 @@ def test_tp2_on_gpu_kernels_matches_reference():
     ctx = mp.get_context("spawn")
     with ctx.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
-        res = [out[0], out[1]]
-    assert res[0] == res[1], "TP ranks disagree on the sampled tokens"
-    std = init_standard_weights(SMALL, seed=3)
+        mp.spawn(_worker, args=(world, port, out, cfg_name), nprocs=world, join=True)
+        res = [out[r] for r in range(world)]
+    assert all(r == res[0] for r in res), "TP ranks disagree on the sampled tokens"
+    cfg = _cfg(cfg_name)
+    std = init_standard_weights(cfg, seed=3)
     worst = 0.0
     for i in range(3):
-        logits, _ = reference_forward(SMALL, std, torch.tensor(PROMPTS[i] + res[0][i]))
+        logits, _ = reference_forward(cfg, std, torch.tensor(PROMPTS[i] + res[0][i]))
         L = len(PROMPTS[i])
         for j, g in enumerate(res[0][i]):
             row = logits[L - 1 + j]
