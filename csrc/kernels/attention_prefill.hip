@@ -29,6 +29,17 @@ constexpr int kBK = 64;    // keys per iteration (2 pages)
 constexpr int kKBytes = kBK * kD * 2;  // 16 KiB
 constexpr int kStage = 2 * kKBytes;    // K + Vᵀ
 constexpr float kRescaleThr = 8.f;     // deferred online-softmax rescale threshold (log2 units)
+
+// KV block of page `pg` (clamped to the last page: pages past the context are a harmless, masked re-read).
+// The index is workgroup-uniform, so this is a scalar load: waiting for it (lgkmcnt) does not drain the
+// vector loads of the K/V blocks already in flight, as a per-lane block-table load's vmcnt(0) did.
+// (The block table is read-only for the kernel's lifetime, so reading it through the constant address space
+// is safe and lets the compiler issue s_load_dword.)
+DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
+  pg = __builtin_amdgcn_readfirstlane(min(pg, npages - 1));
+  const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
+  return DSSE_IDX(cbt[DSSE_IDX(pg, p.max_blocks, 0)], p.num_blocks, 0);
+}
 }  // namespace
 
 // DIST: K/V prefetch distance in blocks.  1 = the next block's loads are issued at the top of an iteration and
@@ -73,13 +84,13 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
 
   // ---- staging: pieces [0, 1024) = K (page, token, 16-byte chunk), [1024, 2048) = V (page, d, chunk)
   auto load_block = [&](int j, bf16x8 (&st)[PPT]) {
+    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int pc = threadIdx.x + i * NT;
       const int v = pc >> 10, off = pc & 1023;
       const int page = off >> 9, o2 = off & 511;
-      const int pg = min(2 * j + page, npages - 1);  // pages past the context: harmless re-read, masked
-      const int blk = DSSE_IDX(bt[DSSE_IDX(pg, p.max_blocks, 0)], p.num_blocks, 0);
+      const int blk = page ? blk1 : blk0;
       const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
                                : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
       st[i] = ld_bf16x8(src);
@@ -115,12 +126,13 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   bf16x8 st0[PPT], st1[PPT];
   load_block(0, st0);
   store_block(0, st0);
-  if (DIST == 2 && nblk > 1) load_block(1, st1);
+  if (DIST == 2) load_block(1, st1);
   // one key block: ld receives the block loaded in this iteration, sv holds the block written to LDS at its end
   auto step = [&](int j, bf16x8 (&ld)[PPT], bf16x8 (&sv)[PPT]) {
     __syncthreads();
-    const bool more = j + 1 < nblk;
-    if (j + DIST < nblk) load_block(j + DIST, ld);
+    // unconditional loads and stores (pages clamp to the context; the blocks past the last are never read):
+    // a branch around them made the compiler's waitcnt placement drain every load in flight (vmcnt(0))
+    load_block(j + DIST, ld);
     const int key0 = j * kBK;
     if (key0 <= w_last_pos) {  // this wave sees at least one key of the block
       const char* kb = smem + (j & 1) * kStage;
@@ -215,11 +227,13 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
         }
     }
-    if (more) store_block((j + 1) & 1, DIST == 2 ? sv : ld);
+    store_block((j + 1) & 1, DIST == 2 ? sv : ld);
   };
   for (int j = 0; j < nblk; j += 2) {
     step(j, st0, st1);
-    if (j + 1 < nblk) step(j + 1, DIST == 2 ? st1 : st0, DIST == 2 ? st0 : st1);
+    // also when j + 1 == nblk (no wave sees that block: loads, stores and the barrier only) -- a branch here
+    // made the loop header's waitcnt merge drain the loads in flight
+    step(j + 1, DIST == 2 ? st1 : st0, DIST == 2 ? st0 : st1);
   }
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
@@ -283,13 +297,13 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_pipe_kernel(AttnParams 
 
   bf16x8 st[PPT];
   auto load_block = [&](int j) {
+    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int pc = threadIdx.x + i * NT;
       const int v = pc >> 10, off = pc & 1023;
       const int page = off >> 9, o2 = off & 511;
-      const int pg = min(2 * j + page, npages - 1);  // past the context (incl. the block after the last): masked
-      const int blk = DSSE_IDX(bt[DSSE_IDX(pg, p.max_blocks, 0)], p.num_blocks, 0);
+      const int blk = page ? blk1 : blk0;
       const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
                                : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
       st[i] = ld_bf16x8(src);
