@@ -72,8 +72,15 @@ paged_attention_kernel(AttnParams p) {
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
   // while the current one is computed (measured slower for decode: VGPRs 100 -> 140 cost occupancy).
-  auto load_page = [&](int kb, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
-    const int page = DSSE_IDX(bt[DSSE_IDX(kb / kPage, p.max_blocks, 0)], p.num_blocks, 0);
+  // KV page of key kb: a wave-uniform index, read through the constant address space (the block table is
+  // read-only for the kernel) so it is an s_load_dword -- a per-lane block-table load made every page wait
+  // vmcnt(0) behind it, draining the K/V loads in flight.
+  auto page_of = [&](int kb) {
+    const int i = __builtin_amdgcn_readfirstlane(DSSE_IDX(kb / kPage, p.max_blocks, 0));
+    const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
+    return DSSE_IDX(cbt[i], p.num_blocks, 0);
+  };
+  auto load_page = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
     const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
     const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
     // K rows for keys kb + r and kb + 16 + r; k-step s of the 4 lane groups = 64 contiguous bytes of a row.
@@ -125,9 +132,12 @@ paged_attention_kernel(AttnParams p) {
   constexpr int kStep = 32 * KWV;
   int kb = kbeg + 32 * kw;
   if constexpr (!PF) {
+    // the next page's index is fetched one page ahead (scalar load under this page's compute)
+    int page = kb < kend ? page_of(kb) : 0;
     for (; kb < kend; kb += kStep) {
       bf16x8 k0[4], k1[4], vf[8];
-      load_page(kb, k0, k1, vf);
+      load_page(page, k0, k1, vf);
+      page = page_of(min(kb + kStep, kend - 1));
       compute_page(kb, k0, k1, vf);
     }
   } else if (kb < kend) {
@@ -136,13 +146,13 @@ paged_attention_kernel(AttnParams p) {
     bf16x8 ka0[4], ka1[4], va[8], kc0[4], kc1[4], vc[8];
     const int n = (kend - kb + kStep - 1) / kStep;  // pages of this wave
     const int kb_last = kb + (n - 1) * kStep;
-    load_page(kb, ka0, ka1, va);
+    load_page(page_of(kb), ka0, ka1, va);
     for (int i = 0; i < n; i += 2) {
-      load_page(min(kb + kStep, kb_last), kc0, kc1, vc);
+      load_page(page_of(min(kb + kStep, kb_last)), kc0, kc1, vc);
       compute_page(kb, ka0, ka1, va);
       kb += kStep;
       if (i + 1 >= n) break;
-      load_page(min(kb + kStep, kb_last), ka0, ka1, va);
+      load_page(page_of(min(kb + kStep, kb_last)), ka0, ka1, va);
       compute_page(kb, kc0, kc1, vc);
       kb += kStep;
     }
