@@ -46,16 +46,17 @@ DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
 }
 }  // namespace
 
-// DIST: K/V prefetch distance in blocks.  1 = the next block's loads are issued at the top of an iteration and
-// written to LDS at its end (one iteration of compute to hide the load latency); 2 = two register staging sets,
-// block j+2's loads issued in iteration j and written to LDS at the end of iteration j+1.
+// DIST: K/V staging mode.  1 = the next block's loads are issued at the top of an iteration and written to LDS
+// at its end (one iteration of compute to hide the load latency); 2 = two register staging sets, block j+2's
+// loads issued in iteration j and written to LDS at the end of iteration j+1; 3 (default) = two blocks per LDS
+// stage and per barrier (8k TTFT 116.1 / 116.6 / 115.5 ms for 1 / 2 / 3, profiles/experiments_r1.md).
 template <int G, int DIST>
 __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   constexpr int NW = 2 * G;
   constexpr int NT = 64 * NW;
   constexpr int PIECES = kStage / 16;  // 16-byte pieces per stage = 2048
   constexpr int PPT = PIECES / NT;             // pieces per thread
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 (DIST 1, 2) or 4 (DIST 3) stages of kStage
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -132,14 +133,11 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   store_block(0, st0);
   if (DIST == 2) load_block(1, st1);
   // one key block: ld receives the block loaded in this iteration, sv holds the block written to LDS at its end
-  auto step = [&](int j, bf16x8 (&ld)[PPT], bf16x8 (&sv)[PPT]) {
-    __syncthreads();
-    // unconditional loads and stores (pages clamp to the context; the blocks past the last are never read):
-    // a branch around them made the compiler's waitcnt placement drain every load in flight (vmcnt(0))
-    load_block(j + DIST, ld);
+  // softmax + PV of key block j staged in LDS buffer `buf`
+  auto compute_block = [&](int j, int buf) {
     const int key0 = j * kBK;
     if (key0 <= w_last_pos) {  // this wave sees at least one key of the block
-      const char* kb = smem + (j & 1) * kStage;
+      const char* kb = smem + buf * kStage;
       const char* vb = kb + kKBytes;
       // Sᵀ[key tile kt][query tile qt]
       f32x4 s4[4][2];
@@ -245,13 +243,37 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
         }
     }
+  };
+  auto step = [&](int j, bf16x8 (&ld)[PPT], bf16x8 (&sv)[PPT]) {
+    __syncthreads();
+    // unconditional loads and stores (pages clamp to the context; the blocks past the last are never read):
+    // a branch around them made the compiler's waitcnt placement drain every load in flight (vmcnt(0))
+    load_block(j + DIST, ld);
+    compute_block(j, j & 1);
     store_block((j + 1) & 1, DIST == 2 ? sv : ld);
   };
-  for (int j = 0; j < nblk; j += 2) {
-    step(j, st0, st1);
-    // also when j + 1 == nblk (no wave sees that block: loads, stores and the barrier only) -- a branch here
-    // made the loop header's waitcnt merge drain the loads in flight
-    step(j + 1, DIST == 2 ? st1 : st0, DIST == 2 ? st0 : st1);
+  if constexpr (DIST == 3) {
+    // two key blocks per LDS stage and per barrier (4 x 32 KiB dynamic LDS): stage s = blocks 2s, 2s + 1 in
+    // buffers 2 (s & 1) + {0, 1}; the next stage's loads are issued at the top and written at the end
+    load_block(1, st1);
+    store_block(1, st1);
+    for (int j = 0; j < nblk; j += 2) {
+      __syncthreads();
+      const int nb = ((j >> 1) + 1) & 1;
+      load_block(j + 2, st0);
+      load_block(j + 3, st1);
+      compute_block(j, 2 * (nb ^ 1));
+      compute_block(j + 1, 2 * (nb ^ 1) + 1);
+      store_block(2 * nb, st0);
+      store_block(2 * nb + 1, st1);
+    }
+  } else {
+    for (int j = 0; j < nblk; j += 2) {
+      step(j, st0, st1);
+      // also when j + 1 == nblk (no wave sees that block: loads, stores and the barrier only) -- a branch here
+      // made the loop header's waitcnt merge drain the loads in flight
+      step(j + 1, DIST == 2 ? st1 : st0, DIST == 2 ? st0 : st1);
+    }
   }
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
@@ -512,21 +534,40 @@ extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p
   }
   static const int dist = [] {
     const char* e = getenv("DSSE_PREFILL_DIST");
-    return e != nullptr && e[0] == '1' ? 1 : 2;
+    return e != nullptr && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 3;
   }();
+  if (dist == 3) {
+    static bool attr3 = false;
+    if (!attr3) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<1, 3>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<2, 3>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<4, 3>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+      attr3 = true;
+    }
+    switch (p->group) {
+      case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 3>), grid, dim3(128), 4 * kStage, st, *p); break;
+      case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 3>), grid, dim3(256), 4 * kStage, st, *p); break;
+      case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 3>), grid, dim3(512), 4 * kStage, st, *p); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (dist == 2) {
     switch (p->group) {
-      case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 2>), grid, dim3(128), 0, st, *p); break;
-      case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 2>), grid, dim3(256), 0, st, *p); break;
-      case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 2>), grid, dim3(512), 0, st, *p); break;
+      case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 2>), grid, dim3(128), 2 * kStage, st, *p); break;
+      case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 2>), grid, dim3(256), 2 * kStage, st, *p); break;
+      case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 2>), grid, dim3(512), 2 * kStage, st, *p); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (p->group) {
-    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 1>), grid, dim3(128), 0, st, *p); break;
-    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 1>), grid, dim3(256), 0, st, *p); break;
-    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 1>), grid, dim3(512), 0, st, *p); break;
+    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 1>), grid, dim3(128), 2 * kStage, st, *p); break;
+    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 1>), grid, dim3(256), 2 * kStage, st, *p); break;
+    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 1>), grid, dim3(512), 2 * kStage, st, *p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
