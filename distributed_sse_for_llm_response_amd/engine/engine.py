@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 import time
 from collections import deque
 from dataclasses import dataclass, field
@@ -114,14 +115,16 @@ class _Drain:
 class LLMEngine:
     def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 2048,
                  idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
-                 pipeline_depth: int = 1, max_pause_s: float = 30.0):
+                 pipeline_depth: int | None = None, max_pause_s: float = 30.0):
         self.r = runner
         self.eos_id = eos_id
         self.alloc = BlockAllocator(runner.kv.num_blocks)
         self.prefill_budget = prefill_budget
         self.idle_prefill_budget = idle_prefill_budget or runner.max_prefill_tokens
         self.default_params = default_params or SamplingParams()
-        self.depth = pipeline_depth
+        # decode steps kept enqueued ahead of the host's token processing: at 2 a host stall (GC, scheduling)
+        # of up to one step time is absorbed instead of idling the GPU; tokens surface one step later
+        self.depth = pipeline_depth if pipeline_depth is not None else int(os.environ.get("DSSE_PIPELINE_DEPTH", "2"))
         self.max_pause_s = max_pause_s
         self.waiting: deque = deque()
         self.slots: list = [None] * runner.max_batch
