@@ -43,8 +43,10 @@ SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgro
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
 # Largest decode bucket on the engine's own GEMMs (gemm_skinny / gemm_stream with fused epilogues); larger
 # buckets use hipBLASLt + separate RoPE / SiLU / norm kernels.  Measured per layer (qkv + o + gate_up + down,
-# profiles/gemm_mid_m_r1.md): 128 rows 156 vs 185 us, 192 rows 207 vs 236, 256 rows 241 vs 194.
-DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "192"))
+# profiles/gemm_mid_m_r1.md): 128 rows 156 vs 185 us, 192 rows 207 vs 236, 256 rows 241 vs 194.  End to end the
+# 192-row bucket is faster on the wide path (hipBLASLt o / gate_up + gemm_wide qkv / down): 192 streams 9.40 vs
+# 10.09 ms/step, 160 streams 8.56 vs 9.52; 128 rows stay here (7.01 vs 7.20) -- profiles/bucket_ab_r1.md.
+DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
 # Deferred RMSNorm scale on the TP=1 engine-GEMM decode path (rmsnorm(row_ss=) + GEMM epilogue scale).
 DEFERRED_NORM = os.environ.get("DSSE_DEFERRED_NORM", "0") == "1"  # measured slower (profiles/experiments_r1.md)
 
