@@ -29,21 +29,7 @@ struct GemmEpi {
   int nh, nkv;
   int num_slots;          // mode 4: KV slots in the cache (pages * kBS); checked build only
   int rope_len;           // mode 4: rows of the rope table; checked build only
-  // Deferred RMSNorm (dsse_rmsnorm_deferred): X rows are bf16(resid * gamma) and rowss[m * nss + g] the
-  // partial sums of squares of row m; every output of row m is scaled by rsqrt(sum / K + eps).
-  const float* rowss;     // nullptr = X already normalised
-  int nss;
-  float inv_k, eps;
 };
-
-// 1 / rms of row m for the deferred-norm input (rmsnorm mode 4), 1 when X is already normalised.
-DEV float row_scale(const GemmEpi& ep, int m) {
-  if (ep.rowss == nullptr) return 1.f;
-  const float* p = ep.rowss + (size_t)m * ep.nss;
-  float s = 0.f;
-  for (int i = 0; i < ep.nss; ++i) s += p[i];
-  return rsqrtf(s * ep.inv_k + ep.eps);
-}
 
 
 struct AttnParams {
@@ -65,6 +51,7 @@ struct AttnParams {
   int part;                 // keys per partition (multiple of 32 * KWV)
   int nparts;               // grid.z
   float scale_log2;         // log2(e) / sqrt(128)
+  int kwv;                  // decode: waves per workgroup splitting the keys (0 = by grid size)
 };
 
 struct SampleParams {
@@ -108,8 +95,6 @@ hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::Samp
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
                         const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
                         int vocab, hipStream_t st);
-hipError_t dsse_rmsnorm_deferred(int M, float* resid, int H, const void* w, void* y, const float* part, int nsplit,
-                                 float* ss, int G, hipStream_t st);
 hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                               const int* slots, const float2* rope, void* q_out, void* k_cache,
                               void* v_cache, int num_slots, int rope_len, hipStream_t st);

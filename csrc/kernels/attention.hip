@@ -264,29 +264,16 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
   if (mode == 0) {
-    // decode: DSSE_ATTN_KWV = waves per workgroup splitting the keys (4 / 8), DSSE_ATTN_PF = 0 / 1 next-page
-    // register prefetch (tools/bench_attn.py)
-    // Measured (profiles/attention_decode_r1.md): the prefetch costs 2-10 %; 4 key-split waves are best
-    // up to ~1k workgroups (64 streams x 8 kv heads: 29 us at 560 keys, 5.1 TB/s), one wave per
-    // (sequence, kv head) above (256 streams: 100 vs 109 us, 5.9 TB/s).
+    // decode: p->kwv (DSSE_ATTN_KWV, read by the bindings) = waves per workgroup splitting the keys (1/2/4/8).
+    // Measured (profiles/attention_decode_r1.md): 4 key-split waves are best up to ~1k workgroups (64 streams x
+    // 8 kv heads: 29 us at 560 keys, 5.1 TB/s), one wave per (sequence, kv head) above (256 streams: 100 vs
+    // 109 us, 5.9 TB/s).  (A next-page register prefetch variant cost 2-10 % and was removed.)
     const dim3 grid(num_work, p->hkv, p->nparts);
-    const char* e1 = getenv("DSSE_ATTN_KWV");
-    const char* e2 = getenv("DSSE_ATTN_PF");
-    const int kwv = e1 ? atoi(e1) : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
-    const bool pf = e2 ? atoi(e2) != 0 : false;
-    if (kwv == 8) {
-      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 8, true>), grid, dim3(512), 0, st, *p);
-      else hipLaunchKernelGGL((paged_attention_kernel<1, 8, false>), grid, dim3(512), 0, st, *p);
-    } else if (kwv == 1) {
-      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 1, true>), grid, dim3(64), 0, st, *p);
-      else hipLaunchKernelGGL((paged_attention_kernel<1, 1, false>), grid, dim3(64), 0, st, *p);
-    } else if (kwv == 2) {
-      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 2, true>), grid, dim3(128), 0, st, *p);
-      else hipLaunchKernelGGL((paged_attention_kernel<1, 2, false>), grid, dim3(128), 0, st, *p);
-    } else {
-      if (pf) hipLaunchKernelGGL((paged_attention_kernel<1, 4, true>), grid, dim3(256), 0, st, *p);
-      else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false>), grid, dim3(256), 0, st, *p);
-    }
+    const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
+    if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false>), grid, dim3(512), 0, st, *p);
+    else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false>), grid, dim3(64), 0, st, *p);
+    else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false>), grid, dim3(128), 0, st, *p);
+    else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false>), grid, dim3(256), 0, st, *p);
     if (p->nparts > 1)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else {

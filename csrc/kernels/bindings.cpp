@@ -8,8 +8,11 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "api.h"
 
@@ -33,10 +36,25 @@ void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
 }
 
+// Tuning knobs (DSSE_* environment variables) are read once and cached: no getenv on the launch path.
+// refresh_env() (op dsse::refresh_env) re-reads them, for the tuning tools that change them in-process.
+std::mutex g_env_mu;
+std::unordered_map<std::string, int> g_env;
 int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
+  std::lock_guard<std::mutex> lk(g_env_mu);
+  auto it = g_env.find(name);
+  if (it == g_env.end()) {
+    const char* v = std::getenv(name);
+    it = g_env.emplace(name, v ? std::atoi(v) : INT32_MIN).first;
+  }
+  return it->second == INT32_MIN ? dflt : it->second;
 }
+void refresh_env() {
+  std::lock_guard<std::mutex> lk(g_env_mu);
+  g_env.clear();
+}
+
+
 
 // Tile selection for the skinny GEMM.  NT = output tiles per wave, KW = waves splitting K.
 // Defaults come from the gfx950 sweep in tools/tune_gemm.py; DSSE_GEMM_NT / DSSE_GEMM_KW override.
@@ -116,33 +134,19 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
   if (c.nt == 2 || c.rd != 2 || M > 64 || (c.nw != 4 && c.nw != 8)) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
   if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
-  // half-width X slices (64 KiB of LDS: two workgroups per CU) for 33-64 rows, flagged as rd = 16 + 2
-  const bool half = c.mt == 4 && c.nt == 1 && M <= 64 && (c.nw == 4 || c.nw == 8 || c.nw == 2) &&
-                    env_int("DSSE_S_HALF", 0) == 1;
-  if (half) c.rd = 18;
-  // in-workgroup split-K by two (KS2, flagged as rd = 32 + 2): the two K halves meet in LDS, no slabs
-  // Opt-in (DSSE_S_KS2=1; DSSE_S_KS2=2 = only the QKV + RoPE projection, with S = 1): measured slower in situ
-  // for QKV at 64 rows (4.86 vs 4.73 ms per decode step, profiles/experiments_r1.md) although it removes the
-  // split-K reduce launch.
-  const int ks2_env = env_int("DSSE_S_KS2", 0);
-  const bool ks2 = !half && c.mt == 4 && c.nt == 1 && M <= 64 && (c.nw == 4 || c.nw == 8) &&
-                   (ks2_env == 1 || (ks2_env == 2 && mode == dsse::kQkvRope && c.nw == 4));
-  if (ks2) c.rd = 34;
-  const int cps = c.mt <= 4 ? ((half || ks2) ? 2 : 4) : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
-  const int kdiv = ks2 ? 2 : 1, tgw = ks2 ? c.nw / 2 : c.nw;
-  c.ok = K % (128 * cps * kdiv) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % tgw == 0;
+  const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
+  c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
-  const int wgs = N / (16 * c.nt) / tgw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps * kdiv);
-  const int per_cu = half ? 2 : 1;
-  int S = env_int("DSSE_S_SPLIT", (ks2 && ks2_env == 2) ? 1 : 0);
+  const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
+  int S = env_int("DSSE_S_SPLIT", 0);
   if (S <= 0 || slices % S != 0) {
-    // smallest split that gives ~one workgroup per CU slot (256 CUs x per_cu), never more than 1.25x that
+    // smallest split that gives ~one workgroup per CU (256 CUs), never more than 1.25x that
     S = 1;
     for (int d = 1; d <= slices; ++d) {
       if (slices % d) continue;
-      if (wgs * d > 320 * per_cu) break;
+      if (wgs * d > 320) break;
       S = d;
-      if (wgs * d >= 192 * per_cu) break;
+      if (wgs * d >= 192) break;
     }
   }
   c.S = S;
@@ -213,6 +217,7 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(M >= 1 && M <= kMaxDecodeM, "decode GEMM supports 1 <= M <= ", kMaxDecodeM, ", got ", M);
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
+  TORCH_CHECK((int64_t)N * K * 2 < (1LL << 31), "weight larger than 2 GiB: the decode GEMMs address it with 32-bit offsets");
   const int impl = gemm_impl(M, N, K);
   TORCH_CHECK(M <= 64 || impl >= 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
   if (impl == 3) {
@@ -246,20 +251,7 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
                                   cur_stream()));
 }
 
-// Deferred-norm input (rmsnorm with row_ss): scale row m of the product by rsqrt(sum(row_ss[m]) / K + eps).
-void set_rowss(dsse::GemmEpi& ep, const c10::optional<Tensor>& row_ss, const Tensor& x, double eps) {
-  if (!row_ss.has_value()) return;
-  check_gpu(*row_ss, "row_ss");
-  check_dtype(*row_ss, at::kFloat, "row_ss");
-  TORCH_CHECK(row_ss->dim() == 2 && row_ss->size(0) >= x.size(0) && row_ss->is_contiguous(),
-              "row_ss must be a contiguous [>= M, G] fp32 tensor");
-  ep.rowss = row_ss->data_ptr<float>();
-  ep.nss = (int)row_ss->size(1);
-  ep.inv_k = 1.f / (float)x.size(1);
-  ep.eps = (float)eps;
-}
-
-void gemm_out(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& row_ss, double eps) {
+void gemm_out(const Tensor& x, const Tensor& w, Tensor& out) {
   check_gpu(out, "out");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) == w.size(0),
               "out must be [M, N]");
@@ -270,7 +262,6 @@ void gemm_out(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional
   if (out.scalar_type() == at::kBFloat16) mode = dsse::kStoreBf16;
   else if (out.scalar_type() == at::kFloat) mode = dsse::kStoreF32;
   else TORCH_CHECK(false, "out must be bf16 or fp32");
-  set_rowss(ep, row_ss, x, eps);
   run_gemm(mode, x, w, ep);
 }
 
@@ -332,7 +323,7 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   return 0;
 }
 
-void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out, const c10::optional<Tensor>& row_ss, double eps) {
+void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out) {
   check_gpu(out, "out");
   check_dtype(out, at::kBFloat16, "out");
   TORCH_CHECK(out.dim() == 2 && out.size(0) == x.size(0) && out.size(1) * 2 == w.size(0),
@@ -340,13 +331,12 @@ void gemm_silu(const Tensor& x, const Tensor& w, Tensor& out, const c10::optiona
   dsse::GemmEpi ep{};
   ep.out = out.data_ptr();
   ep.ldo = (int)out.size(1);
-  set_rowss(ep, row_ss, x, eps);
   run_gemm(dsse::kSiluMul, x, w, ep);
 }
 
 void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
                    const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
-                   int64_t nkv, const c10::optional<Tensor>& row_ss, double eps) {
+                   int64_t nkv) {
   for (auto* t : {&positions, &slots, &rope}) check_gpu(*t, "metadata");
   check_gpu(q_out, "q_out");
   check_gpu(k_cache, "k_cache");
@@ -374,13 +364,12 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
   ep.nkv = (int)nkv;
   ep.num_slots = (int)(k_cache.size(0) * dsse::kBS);
   ep.rope_len = (int)rope.size(0);
-  set_rowss(ep, row_ss, x, eps);
   run_gemm(dsse::kQkvRope, x, w, ep);
 }
 
 void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
              const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids,
-             const c10::optional<Tensor>& part, int64_t nsplit, const c10::optional<Tensor>& row_ss) {
+             const c10::optional<Tensor>& part, int64_t nsplit) {
   check_gpu(resid, "resid");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -411,26 +400,6 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     TORCH_CHECK(delta->size(0) >= M && delta->size(1) == H, "delta shape mismatch");
     mode = 1;
     dptr = delta->data_ptr();
-  }
-  if (row_ss.has_value()) {  // deferred norm: split-K slabs (or nothing) added, scale left to the GEMM
-    TORCH_CHECK(mode == 0, "row_ss (deferred norm) takes no delta / embed");
-    check_gpu(*row_ss, "row_ss");
-    check_dtype(*row_ss, at::kFloat, "row_ss");
-    const int G = (int)row_ss->size(1);
-    TORCH_CHECK(row_ss->dim() == 2 && row_ss->size(0) >= M && row_ss->is_contiguous() && G > 0 && H % (4 * G) == 0 &&
-                    (H / (4 * G)) % 64 == 0 && H / (4 * G) <= 1024,
-                "row_ss must be [>= M, G] with H / (4 G) a multiple of 64 threads, <= 1024");
-    const float* pp = nullptr;
-    if (nsplit > 0) {
-      TORCH_CHECK(part.has_value(), "nsplit > 0 needs part");
-      check_gpu(*part, "part");
-      check_dtype(*part, at::kFloat, "part");
-      TORCH_CHECK(part->numel() >= nsplit * M * H, "part too small for ", nsplit, " slabs");
-      pp = part->data_ptr<float>();
-    }
-    DSSE_CHECK_HIP(dsse_rmsnorm_deferred(M, resid.data_ptr<float>(), H, w.data_ptr(), y.data_ptr(), pp, (int)nsplit,
-                                         row_ss->data_ptr<float>(), G, cur_stream()));
-    return;
   }
   const float* pptr = nullptr;
   if (part.has_value() && nsplit > 0 && mode == 0) {
@@ -541,6 +510,10 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   p.part = (int)part;
   p.nparts = (int)nparts;
   p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
+  {
+    const int kwv = env_int("DSSE_ATTN_KWV", 0);
+    p.kwv = (kwv == 1 || kwv == 2 || kwv == 4 || kwv == 8) ? kwv : 0;
+  }
   if (mode == 2) DSSE_CHECK_HIP(dsse_flash_prefill(num_work, &p, cur_stream()));
   else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
 }
@@ -658,14 +631,15 @@ std::string kernel_check_files() {
 }  // namespace
 
 TORCH_LIBRARY(dsse, m) {
-  m.def("gemm_out(Tensor x, Tensor w, Tensor(a!) out, Tensor? row_ss=None, float eps=0.0) -> ()");
+  m.def("gemm_out(Tensor x, Tensor w, Tensor(a!) out) -> ()");
   m.def("gemm_resid(Tensor x, Tensor w, Tensor(a!) resid) -> ()");
-  m.def("gemm_silu(Tensor x, Tensor w, Tensor(a!) out, Tensor? row_ss=None, float eps=0.0) -> ()");
+  m.def("gemm_silu(Tensor x, Tensor w, Tensor(a!) out) -> ()");
   m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
-        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor? row_ss=None, float eps=0.0) -> ()");
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
-        "Tensor? ids=None, Tensor? part=None, int nsplit=0, Tensor(c!)? row_ss=None) -> ()");
+        "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
   m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
+  m.def("refresh_env() -> ()", &refresh_env);
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("silu_mul(Tensor gu, Tensor(a!) h) -> ()");

@@ -39,6 +39,18 @@ DEV bf16x8 zero_bf16x8() {
   return z;
 }
 
+// Buffer descriptor over [base, base + bytes) (wave-uniform inputs): raw buffer loads past `bytes` return zeros
+// without touching memory, so a prefetch ring can run past the end of its range for free.
+constexpr int kAuxNT = 2;  // buffer-load cache policy bits: non-temporal (streamed-once data)
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <int AUX>
+DEV bf16x8 ld_buf_bf16x8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
+}
+
+
 // Non-temporal 16-byte load for once-read streams (weights, KV pages).
 DEV bf16x8 ld_nt_bf16x8(const bf16* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));

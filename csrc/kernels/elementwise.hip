@@ -90,54 +90,6 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
   }
 }
 
-// ---- K2, deferred: residual add + split-K reduction with the norm scale left to the consumer ----------
-// resid[m] += sum_s part[s, m] (S may be 0); y[m] = bf16(resid[m] * w); ss[m, g] = sum of squares of chunk g.
-// The consuming decode GEMM multiplies row m of its product by rsqrt(sum_g ss[m, g] / H + eps)
-// (GemmEpi::rowss), so no workgroup needs the whole row: grid (G, M), H / G columns per workgroup, one
-// float4 per thread -- every CU gets work at M = 64 instead of one workgroup per row.
-__global__ void __launch_bounds__(1024)
-rmsnorm_deferred_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ w, bf16* __restrict__ y,
-                        const float* __restrict__ part, int nsplit, int M, float* __restrict__ ss) {
-  const int g = blockIdx.x, m = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
-  const int i = (g * nt + tid) * 4;
-  float* rp = resid + (size_t)m * H + i;
-  float4 x = *reinterpret_cast<const float4*>(rp);
-  const float* p = part + (size_t)m * H + i;
-  const size_t slab = (size_t)M * H;
-  int s = 0;
-  for (; s + 4 <= nsplit; s += 4) {
-    const float4 d0 = *reinterpret_cast<const float4*>(p + (s + 0) * slab);
-    const float4 d1 = *reinterpret_cast<const float4*>(p + (s + 1) * slab);
-    const float4 d2 = *reinterpret_cast<const float4*>(p + (s + 2) * slab);
-    const float4 d3 = *reinterpret_cast<const float4*>(p + (s + 3) * slab);
-    x.x += (d0.x + d1.x) + (d2.x + d3.x);
-    x.y += (d0.y + d1.y) + (d2.y + d3.y);
-    x.z += (d0.z + d1.z) + (d2.z + d3.z);
-    x.w += (d0.w + d1.w) + (d2.w + d3.w);
-  }
-  for (; s < nsplit; ++s) {
-    const float4 d = *reinterpret_cast<const float4*>(p + s * slab);
-    x.x += d.x; x.y += d.y; x.z += d.z; x.w += d.w;
-  }
-  if (nsplit > 0) *reinterpret_cast<float4*>(rp) = x;
-  const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + i);
-  bf16x4 o;
-  o[0] = f2bf(x.x * bf2f(wv[0]));
-  o[1] = f2bf(x.y * bf2f(wv[1]));
-  o[2] = f2bf(x.z * bf2f(wv[2]));
-  o[3] = f2bf(x.w * bf2f(wv[3]));
-  *reinterpret_cast<bf16x4*>(y + (size_t)m * H + i) = o;
-  float q = wave_sum(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
-  __shared__ float red[16];
-  if ((tid & 63) == 0) red[tid >> 6] = q;
-  __syncthreads();
-  if (tid == 0) {
-    float tot = 0.f;
-    for (int k = 0; k < (nt >> 6); ++k) tot += red[k];
-    ss[(size_t)m * gridDim.x + g] = tot;
-  }
-}
-
 // ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
 // qkv: [T, (hq + 2 hkv) * 128] bf16 in the engine's permuted column order (inside each 16-column
 // tile j of a head: columns 0..7 = dims 8j..8j+7, columns 8..15 = dims 64+8j..64+8j+7).
@@ -247,15 +199,6 @@ extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const v
     case 3: hipLaunchKernelGGL(rmsnorm_kernel<3>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-extern "C" hipError_t dsse_rmsnorm_deferred(int M, float* resid, int H, const void* w, void* y, const float* part,
-                                            int nsplit, float* ss, int G, hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  const int nt = H / (4 * G);  // host-checked: H % (4 G) == 0, nt % 64 == 0, nt <= 1024
-  hipLaunchKernelGGL(rmsnorm_deferred_kernel, dim3(G, M), dim3(nt), 0, st, resid, H, reinterpret_cast<const bf16*>(w),
-                     reinterpret_cast<bf16*>(y), part, nsplit, M, ss);
   return hipGetLastError();
 }
 

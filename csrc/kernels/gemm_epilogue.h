@@ -13,11 +13,6 @@ DEV int vperm_tok(int off) { return ((off & 15) >> 2) * 8 + ((off >> 4) & 1) * 4
 template <int MODE>
 DEV void epilogue(const GemmEpi& ep, float* part, int M, int N, int m, int tile, int r, float v, float partner) {
   if (m >= M) return;
-  if constexpr (MODE != kPartial) {  // split-K slabs stay unscaled; their reduction applies it once
-    const float sc = row_scale(ep, m);
-    v *= sc;
-    partner *= sc;
-  }
   const int n = tile * 16 + r;
   if constexpr (MODE == kStoreBf16) {
     reinterpret_cast<bf16*>(ep.out)[(size_t)m * ep.ldo + n] = f2bf(v);

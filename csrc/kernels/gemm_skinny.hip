@@ -123,7 +123,7 @@ skinny_gemm_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = 16 * mt + 4 * g + i;
-        const float v = acc[mt][t][i] * (m < M ? row_scale(ep, m) : 1.f);
+        const float v = acc[mt][t][i];
         if constexpr (MODE == kStoreBf16) {
           if (m < M) reinterpret_cast<bf16*>(ep.out)[(size_t)m * ep.ldo + n] = f2bf(v);
         } else if constexpr (MODE == kStoreF32) {

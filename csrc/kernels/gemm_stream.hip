@@ -42,22 +42,17 @@ constexpr int stream_cps(int mt) { return mt <= 4 ? 4 : (mt <= 8 ? 2 : 1); }
 // blocks of 64) and workgroups are renumbered so that the MB row blocks of one tile group are consecutive
 // on the same XCD: they stream the same weight bytes at about the same time, so HBM serves them once and
 // the XCD's L2 the other MB-1 times.  That sharing needs temporal (cached) weight loads (SHARED_W).
-// KS2: in-workgroup split-K by two — waves [0, NW/2) and [NW/2, NW) stream the two K halves of the same NW/2
-// tile groups (each half with its own half-width X slices) and meet in LDS at the end, so a narrow projection
-// gets split-K parallelism without fp32 slabs or a reduce launch (the QKV + RoPE epilogue runs in place).
-template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false, bool HALF = false, bool KS2 = false>
+
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N,
                    int Kr, GemmEpi ep, float* __restrict__ part) {
-  // HALF: X slices of half the columns (64 KiB of LDS for 64 rows): two workgroups fit on a CU
-  constexpr int CPS = (HALF || KS2) ? stream_cps(MT) / 2 : stream_cps(MT);
+  constexpr int CPS = stream_cps(MT);
   constexpr int MP = 16 * MT;
   constexpr int ROWB = CPS * 256;                        // bytes of one X row in a slice
   constexpr int BUF = MP * ROWB;                         // bytes per slice buffer
-  constexpr int XH = KS2 ? 2 : 1;                        // K halves staged per slice
-  constexpr int TG_W = KS2 ? NW / 2 : NW;                // tile groups per workgroup
-  constexpr int PPH = MP * CPS * 16;                     // 16-byte pieces per half per slice
-  constexpr int PPT = (XH * PPH + 64 * NW - 1) / (64 * NW);  // 16-byte pieces per thread
+  constexpr int PPH = MP * CPS * 16;                     // 16-byte pieces per slice
+  constexpr int PPT = (PPH + 64 * NW - 1) / (64 * NW);   // 16-byte pieces per thread
   constexpr int XG = MT * NT <= 4 ? 4 : 2;  // k-steps whose X fragments are read at once (MT * NT <= 8)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -82,42 +77,46 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
     wg = slot * per + xcd % per;
   }
   const int m0 = rb * MP;     // first row of this workgroup's row block
-  const int half = KS2 ? w / TG_W : 0;
-  const int tgi = wg * TG_W + (KS2 ? w % TG_W : w);  // host guarantees N / (16 NT) % TG_W == 0
-  const int kx = ks * Kr;                             // this workgroup's K range
-  const int k0 = kx + half * (KS2 ? Kr / 2 : 0);      // this wave's
-  const int nch = (KS2 ? Kr / 2 : Kr) >> 7;  // multiple of CPS (host-checked)
+  const int tgi = wg * NW + w;  // host guarantees N / (16 NT) % NW == 0
+  const int k0 = ks * Kr;       // this workgroup's K range
+  const int nch = Kr >> 7;      // multiple of CPS (host-checked)
   const int nsl = nch / CPS;
   const int npieces = min(M - m0, MP) * CPS * 16;
   const int KC = K >> 7;
 
-  const bf16* wbase = W + ((size_t)tgi * NT * KC + (k0 >> 7)) * kTileChunk + lane * 8;
+  // Weight stream through one buffer descriptor per tile covering exactly this wave's K range: the ring's
+  // look-ahead loads past the range (its last DEPTH-1 issues) fail the descriptor's range check and cost no
+  // memory traffic.  Clamping them to the last chunk instead re-fetched up to DEPTH-1 chunks per wave: +37 %
+  // bytes for a split-K O projection with 8 chunks per wave, +9 % for gate_up.
+  const int tgu = __builtin_amdgcn_readfirstlane(tgi), k0u = __builtin_amdgcn_readfirstlane(k0);
+  __amdgpu_buffer_rsrc_t wrs[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    wrs[t] = make_rsrc(W + ((size_t)(tgu * NT + t) * KC + (k0u >> 7)) * kTileChunk, (uint32_t)nch * kTileChunk * 2);
+  constexpr int WAUX = (SHARED_W || DSSE_W_DEFAULT) ? 0 : kAuxNT;
   auto load_w = [&](int c, bf16x8 (&wf)[NT][4]) {
-    const bf16* p = wbase + (size_t)min(c, nch - 1) * kTileChunk;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        wf[t][s] = (SHARED_W || DSSE_W_DEFAULT) ? ld_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s)
-                            : ld_nt_bf16x8(p + (size_t)t * KC * kTileChunk + 512 * s);
+      for (int s = 0; s < 4; ++s) wf[t][s] = ld_buf_bf16x8<WAUX>(wrs[t], (uint32_t)c * (kTileChunk * 2) + 1024 * s + lane * 16);
   };
 
   bf16x8 xs[PPT];
   auto load_x = [&](int sl) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int idx = threadIdx.x + i * 64 * NW, hh = KS2 ? idx / PPH : 0, pi = KS2 ? idx % PPH : idx;
-      const bf16* src = X + kx + hh * (Kr / 2) + sl * (CPS * 128);
-      if (idx < XH * PPH && pi < npieces)
+      const int pi = threadIdx.x + i * 64 * NW;
+      const bf16* src = X + k0 + sl * (CPS * 128);
+      if (pi < PPH && pi < npieces)
         xs[i] = ld_bf16x8(src + (size_t)(pi / (CPS * 16)) * ldx + 8 * (pi % (CPS * 16)));
     }
   };
   auto store_x = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int idx = threadIdx.x + i * 64 * NW, hh = KS2 ? idx / PPH : 0, pi = KS2 ? idx % PPH : idx;
-      char* dst = smem + (hh * 2 + buf) * BUF;
-      if (idx < XH * PPH && pi < npieces) {
+      const int pi = threadIdx.x + i * 64 * NW;
+      char* dst = smem + buf * BUF;
+      if (pi < PPH && pi < npieces) {
         const int row = pi / (CPS * 16), c = pi % (CPS * 16);
         *reinterpret_cast<bf16x8*>(dst + row * ROWB + ((c >> 4) << 8) + (((c & 15) ^ swz(row & 15)) << 4)) = xs[i];
       }
@@ -130,7 +129,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
   // that never executes (M >= 0), so the loads stay.
   // Only for the wide-N launches (7-8 waves, no split-K: gate_up, LM head): the split-K narrow projections,
   // with 2-7 slices per workgroup, measured slower with it (+140 us per 64-stream step).
-  constexpr bool TOUCH = DSSE_X_TOUCH && NW >= 7 && !KS2;
+  constexpr bool TOUCH = DSSE_X_TOUCH && NW >= 7;
   constexpr int LPR = CPS * 2;                 // 128-B lines per X row of a slice
   constexpr int TOUCH_PT = (MP * LPR + 64 * NW - 1) / (64 * NW);
   const int touch_last_row = min(M - m0, MP) - 1;
@@ -169,7 +168,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       const bool more = sl + 1 < nsl;
       if (TOUCH) touch_x(min(sl + 2, nsl - 1));
       if (more) load_x(sl + 1);
-      const char* xb0 = smem + (half * 2 + (sl & 1)) * BUF;
+      const char* xb0 = smem + (sl & 1) * BUF;
 #pragma unroll
       for (int d = 0; d < CPS; ++d) {
         const int slot = h * CPS + d;
@@ -216,27 +215,6 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 
   if (TOUCH && M < 0) part[touch & 1] = (float)touch;  // never runs: keeps the warm-up loads
 
-  if constexpr (KS2) {  // the upper K half hands its accumulators to the lower one through LDS
-    __syncthreads();    // every wave is done with the X slices
-    float* red = reinterpret_cast<float*>(smem) + (size_t)(w % TG_W) * MT * NT * 4 * 64;
-    if (half == 1) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) red[((mt * NT + t) * 4 + i) * 64 + lane] = acc[mt][t][i];
-    }
-    __syncthreads();
-    if (half == 1) return;  // no barrier below
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[mt][t][i] += red[((mt * NT + t) * 4 + i) * 64 + lane];
-  }
-
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -250,38 +228,30 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
       }
 }
 
-template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false, bool HALF = false, bool KS2 = false>
+// LDS bytes of a gemm_stream launch: the two X slice buffers
+constexpr size_t stream_lds(int mt) { return (size_t)2 * 16 * mt * stream_cps(mt) * 256; }
+
+template <int MT, int NT, int NW, int RD, int MODE, bool SHARED_W = false>
 static hipError_t launch_s(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
   const int TG = N / (16 * NT);
   const int MB = SHARED_W ? (M + 16 * MT - 1) / (16 * MT) : 1;
-  const size_t lds = (size_t)2 * (KS2 ? 2 : 1) * 16 * MT * ((HALF || KS2) ? stream_cps(MT) / 2 : stream_cps(MT)) * 256;
+  const size_t lds = stream_lds(MT);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W, HALF, KS2>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  dim3 grid(TG / (KS2 ? NW / 2 : NW) * MB, S), block(64 * NW);
-  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W, HALF, KS2>), grid, block, lds, st, X, ldx, M, W,
-                     K, N, K / S, ep, part);
+  dim3 grid(TG / NW * MB, S), block(64 * NW);
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, NT, NW, RD, MODE, SHARED_W>), grid, block, lds, st, X, ldx, M, W, K, N,
+                     K / S, ep, part);
   return hipGetLastError();
 }
 
 template <int MODE>
 static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, int ldx, int M, const bf16* W, int K, int N,
                                 int S, const GemmEpi& ep, float* part, hipStream_t st) {
-  if (rd >= 32) {  // rd = 32 + ring slices: in-workgroup split-K by two (KS2), mt 4 only
-    if (mt == 4 && nt == 1 && nw == 8 && rd == 34) return launch_s<4, 1, 8, 2, MODE, false, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
-    if (mt == 4 && nt == 1 && nw == 4 && rd == 34) return launch_s<4, 1, 4, 2, MODE, false, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
-    return hipErrorInvalidValue;
-  }
-  if (rd >= 16) {  // rd = 16 + ring slices: HALF-width X slices (two workgroups per CU), mt 4 only
-    if (mt == 4 && nt == 1 && nw == 4 && rd == 18) return launch_s<4, 1, 4, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
-    if (mt == 4 && nt == 1 && nw == 8 && rd == 18) return launch_s<4, 1, 8, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
-    if (mt == 4 && nt == 1 && nw == 2 && rd == 18) return launch_s<4, 1, 2, 2, MODE, false, true>(X, ldx, M, W, K, N, S, ep, part, st);
-    return hipErrorInvalidValue;
-  }
   if (M > 16 * mt) {  // row blocks with L2-shared weights (64-row MFMA tiles, one or eight waves)
     if (mt == 4 && nt == 1 && nw == 4) return launch_s<4, 1, 4, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);
     if (mt == 4 && nt == 1 && nw == 8) return launch_s<4, 1, 8, 1, MODE, true>(X, ldx, M, W, K, N, S, ep, part, st);

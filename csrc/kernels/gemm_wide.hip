@@ -59,11 +59,14 @@ gemm_wide_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   const int nsl = nch / CPS;
   const int KC = K >> 7;
 
-  const bf16* wbase = W + ((size_t)(2 * strip + (n32 >> 4)) * KC + (k0 >> 7)) * kTileChunk + (n32 & 15) * 8;
+  // One range-checked descriptor over all of W: the ring's look-ahead issues past this wave's K range get an
+  // out-of-range offset and return zeros without memory traffic (clamping them re-fetched the last chunk).
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(W, (uint32_t)((size_t)N * K * 2));
+  const uint32_t wbase = (uint32_t)((((size_t)(2 * strip + (n32 >> 4)) * KC + (k0 >> 7)) * kTileChunk + (n32 & 15) * 8) * 2);
   auto load_w = [&](int c, bf16x8 (&wf)[8]) {
-    const bf16* p = wbase + (size_t)min(c, nch - 1) * kTileChunk;
+    const uint32_t p = c < nch ? wbase + (uint32_t)c * (kTileChunk * 2) : 0xFFFFF000u;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) wf[q] = ld_nt_bf16x8(p + ((q & 3) * 64 + 16 * (2 * (q >> 2) + h)) * 8);
+    for (int q = 0; q < 8; ++q) wf[q] = ld_buf_bf16x8<kAuxNT>(wrs, p + ((q & 3) * 64 + 16 * (2 * (q >> 2) + h)) * 16);
   };
 
   // X pieces: every thread loads PPT pieces unconditionally (rows past M re-read row M - 1; those LDS rows

@@ -24,6 +24,8 @@ FramePtr Bus::make_frame(const TokenMessage& m) {
   f->seq = m.sequence;
   f->done = m.done;
   f->timestamp = m.timestamp;
+  f->finish = m.finish;
+  f->prompt_tokens = m.prompt_tokens;
   f->json.reserve(112 + m.conversation_id.size() + m.token.size());
   encode_token_message(f->json, m);
   char head[48];

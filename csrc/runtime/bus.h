@@ -34,6 +34,8 @@ struct Frame {
   int64_t seq = 0;
   bool done = false;
   int64_t timestamp = 0;
+  uint8_t finish = kFinishNone;  // TokenMessage::finish
+  int32_t prompt_tokens = -1;
 };
 using FramePtr = std::shared_ptr<const Frame>;
 

@@ -252,6 +252,8 @@ void DpRouter::handle_tokens(int w, dpwire::Reader& rd) {
     m.sequence = rd.i64();
     m.done = rd.u8() != 0;
     std::string text = rd.str();
+    m.finish = rd.u8();
+    m.prompt_tokens = rd.i32();
     if (!text.empty()) m.token = std::move(text);
     else if (tok >= 0 && (size_t)tok < vocab->size()) m.token = (*vocab)[(size_t)tok];
     else m.token = "<" + std::to_string(tok) + ">";
@@ -364,7 +366,8 @@ std::vector<ChatRequest> DpWorker::poll(size_t max, int timeout_ms, std::vector<
 
 bool DpWorker::publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
                               const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
-                              const std::vector<std::string>& texts) {
+                              const std::vector<std::string>& texts, const std::vector<int>& finish,
+                              const std::vector<int>& prompt_tokens) {
   const size_t n = conv_ids.size();
   dpwire::Writer m;
   m.u8(dpwire::kTokens);
@@ -377,6 +380,8 @@ bool DpWorker::publish_tokens(const std::vector<std::string>& conv_ids, const st
     m.i64(seqs[i]);
     m.u8(dones[i] ? 1 : 0);
     m.str(i < texts.size() ? texts[i] : empty);
+    m.u8(i < finish.size() ? (uint8_t)finish[i] : 0);
+    m.i32(i < prompt_tokens.size() ? prompt_tokens[i] : -1);
   }
   return send(m.data());
 }

@@ -147,7 +147,8 @@ class DpWorker {
                                 std::vector<std::pair<std::string, bool>>* flow = nullptr);
   bool publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
                       const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
-                      const std::vector<std::string>& texts);
+                      const std::vector<std::string>& texts, const std::vector<int>& finish = {},
+                      const std::vector<int>& prompt_tokens = {});
   void hello();
   void bye();
   void stats(double step_s, double batch, double kv_free, double active, const std::vector<double>& ttft,

@@ -15,12 +15,18 @@
 
 namespace dsse {
 
+// Engine finish reason of a terminal message (not part of the wire JSON: it rides along in the Frame so the
+// OpenAI surface can report vLLM's finish_reason / usage).
+enum FinishReason : uint8_t { kFinishNone = 0, kFinishStop = 1, kFinishLength = 2, kFinishAbort = 3 };
+
 struct TokenMessage {
   std::string conversation_id;
   std::string token;
   int64_t sequence = 0;
   bool done = false;
   int64_t timestamp = 0;
+  uint8_t finish = kFinishNone;  // terminal messages from the engine
+  int32_t prompt_tokens = -1;    // terminal messages from the engine: prompt length (-1 = unknown)
 };
 
 // Append a JSON string literal (with quotes) using Go json.Marshal escaping rules.

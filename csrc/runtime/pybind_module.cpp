@@ -147,7 +147,8 @@ class Runtime {
   // comes from the vocabulary; `texts` (optional) overrides per entry (e.g. "[DONE]", "[ERROR]").
   int publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
                      const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
-                     const std::vector<std::string>& texts) {
+                     const std::vector<std::string>& texts, const std::vector<int>& finish,
+                     const std::vector<int>& prompt_tokens) {
     const size_t n = conv_ids.size();
     if (token_ids.size() != n || seqs.size() != n || dones.size() != n)
       throw std::invalid_argument("publish_tokens: length mismatch");
@@ -165,6 +166,8 @@ class Runtime {
         m.sequence = seqs[i];
         m.done = dones[i];
         m.timestamp = t;
+        m.finish = i < finish.size() ? (uint8_t)finish[i] : kFinishNone;
+        m.prompt_tokens = i < prompt_tokens.size() ? prompt_tokens[i] : -1;
         frames.push_back(Bus::make_frame(m));
       }
       bus_->publish_batch(frames);
@@ -236,12 +239,13 @@ class DpWorkerPy {
   bool shutdown_requested() const { return shutdown_; }
   int publish_tokens(const std::vector<std::string>& conv_ids, const std::vector<int>& token_ids,
                      const std::vector<int64_t>& seqs, const std::vector<bool>& dones, int64_t ts,
-                     const std::vector<std::string>& texts) {
+                     const std::vector<std::string>& texts, const std::vector<int>& finish,
+                     const std::vector<int>& prompt_tokens) {
     const size_t n = conv_ids.size();
     if (token_ids.size() != n || seqs.size() != n || dones.size() != n)
       throw std::invalid_argument("publish_tokens: length mismatch");
     py::gil_scoped_release nogil;
-    if (!w_->publish_tokens(conv_ids, token_ids, seqs, dones, ts, texts))
+    if (!w_->publish_tokens(conv_ids, token_ids, seqs, dones, ts, texts, finish, prompt_tokens))
       throw std::runtime_error("dp worker: token ring closed or full");
     return (int)n;
   }
@@ -278,7 +282,8 @@ PYBIND11_MODULE(_dsse_runtime, m) {
       .def("set_vocab", &Runtime::set_vocab)
       .def("publish_tokens", &Runtime::publish_tokens, py::arg("conversation_ids"), py::arg("token_ids"),
            py::arg("sequences"), py::arg("dones"), py::arg("timestamp_ns") = 0,
-           py::arg("texts") = std::vector<std::string>{})
+           py::arg("texts") = std::vector<std::string>{}, py::arg("finish") = std::vector<int>{},
+           py::arg("prompt_tokens") = std::vector<int>{})
       .def("publish", &Runtime::publish, py::arg("conversation_id"), py::arg("token"), py::arg("sequence"),
            py::arg("done") = false, py::arg("timestamp_ns") = 0)
       .def("pop_cancellations", &Runtime::pop_cancellations)
@@ -303,7 +308,8 @@ PYBIND11_MODULE(_dsse_runtime, m) {
       .def("shutdown_requested", &DpWorkerPy::shutdown_requested)
       .def("publish_tokens", &DpWorkerPy::publish_tokens, py::arg("conversation_ids"), py::arg("token_ids"),
            py::arg("sequences"), py::arg("dones"), py::arg("timestamp_ns") = 0,
-           py::arg("texts") = std::vector<std::string>{})
+           py::arg("texts") = std::vector<std::string>{}, py::arg("finish") = std::vector<int>{},
+           py::arg("prompt_tokens") = std::vector<int>{})
       .def("set_ready", &DpWorkerPy::set_ready)
       .def("observe", &DpWorkerPy::observe)
       .def("set_vocab", &DpWorkerPy::set_vocab);

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cmath>
 #include <cstring>
 #include <ctime>
 #include <map>
@@ -375,7 +376,7 @@ class IoThread {
   void deliver_token(Conn& c, const FramePtr& f);
   void handle_openai(Conn& c, HttpRequest& req);
   void deliver_openai(Conn& c, const FramePtr& f);
-  void finish_openai(Conn& c, const char* finish_reason);
+  void finish_openai(Conn& c, const char* finish_reason, int prompt_tokens = -1);
   void flush_out(Conn& c);
   void close_conn(Conn& c);
   void drain_outbox();
@@ -671,11 +672,26 @@ void IoThread::handle_openai(Conn& c, HttpRequest& req) {
       msgs.empty())
     return bad(400, "messages must be a non-empty array of {role, content} objects");
   std::string norm = "[", last_user;
+  // The Mistral instruct template accepts system messages first, then user/assistant turns that alternate
+  // starting and ending with user (vLLM returns 400 on anything else): validate here, so a malformed
+  // conversation never reaches the engine's tokenizer.
+  std::string expect = "user";
+  bool seen_turn = false;
   for (size_t i = 0; i < msgs.size(); ++i) {
     auto& m = msgs[i];
     auto r = m.find("role");
     auto ct = m.find("content");
     if (r == m.end() || r->second.kind != JsonValue::kString) return bad(400, "every message needs a string role");
+    const std::string& role = r->second.str;
+    if (role != "system" && role != "user" && role != "assistant")
+      return bad(400, "unsupported message role '" + role + "' (system, user, assistant)");
+    if (role == "system") {
+      if (seen_turn) return bad(400, "system messages must come before the conversation turns");
+    } else {
+      if (role != expect) return bad(400, "conversation roles must alternate user/assistant/user/...");
+      expect = role == "user" ? "assistant" : "user";
+      seen_turn = true;
+    }
     std::string text;
     if (ct != m.end() && ct->second.kind == JsonValue::kString) {
       text = ct->second.str;
@@ -693,11 +709,32 @@ void IoThread::handle_openai(Conn& c, HttpRequest& req) {
     norm += (i ? ",{\"role\":" : "{\"role\":") + json_quote(r->second.str) + ",\"content\":" + json_quote(text) + "}";
   }
   norm += "]";
+  if (expect != "assistant") return bad(400, "the last conversation turn must be a user message");
   auto num = [&](const char* k, double dflt) {
     auto it2 = o.find(k);
     return (it2 != o.end() && it2->second.kind == JsonValue::kNumber) ? it2->second.num : dflt;
   };
+  // integer parameters: reject fractional / out-of-range values before any conversion (a double outside
+  // the target range is undefined behaviour to cast)
+  std::string int_err;
+  auto int_param = [&](const char* k, double lo, double hi) -> int64_t {
+    const double v = num(k, -1);
+    if (v == -1) return -1;
+    if (!(v >= lo && v <= hi) || v != std::floor(v)) {
+      if (int_err.empty()) int_err = std::string(k) + " must be an integer in [" + std::to_string((long long)lo) + ", " +
+                                     std::to_string((long long)hi) + "]";
+      return -1;
+    }
+    return (int64_t)v;
+  };
   if (num("n", 1) != 1) return bad(400, "only n = 1 is supported");
+  int64_t max_tokens = int_param("max_tokens", 1, 1 << 20);
+  if (max_tokens < 0) max_tokens = int_param("max_completion_tokens", 1, 1 << 20);
+  const int64_t top_k = int_param("top_k", -1, 1 << 20);
+  const int64_t seed = int_param("seed", 0, 9007199254740991.0);  // 2^53 - 1: every such double is exact
+  if (!int_err.empty()) return bad(400, int_err);
+  const double temperature = num("temperature", -1), top_p = num("top_p", -1);
+  if (!std::isfinite(temperature) || !std::isfinite(top_p)) return bad(400, "temperature and top_p must be finite");
   auto st = o.find("stream");
   const bool stream = st != o.end() && st->second.kind == JsonValue::kBool && st->second.b;
   std::string id = uuid4();
@@ -707,11 +744,11 @@ void IoThread::handle_openai(Conn& c, HttpRequest& req) {
   r.conversation_id = conv;
   r.message = last_user;
   r.messages_json = norm;
-  r.max_tokens = (int)num("max_tokens", num("max_completion_tokens", -1));
-  r.temperature = num("temperature", -1);
-  r.top_p = num("top_p", -1);
-  r.top_k = (int)num("top_k", -1);
-  r.seed = (int64_t)num("seed", -1);
+  r.max_tokens = (int)max_tokens;
+  r.temperature = temperature;
+  r.top_p = top_p;
+  r.top_k = (int)top_k;
+  r.seed = seed;
   {
     auto ie = o.find("ignore_eos");
     r.ignore_eos = ie != o.end() && ie->second.kind == JsonValue::kBool && ie->second.b;
@@ -758,9 +795,14 @@ void IoThread::deliver_openai(Conn& c, const FramePtr& f) {
   TokenMessage m;
   if (!parse_token_message(f->json, m)) return;
   if (f->done) {
-    if (m.token == "[ERROR]") return finish_openai(c, "abort");
-    // the engine ends a completion at EOS or at max_tokens; the count tells which (vLLM's finish_reason)
-    return finish_openai(c, c.oa_max_tokens > 0 && c.oa_count >= c.oa_max_tokens ? "length" : "stop");
+    // vLLM's finish_reason: the engine's own reason when it sent one (EOS = stop; max_tokens or the context
+    // limit = length; cancelled = abort), else from the terminal token and the count
+    const char* reason;
+    if (f->finish == kFinishStop) reason = "stop";
+    else if (f->finish == kFinishLength) reason = "length";
+    else if (f->finish == kFinishAbort || m.token == "[ERROR]" || m.token == "[BLOCKED]" || m.token == "[KILLED]") reason = "abort";
+    else reason = c.oa_max_tokens > 0 && c.oa_count >= c.oa_max_tokens ? "length" : "stop";
+    return finish_openai(c, reason, f->prompt_tokens);
   }
   c.got_first = true;
   ++c.oa_count;
@@ -784,13 +826,14 @@ void IoThread::deliver_openai(Conn& c, const FramePtr& f) {
   write_sse_bytes(c, ev);
 }
 
-void IoThread::finish_openai(Conn& c, const char* finish_reason) {
+void IoThread::finish_openai(Conn& c, const char* finish_reason, int prompt_tokens) {
   if (!c.sse) return;
+  const int pt = std::max(0, prompt_tokens);
   const std::string head = "{\"id\":" + json_quote(c.conv_id) + ",\"object\":\"chat.completion" +
                            std::string(c.oa_stream ? ".chunk" : "") + "\",\"created\":" + std::to_string(c.oa_created) +
                            ",\"model\":" + json_quote(c.oa_model) + ",\"choices\":[{\"index\":0,";
-  const std::string usage = "\"usage\":{\"prompt_tokens\":0,\"total_tokens\":" + std::to_string(c.oa_count) +
-                            ",\"completion_tokens\":" + std::to_string(c.oa_count) + "}";
+  const std::string usage = "\"usage\":{\"prompt_tokens\":" + std::to_string(pt) + ",\"total_tokens\":" +
+                            std::to_string(pt + c.oa_count) + ",\"completion_tokens\":" + std::to_string(c.oa_count) + "}";
   if (c.oa_stream) {
     std::string ev = "data: " + head + "\"delta\":{},\"logprobs\":null,\"finish_reason\":\"" + finish_reason +
                      "\",\"stop_reason\":null}]}\n\ndata: [DONE]\n\n";
@@ -802,10 +845,15 @@ void IoThread::finish_openai(Conn& c, const char* finish_reason) {
   std::string body = head + "\"message\":{\"role\":\"assistant\",\"content\":" + json_quote(c.oa_text) +
                      ",\"tool_calls\":[]},\"logprobs\":null,\"finish_reason\":\"" + finish_reason +
                      "\",\"stop_reason\":null}]," + usage + "}";
-  // buffered mode never wrote headers: close the pseudo-SSE session, then send one JSON response
+  // buffered mode never wrote headers: close the pseudo-SSE session, then send one JSON response (and close
+  // the connection after it when the client asked for Connection: close)
   end_sse(c, false);
   c.oa_text.clear();
   write_raw(c, simple_response(200, body, "application/json", ka));
+  if (!ka) {
+    c.close_after_write = true;
+    flush_out(c);
+  }
 }
 
 void IoThread::drain_outbox() {

@@ -51,6 +51,9 @@ class SamplingParams:
     ignore_eos: bool = False
 
 
+FINISH_CODES = {"": 0, "stop": 1, "length": 2, "abort": 3}  # runtime FinishReason (csrc/runtime/json.h)
+
+
 @dataclass(slots=True)
 class TokenEvent:
     conversation_id: str
@@ -59,6 +62,8 @@ class TokenEvent:
     done: bool
     text: str = ""          # overrides the vocabulary piece ("[DONE]", "[ERROR]")
     timestamp_ns: int = 0
+    finish: str = ""        # terminal events: "stop" (EOS), "length" (max_tokens / context), "abort"
+    prompt_tokens: int = -1  # terminal events: prompt length (OpenAI usage)
 
 
 @dataclass
@@ -283,7 +288,8 @@ class LLMEngine:
             return
         s.state = "finished"
         now = time.time_ns()
-        events.append(TokenEvent(s.conversation_id, -1, s.produced + 1, True, text=text, timestamp_ns=now))
+        events.append(TokenEvent(s.conversation_id, -1, s.produced + 1, True, text=text, timestamp_ns=now,
+                                 finish=reason, prompt_tokens=len(s.prompt)))
         if s.slot >= 0 and self.slots[s.slot] is s:
             self.slots[s.slot] = None
             self._dirty_slots.add(s.slot)
@@ -382,8 +388,10 @@ class LLMEngine:
                 self.stats["tokens"] += 1
             else:
                 s.produced -= 1
-            if is_eos or s.produced >= s.params.max_tokens or len(s.prompt) + s.produced >= self.r.max_model_len:
-                self._finish(s, events)
+            if is_eos:
+                self._finish(s, events, reason="stop")
+            elif s.produced >= s.params.max_tokens or len(s.prompt) + s.produced >= self.r.max_model_len:
+                self._finish(s, events, reason="length")
 
     def run_until_idle(self, max_steps: int = 100000) -> list:
         out = []

@@ -14,9 +14,6 @@ Decode step for a batch bucket of B slots (all device-resident, no host round tr
       rmsnorm            x = norm(resid) with the next layer's (or the final) weight
     gemm_out (fp32)      logits = x·Wlmᵀ (vocab shard)
 
-Optionally (DSSE_DEFERRED_NORM=1, TP=1; measured slower, off) the two per-layer norms are deferred: rmsnorm reduces the split-K slabs into resid and writes
-x = bf16(resid·γ) plus per-row partial sums of squares, spread over all CUs; the consuming GEMM (gate_up,
-the next QKV, the LM head) multiplies row m of its product by 1/rms(m) in its epilogue, (x·γ·r)W = r·(x·γ)W.
     sample               Gumbel-max / greedy; ids[b] <- token, ring[head][b] <- token, positions += 1
     ring_advance         head += 1
 
@@ -47,19 +44,12 @@ PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefil
 # 192-row bucket is faster on the wide path (hipBLASLt o / gate_up + gemm_wide qkv / down): 192 streams 9.40 vs
 # 10.09 ms/step, 160 streams 8.56 vs 9.52; 128 rows stay here (7.01 vs 7.20) -- profiles/bucket_ab_r1.md.
 DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
-# Deferred RMSNorm scale on the TP=1 engine-GEMM decode path (rmsnorm(row_ss=) + GEMM epilogue scale).
-DEFERRED_NORM = os.environ.get("DSSE_DEFERRED_NORM", "0") == "1"  # measured slower (profiles/experiments_r1.md)
 
 
 # Decode buckets above DECODE_GEMM_MAX_M (<= 256 rows): projections that run on the engine's 32x32-MFMA decode GEMM
 # (gemm_wide) instead of hipBLASLt -- QKV with its fused RoPE + KV-write epilogue (no separate rope kernel) and,
 # at TP=1, down with its split-K slabs reduced inside the next norm (profiles/experiments_r1.md).
 WIDE_ENGINE_OPS = frozenset(x for x in os.environ.get("DSSE_WIDE_ENGINE_OPS", "qkv,down").split(",") if x)
-
-
-def norm_chunks(H: int) -> int:
-    """Column chunks per row of the deferred norm: 128 threads x float4 per workgroup (H = 4096 -> 8)."""
-    return max(1, H // 512) if H % 512 == 0 else 1
 
 
 def batch_buckets(max_batch: int):
@@ -138,9 +128,6 @@ class ModelRunner:
         self.tmp = torch.zeros(Bm, H, **bf)
         # fp32 split-K slabs of the residual projections (reduced inside the next RMSNorm)
         self.split_part = torch.zeros(32 * Bm * H, device=dev, dtype=torch.float32)
-        # deferred RMSNorm (TP=1 engine-GEMM decode): per-row partial sums of squares over NORM_CHUNKS column
-        # chunks, written by rmsnorm(row_ss=) and turned into the row scale by the consuming GEMM's epilogue
-        self.row_ss = torch.zeros(Bm, norm_chunks(H), device=dev, dtype=torch.float32)
         self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
         nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
         self._cand = {b: torch.zeros(b, nch, 2, device=dev, dtype=torch.float32) for b in batch_buckets(Bm)}
@@ -171,35 +158,29 @@ class ModelRunner:
         if B > DECODE_GEMM_MAX_M:
             self._decode_layers_wide(B, resid, x, part, nparts)
             return
-        # TP=1: the norms after the split-K residual projections are deferred (x = bf16(resid * gamma) plus
-        # per-row partial sums of squares; the next GEMM applies 1/rms in its epilogue).  `ss` is the row_ss of
-        # the current x (None for layer 0's embedding norm and on the TP path, whose norms are complete).
-        ss = None
-        dss = self.row_ss[r] if comm.size == 1 and DEFERRED_NORM else None
         for li, L in enumerate(w.layers):
             ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
-                              self.kv.v[li], nh, nkv, row_ss=ss, eps=eps)
+                              self.kv.v[li], nh, nkv)
             ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
                                 self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
                                 self.part_ml, part, nparts)
-            if comm.size == 1:
+            if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
                 ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
-                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns, row_ss=dss)
+                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
             else:
                 ops.gemm_out(self.attn[r], L.wo_t, self.tmp[r])
                 comm.all_reduce(self.tmp[r])
                 ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=self.tmp[r])
-            ops.gemm_silu(x, L.wgu_t, self.h[r], row_ss=dss, eps=eps)
+            ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             if comm.size == 1:
                 ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
-                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns, row_ss=dss)
+                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
             else:
                 ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
                 comm.all_reduce(self.tmp[r])
                 ops.rmsnorm(resid, w_next, x, eps, delta=self.tmp[r])
-            ss = dss
-        ops.gemm_out(x, w.lm_head_t, self.logits[r], row_ss=ss, eps=eps)
+        ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
 

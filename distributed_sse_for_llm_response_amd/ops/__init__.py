@@ -61,13 +61,12 @@ def _hip(t: torch.Tensor) -> bool:
     return False
 
 
-def gemm_out(x, w, out, row_ss=None, eps=0.0):
-    """out[M, N] = x[M, K] · w[N, K]ᵀ (bf16 or fp32 out).  With `row_ss` (from rmsnorm(..., row_ss=)) row m
-    of the product is scaled by rsqrt(sum(row_ss[m]) / K + eps): the deferred RMSNorm scale."""
+def gemm_out(x, w, out):
+    """out[M, N] = x[M, K] · w[N, K]ᵀ (bf16 or fp32 out)."""
     if _hip(x):
-        torch.ops.dsse.gemm_out(x, w, out, row_ss, eps)
+        torch.ops.dsse.gemm_out(x, w, out)
     else:
-        ref.gemm_out(x, w, out, row_ss, eps)
+        ref.gemm_out(x, w, out)
 
 
 def gemm_resid(x, w, resid):
@@ -78,20 +77,20 @@ def gemm_resid(x, w, resid):
         ref.gemm_resid(x, w, resid)
 
 
-def gemm_silu(x, w, out, row_ss=None, eps=0.0):
-    """out[M, N/2] = silu(gate) * up with the interleaved gate/up weight rows (row_ss: as gemm_out)."""
+def gemm_silu(x, w, out):
+    """out[M, N/2] = silu(gate) * up with the interleaved gate/up weight rows."""
     if _hip(x):
-        torch.ops.dsse.gemm_silu(x, w, out, row_ss, eps)
+        torch.ops.dsse.gemm_silu(x, w, out)
     else:
-        ref.gemm_silu(x, w, out, row_ss, eps)
+        ref.gemm_silu(x, w, out)
 
 
-def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss=None, eps=0.0):
-    """Fused QKV projection + RoPE + paged KV write (decode; row_ss: as gemm_out)."""
+def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
+    """Fused QKV projection + RoPE + paged KV write (decode)."""
     if _hip(x):
-        torch.ops.dsse.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss, eps)
+        torch.ops.dsse.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
     else:
-        ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss, eps)
+        ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
 
 
 def gemm_resid_split(x, w, resid, part) -> int:
@@ -103,16 +102,18 @@ def gemm_resid_split(x, w, resid, part) -> int:
     return 0
 
 
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0, row_ss=None):
-    """resid (+= delta | sum of `nsplit` split-K slabs in `part` | = embed[ids]); y = rmsnorm(resid) * w.
+def refresh_env() -> None:
+    """Re-read the DSSE_* kernel tuning variables (cached by the library on first use)."""
+    if load_library():
+        torch.ops.dsse.refresh_env()
 
-    With `row_ss` [M, G] (fp32; split-K slab or no-delta mode only) the norm is deferred to the consuming
-    decode GEMM: y = bf16(resid * w) and row_ss[m, g] = sum of squares of chunk g of row m, so the kernel
-    spreads every row over G workgroups with no row-wide reduction; pass row_ss (and eps) to the GEMM."""
+
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
+    """resid (+= delta | sum of `nsplit` split-K slabs in `part` | = embed[ids]); y = rmsnorm(resid) * w."""
     if _hip(resid):
-        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit, row_ss)
+        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
     else:
-        ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit, row_ss)
+        ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
 
 
 def rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):

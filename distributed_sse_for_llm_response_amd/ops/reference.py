@@ -99,32 +99,23 @@ def _write_kv(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache, v_
 
 # ---------------------------------------------------------------- GEMMs
 # The decode GEMMs take their weight in the tiled layout (tile_weight), like the HIP kernels.
-def _row_scale(y, row_ss, eps, K):
-    """Deferred RMSNorm scale (rmsnorm with row_ss): x rows are bf16(resid * gamma), row_ss [M, G] holds the
-    rows' partial sums of squares; (x·r) W = r·(x W) with r = 1 / rms."""
-    if row_ss is None:
-        return y
-    M = y.shape[0]
-    return y * torch.rsqrt(row_ss[:M].float().sum(1, keepdim=True) / K + eps)
-
-
-def gemm_out(x, w, out, row_ss=None, eps=0.0):
-    out.copy_(_row_scale(x.float() @ untile_weight(w).float().t(), row_ss, eps, x.shape[1]).to(out.dtype))
+def gemm_out(x, w, out):
+    out.copy_((x.float() @ untile_weight(w).float().t()).to(out.dtype))
 
 
 def gemm_resid(x, w, resid):
     resid.add_(x.float() @ untile_weight(w).float().t())
 
 
-def gemm_silu(x, w, out, row_ss=None, eps=0.0):
-    y = _row_scale(x.float() @ untile_weight(w).float().t(), row_ss, eps, x.shape[1]).view(x.shape[0], -1, 2, 8)
+def gemm_silu(x, w, out):
+    y = (x.float() @ untile_weight(w).float().t()).view(x.shape[0], -1, 2, 8)
     g, u = y[:, :, 0, :], y[:, :, 1, :]
     out.copy_((torch.nn.functional.silu(g) * u).reshape(x.shape[0], -1).to(out.dtype))
 
 
-def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, row_ss=None, eps=0.0):
+def gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):
     M = x.shape[0]
-    y = _row_scale(x.float() @ untile_weight(w).float().t(), row_ss, eps, x.shape[1])
+    y = x.float() @ untile_weight(w).float().t()
     qkv = _unpermute_units(y, nh + 2 * nkv)
     rot = _rope(qkv[:, : nh + nkv], positions[:M], rope)
     q_out.view(-1)[: M * nh * HEAD_DIM].copy_(rot[:, :nh].reshape(-1).to(q_out.dtype))
@@ -145,7 +136,7 @@ def silu_mul(gu, h):
 
 
 # ---------------------------------------------------------------- norms
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0, row_ss=None):
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
     M = y.shape[0]
     H = y.shape[1]
     if embed is not None:
@@ -155,11 +146,6 @@ def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nspli
     elif part is not None and nsplit > 0:
         resid[:M] += part.view(-1)[: nsplit * M * H].view(nsplit, M, H).sum(0)
     r = resid[:M]
-    if row_ss is not None:  # deferred scale: y = bf16(resid * gamma), per-chunk sums of squares for the consumer
-        G = row_ss.shape[1]
-        row_ss[:M].copy_(r.view(M, G, H // G).pow(2).sum(-1))
-        y.copy_((r * w.float()).to(y.dtype))
-        return
     y.copy_((r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(y.dtype))
 
 

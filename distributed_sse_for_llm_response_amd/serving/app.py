@@ -19,7 +19,7 @@ import time
 import torch
 
 from .. import runtime as rt_mod
-from ..engine.engine import LLMEngine, SamplingParams
+from ..engine.engine import FINISH_CODES, LLMEngine, SamplingParams, TokenEvent
 from ..engine.kv_cache import KVCache
 from ..engine.model_runner import ModelRunner
 from ..models.mistral import TINY, get_config, init_standard_weights
@@ -82,6 +82,7 @@ class EngineLoop(threading.Thread):
         self.tracer = StepTracer()
         self.last_progress = time.monotonic()
         self.steps = 0
+        self.tokenize_errors = 0
         if self._remote:
             engine.on_ttft = self._ttft.append
             engine.on_itl = self._itl.append
@@ -108,7 +109,21 @@ class EngineLoop(threading.Thread):
             return
         self.rt.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
                                [e.sequence for e in events], [e.done for e in events], 0,
-                               [e.text for e in events])
+                               [e.text for e in events], [FINISH_CODES.get(e.finish, 0) for e in events],
+                               [e.prompt_tokens for e in events])
+
+    def tokenize(self, req):
+        """Prompt ids of a queued request, or None after publishing a terminal [ERROR] event for it: a
+        conversation the tokenizer / chat template rejects must fail alone, not stop the loop (every other
+        live stream of this replica depends on it)."""
+        try:
+            return prompt_for_request(self.tok, req)
+        except Exception as e:  # noqa: BLE001 - any tokenizer / template failure is this request's error
+            self.tokenize_errors += 1
+            self.publish([TokenEvent(req["conversation_id"], -1, 1, True, text="[ERROR]", timestamp_ns=time.time_ns(),
+                                     finish="abort", prompt_tokens=0)])
+            print(f"[engine] request {req['conversation_id']} rejected by the tokenizer: {e!r}", flush=True)
+            return None
 
     def _observe(self):
         e = self.engine
@@ -144,8 +159,10 @@ class EngineLoop(threading.Thread):
                 # only paused streams left: wait briefly so their resume events get through
                 wait = 0 if busy else (2 if self.engine.has_work() else 20)
                 for req in self.rt.poll_requests(256, wait):
-                    self.engine.add_request(req["conversation_id"], prompt_for_request(self.tok, req),
-                                            self._params(req), arrival_ns=req["arrival_ns"])
+                    prompt = self.tokenize(req)
+                    if prompt is not None:
+                        self.engine.add_request(req["conversation_id"], prompt, self._params(req),
+                                                arrival_ns=req["arrival_ns"])
                 for conv in self.rt.pop_cancellations():
                     self.engine.abort(conv)
                 for conv, paused in self.flow_events():

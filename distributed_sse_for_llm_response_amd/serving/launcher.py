@@ -15,7 +15,6 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.comm import TPComm, init_distributed
-from ..models.tokenizer import prompt_for_request
 from .app import EngineLoop, ServingApp, build_engine
 from .config import ServeConfig
 
@@ -53,9 +52,9 @@ class TPLeaderLoop(EngineLoop):
                 adds, aborts = [], []
                 wait = 0 if busy else (2 if self.engine.has_work() else 20)
                 for req in self.rt.poll_requests(256, wait):
-                    p = self._params(req)
-                    prompt = prompt_for_request(self.tok, req)
-                    adds.append((req["conversation_id"], prompt, p, req["arrival_ns"]))
+                    prompt = self.tokenize(req)
+                    if prompt is not None:
+                        adds.append((req["conversation_id"], prompt, self._params(req), req["arrival_ns"]))
                 aborts = list(self.rt.pop_cancellations())
                 flow = self.flow_events()  # pause timeouts are decided here, so all ranks agree
                 for conv, paused in flow:

@@ -137,3 +137,86 @@ def test_openai_chat_completions_non_stream_multi_turn_and_models(cpu_app):
     assert m["object"] == "list" and m["data"][0]["object"] == "model"
     bad = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions", {"messages": []})
     assert bad.status == 400 and json.loads(bad.body)["object"] == "error"
+
+
+@pytest.mark.parametrize("msgs,why", [
+    ([{"role": "user", "content": "a"}, {"role": "user", "content": "b"}], "alternate"),
+    ([{"role": "tool", "content": "x"}, {"role": "user", "content": "b"}], "unsupported"),
+    ([{"role": "assistant", "content": "x"}], "alternate"),
+    ([{"role": "user", "content": "a"}, {"role": "assistant", "content": "b"}], "last"),
+    ([{"role": "user", "content": "a"}, {"role": "system", "content": "late"}, {"role": "assistant", "content": "b"},
+      {"role": "user", "content": "c"}], "system"),
+])
+def test_openai_rejects_malformed_conversations_and_keeps_serving(cpu_app, msgs, why):
+    """Conversations the Mistral chat template would reject are a 400 (vLLM's answer), never an engine error."""
+    r = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions", {"messages": msgs, "max_tokens": 3})
+    assert r.status == 400, r.body
+    err = json.loads(r.body)
+    assert err["object"] == "error" and why in err["message"]
+    ok = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions",
+                 {"messages": [{"role": "user", "content": "still up?"}], "max_tokens": 2}, timeout=60)
+    assert ok.status == 200 and json.loads(ok.body)["usage"]["completion_tokens"] <= 2
+
+
+@pytest.mark.parametrize("field,value", [("max_tokens", 2.5), ("max_tokens", 1e20), ("top_k", 1e12), ("seed", -5),
+                                         ("max_tokens", 0)])
+def test_openai_rejects_out_of_range_integer_parameters(cpu_app, field, value):
+    body = {"messages": [{"role": "user", "content": "x"}], "max_tokens": 3, field: value}
+    r = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions", body)
+    assert r.status == 400 and field in json.loads(r.body)["message"]
+
+
+def test_openai_finish_reason_and_usage_from_the_engine(cpu_app):
+    """The engine's default max_tokens (8 here, not sent by the client) ends the completion: finish_reason is
+    "length" and usage carries the real prompt length."""
+    r = request(H, cpu_app.port("origin"), "POST", "/v1/chat/completions",
+                {"messages": [{"role": "user", "content": "tell me a long story please"}]}, timeout=60)
+    d = json.loads(r.body)
+    u = d["usage"]
+    if u["completion_tokens"] == 8:
+        assert d["choices"][0]["finish_reason"] == "length"
+    else:  # EOS before the budget
+        assert d["choices"][0]["finish_reason"] == "stop"
+    assert u["prompt_tokens"] > 0 and u["total_tokens"] == u["prompt_tokens"] + u["completion_tokens"]
+
+
+def test_openai_non_stream_honours_connection_close(cpu_app):
+    import socket
+
+    body = json.dumps({"messages": [{"role": "user", "content": "bye"}], "max_tokens": 2}).encode()
+    s = socket.create_connection((H, cpu_app.port("origin")), timeout=60)
+    s.sendall(b"POST /v1/chat/completions HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nConnection: close\r\n"
+              b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+    data = b""
+    while True:  # the server closes after the response: recv returns b"" (a keep-alive socket would time out)
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.startswith(b"HTTP/1.1 200") and b'"chat.completion"' in data
+
+
+def test_tokenizer_failure_fails_only_that_request():
+    """A request the tokenizer rejects gets a terminal [ERROR] event; the engine loop keeps serving."""
+    from distributed_sse_for_llm_response_amd.serving.app import EngineLoop
+
+    class _Tok:
+        def chat_prompt(self, m):
+            raise ValueError("template says no")
+
+        messages_prompt = chat_prompt
+
+    class _Rt:
+        def __init__(self):
+            self.published = []
+
+        def publish_tokens(self, *a):
+            self.published.append(a)
+
+    loop = EngineLoop.__new__(EngineLoop)
+    loop.rt, loop.tok, loop.tokenize_errors = _Rt(), _Tok(), 0
+    assert loop.tokenize({"conversation_id": "bad-1", "message": "x"}) is None
+    assert loop.tokenize_errors == 1
+    (convs, ids, seqs, dones, ts, texts, finish, ptoks), = loop.rt.published
+    assert convs == ["bad-1"] and dones == [True] and texts == ["[ERROR]"] and finish == [3]

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Decode paged-attention microbenchmark: B sequences x ctx tokens, Mistral-7B heads (32 q / 8 kv, d 128).
 
-Usage (GPU box): python tools/bench_attn.py [--B 64] [--ctx 560] [--configs "KWV=4,PF=1;KWV=8,PF=0"]
+Usage (GPU box): python tools/bench_attn.py [--B 64] [--ctx 560] [--configs "KWV=4;KWV=1"]
 Pages are randomly permuted over the cache and several layer caches are rotated (> 256 MiB Infinity
 Cache), so every call streams its K/V from HBM as in a decode step.  Times hipGraph replays; prints us and
 the achieved K/V bandwidth.
@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--hq", type=int, default=32)
     ap.add_argument("--hkv", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--configs", default="KWV=4,PF=1")
+    ap.add_argument("--configs", default="KWV=4;KWV=1")
     ap.add_argument("--target-wgs", default="512", help="flash-decoding partition targets to sweep")
     args = ap.parse_args()
     ops.load_library(required=True)
@@ -54,6 +54,7 @@ def main():
                 for item in filter(None, cfg.split(",")):
                     k, v = item.split("=")
                     os.environ["DSSE_ATTN_" + k] = v
+                ops.refresh_env()
 
                 def run(i):
                     ops.paged_attention(0, q, ks[i % copies], vs[i % copies], bt, q_start, q_len, ctx_len, work_seq,

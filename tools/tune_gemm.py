@@ -95,6 +95,7 @@ def main():
                 for item in filter(None, kv.split(",")):
                     k, v = item.split("=")
                     os.environ[k] = v
+                ops.refresh_env()
                 if name == "gate_up":
                     out = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
                     fn = (lambda i, out=out, x=x: ops.gemm_silu(x, ws[i % copies], out))
