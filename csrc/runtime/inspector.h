@@ -31,4 +31,28 @@ enum class InspectionMode { kDisabled, kInline, kAsync, kHybrid };
 InspectionMode parse_inspection_mode(std::string_view s);
 const char* inspection_mode_name(InspectionMode m);
 
+// Client of a remote inspector (INSPECTION_ENDPOINT, src/sse-adapter/main.go:36; the inline hook of
+// src/sse-adapter/sse_handler.go:199-206 calls it per token): POSTs the reference's NatsMessage
+// {"subject","data","sequence","timestamp"} to the endpoint URL (the Spin function's POST /inspect,
+// src/spin-functions/nats-subscriber/src/lib.rs:34-54) and parses {"action","reason","redacted_content"}.
+// Blocking HTTP/1.1 over one keep-alive connection (reconnected on error); one client per calling thread.
+class RemoteInspector {
+ public:
+  explicit RemoteInspector(const std::string& url, int timeout_ms = 250);
+  ~RemoteInspector();
+  RemoteInspector(const RemoteInspector&) = delete;
+  RemoteInspector& operator=(const RemoteInspector&) = delete;
+  bool valid() const { return !host_.empty(); }
+  // false on transport / protocol failure (the caller fails open)
+  bool inspect(const std::string& subject, std::string_view data, int64_t sequence, int64_t timestamp,
+               InspectionResult* out);
+
+ private:
+  bool connect_();
+  bool roundtrip(const std::string& req, std::string* body);
+  std::string host_, port_, path_;
+  int timeout_ms_;
+  int fd_ = -1;
+};
+
 }  // namespace dsse

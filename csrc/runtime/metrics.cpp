@@ -107,6 +107,12 @@ std::string Metrics::render() const {
   line(o, "bus_conversations", "Conversations tracked by the bus (live + retained)", "gauge", bus_conversations.get());
   line(o, "resp_publish_total", "PUBLISH commands accepted by the RESP ingest shim", "counter",
        resp_publish_total.get());
+  line(o, "bus_duplicates_dropped_total", "Frames dropped as duplicates (dedupe window) or after a conversation ended",
+       "counter", bus_duplicates_dropped_total.get());
+  line(o, "control_kills_total", "Conversations killed through chat.<id>.control / chat.control.kill", "counter",
+       control_kills_total.get());
+  line(o, "inspection_remote_errors_total", "INSPECTION_ENDPOINT calls that failed (fail-open)", "counter",
+       inspection_remote_errors_total.get());
   line(o, "inspection_redacted_total", "Tokens redacted by the security inspector", "counter",
        inspection_redacted_total.get());
   line(o, "inspection_dropped_total", "Tokens dropped by the security inspector", "counter",

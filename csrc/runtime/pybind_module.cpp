@@ -59,6 +59,9 @@ class Runtime {
     c.model_name = gets("model_name", c.model_name);
     c.inspection = parse_inspection_mode(gets("inspection_mode", "disabled"));
     c.inspection_buffer_ms = geti("inspection_buffer_ms", c.inspection_buffer_ms);
+    c.inspection_endpoint = gets("inspection_endpoint", "");
+    c.inspection_timeout_ms = geti("inspection_timeout_ms", c.inspection_timeout_ms);
+    c.dedupe_window_s = geti("dedupe_window_s", c.dedupe_window_s);
     c.keepalive_ms = geti("keepalive_ms", c.keepalive_ms);
     c.first_token_timeout_ms = geti("first_token_timeout_ms", c.first_token_timeout_ms);
     c.max_pending_bytes = (size_t)geti("max_pending_bytes", (int)c.max_pending_bytes);
@@ -70,6 +73,7 @@ class Runtime {
     BusConfig bc;
     bc.replay_max = c.replay_max;
     bc.retention_s = c.retention_s;
+    bc.dedupe_window_s = c.dedupe_window_s;
     bus_ = std::make_shared<Bus>(bc);
     server_ = std::make_unique<Server>(c, bus_);
   }

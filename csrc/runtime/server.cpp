@@ -266,7 +266,37 @@ bool glob_match(const char* p, const char* s) {
   return !*s;
 }
 
-std::string resp_bulk(const std::string& s) { return "$" + std::to_string(s.size()) + "\r\n" + s + "\r\n"; }
+std::string resp_bulk(std::string_view s) {
+  std::string o = "$" + std::to_string(s.size()) + "\r\n";
+  o.append(s.data(), s.size());
+  o += "\r\n";
+  return o;
+}
+
+// The conversation a control-subject message targets, or "" when `subject` is not a control subject:
+//   chat.<id>.control   (the CHAT_CONTROL stream, kubernetes/base/nats-core/core-cluster.yaml:246-255)
+//   chat.control.kill   payload = the conversation id, raw or {"conversation_id": ...}
+//                       (docs/security-inspection-patterns.md:118-123)
+std::string control_target(const std::string& subject, const std::string& payload) {
+  if (subject == "chat.control.kill") {
+    std::map<std::string, JsonValue> o;
+    if (parse_json_object(payload, o)) {
+      auto it = o.find("conversation_id");
+      return (it != o.end() && it->second.kind == JsonValue::kString) ? it->second.str : std::string();
+    }
+    size_t b = payload.find_first_not_of(" \t\r\n\""), e = payload.find_last_not_of(" \t\r\n\"");
+    return b == std::string::npos ? std::string() : payload.substr(b, e - b + 1);
+  }
+  const std::string pre = "chat.", suf = ".control";
+  if (subject.size() > pre.size() + suf.size() && subject.rfind(pre, 0) == 0 &&
+      subject.compare(subject.size() - suf.size(), suf.size(), suf) == 0)
+    return subject.substr(pre.size(), subject.size() - pre.size() - suf.size());
+  return std::string();
+}
+bool is_control_subject(const std::string& subject) {
+  return subject == "chat.control.kill" ||
+         (subject.rfind("chat.", 0) == 0 && subject.size() > 13 && subject.compare(subject.size() - 8, 8, ".control") == 0);
+}
 
 }  // namespace
 
@@ -587,7 +617,8 @@ void IoThread::deliver_token(Conn& c, const FramePtr& f) {
     deliver_openai(c, f);
     return;
   }
-  const InspectionMode mode = srv_.config().inspection;
+  // with a remote inspection gate the bus has already applied the verdict to this frame
+  const InspectionMode mode = srv_.remote_inspection() ? InspectionMode::kDisabled : srv_.config().inspection;
   if (mode == InspectionMode::kHybrid) {
     c.held.emplace_back(mono_ns() + (int64_t)srv_.config().inspection_buffer_ms * 1000000LL, f);
     return;
@@ -595,7 +626,7 @@ void IoThread::deliver_token(Conn& c, const FramePtr& f) {
   FramePtr out = f;
   if (mode == InspectionMode::kInline && !f->done) {
     TokenMessage m;
-    if (parse_token_message(f->json, m)) {
+    if (parse_token_message(f->json(), m)) {
       InspectionResult r = inspect_message(m.token);
       if (r.action == InspectAction::kDrop) {
         metrics().inspection_dropped_total.inc();
@@ -793,7 +824,7 @@ void IoThread::handle_openai(Conn& c, HttpRequest& req) {
 
 void IoThread::deliver_openai(Conn& c, const FramePtr& f) {
   TokenMessage m;
-  if (!parse_token_message(f->json, m)) return;
+  if (!parse_token_message(f->json(), m)) return;
   if (f->done) {
     // vLLM's finish_reason: the engine's own reason when it sent one (EOS = stop; max_tokens or the context
     // limit = length; cancelled = abort), else from the terminal token and the count
@@ -883,10 +914,10 @@ void IoThread::drain_outbox() {
         const std::string subj = Bus::subject_for(it.frame->conversation_id);
         std::string msg;
         for (const auto& ch : c.resp_channels)
-          if (ch == subj) msg += "*3\r\n$7\r\nmessage\r\n" + resp_bulk(ch) + resp_bulk(it.frame->json);
+          if (ch == subj) msg += "*3\r\n$7\r\nmessage\r\n" + resp_bulk(ch) + resp_bulk(it.frame->json());
         for (const auto& p : c.resp_patterns)
           if (glob_match(p.c_str(), subj.c_str()))
-            msg += "*4\r\n$8\r\npmessage\r\n" + resp_bulk(p) + resp_bulk(subj) + resp_bulk(it.frame->json);
+            msg += "*4\r\n$8\r\npmessage\r\n" + resp_bulk(p) + resp_bulk(subj) + resp_bulk(it.frame->json());
         if (!msg.empty()) write_raw(c, msg);
         break;
       }
@@ -909,7 +940,7 @@ void IoThread::timers() {
       FramePtr f = c.held.front().second;
       c.held.pop_front();
       TokenMessage m;
-      if (!f->done && parse_token_message(f->json, m)) {
+      if (!f->done && parse_token_message(f->json(), m)) {
         InspectionResult r = inspect_message(m.token);
         if (r.action == InspectAction::kDrop) {
           metrics().inspection_dropped_total.inc();
@@ -1163,8 +1194,22 @@ void IoThread::handle_request(Conn& c, HttpRequest& req) {
       write_raw(c, http_error(405, "Method not allowed", ka));
       return;
     }
-    // subject chat.<id>.tokens (or a bare conversation id); body: a TokenMessage JSON
+    // subject chat.<id>.tokens (or a bare conversation id); body: a TokenMessage JSON.  Control subjects
+    // (chat.<id>.control, chat.control.kill) end the conversation instead.
     std::string subject = path.substr(9);
+    if (is_control_subject(subject)) {
+      const std::string conv = control_target(subject, req.body);
+      if (conv.empty()) {
+        write_raw(c, http_error(400, "control message names no conversation", ka));
+        return;
+      }
+      const bool killed = srv_.kill_conversation(conv, "[KILLED]", "control subject " + subject);
+      if (killed) metrics().control_kills_total.inc();
+      write_raw(c, simple_response(200, std::string("{\"status\": \"") + (killed ? "killed" : "published") +
+                                            "\", \"conversation_id\": " + json_quote(conv) + "}",
+                                   "application/json", ka));
+      return;
+    }
     TokenMessage m;
     if (!parse_token_message(req.body, m)) {
       write_raw(c, http_error(400, "Invalid JSON body", ka));
@@ -1252,6 +1297,12 @@ void IoThread::handle_resp(Conn& c) {
     if (cmd == "ping") {
       if (c.resp_pubsub) write_raw(c, "*2\r\n$4\r\npong\r\n" + resp_bulk(args.size() > 1 ? args[1] : ""));
       else write_raw(c, args.size() > 1 ? resp_bulk(args[1]) : "+PONG\r\n");
+    } else if (cmd == "publish" && args.size() == 3 && is_control_subject(args[1])) {
+      // kill signal: PUBLISH chat.<id>.control <any> / PUBLISH chat.control.kill <conversation id>
+      const std::string conv = control_target(args[1], args[2]);
+      const bool killed = srv_.kill_conversation(conv, "[KILLED]", "control subject " + args[1]);
+      if (killed) metrics().control_kills_total.inc();
+      write_raw(c, killed ? ":1\r\n" : ":0\r\n");
     } else if (cmd == "publish" && args.size() == 3) {
       TokenMessage m;
       int n = 0;
@@ -1376,6 +1427,12 @@ bool Server::start(std::string* err) {
     inspector_->start();
     bus_->add_tap(inspector_);
   }
+  if (!cfg_.inspection_endpoint.empty() &&
+      (cfg_.inspection == InspectionMode::kInline || cfg_.inspection == InspectionMode::kHybrid)) {
+    gate_ = std::make_shared<InspectionGate>(*this, 4);
+    gate_->start();
+    bus_->set_gate(gate_);
+  }
   if (!cfg_.upstream_url.empty()) {
     relay_ = std::make_unique<UpstreamRelay>(*bus_, cfg_.upstream_url);
     if (!relay_->start(err)) return false;
@@ -1411,6 +1468,11 @@ void Server::stop() {
     inspector_->stop();
     inspector_.reset();
   }
+  if (gate_) {
+    bus_->set_gate(nullptr);
+    gate_->stop();
+    gate_.reset();
+  }
   io_.clear();
 }
 
@@ -1430,6 +1492,16 @@ void Server::note_cancel(const std::string& conv_id) {
   std::lock_guard<std::mutex> g(cancel_mu_);
   cancels_.push_back(conv_id);
 }
+
+bool Server::kill_conversation(const std::string& conv_id, const std::string& token, const std::string& why) {
+  if (conv_id.empty() || !bus_->terminate(conv_id, token, kFinishAbort)) return false;
+  note_cancel(conv_id);
+  log_json(LogLevel::kWarn, "conversation killed",
+           "\"conversation_id\":" + json_quote(conv_id) + ",\"token\":" + json_quote(token) + ",\"reason\":" + json_quote(why));
+  return true;
+}
+
+
 
 void Server::flow_update(const std::string& conv_id, int delta) {
   std::lock_guard<std::mutex> g(flow_mu_);  // lock order: flow_mu_ -> bus shard (the bus never calls back)
@@ -1539,7 +1611,10 @@ constexpr int kNumStubWords = sizeof(kStubWords) / sizeof(kStubWords[0]);
 }  // namespace
 
 // ------------------------------------------------------------------ async inspection
-AsyncInspector::AsyncInspector(Server& s) : srv_(s) {}
+AsyncInspector::AsyncInspector(Server& s) : srv_(s) {
+  if (!s.config().inspection_endpoint.empty())
+    remote_ = std::make_unique<RemoteInspector>(s.config().inspection_endpoint, s.config().inspection_timeout_ms);
+}
 AsyncInspector::~AsyncInspector() { stop(); }
 
 void AsyncInspector::start() { thread_ = std::thread([this] { run(); }); }
@@ -1576,20 +1651,177 @@ void AsyncInspector::run() {
       if (f->done) continue;
       if (std::find(killed_.begin(), killed_.end(), f->conversation_id) != killed_.end()) continue;
       TokenMessage m;
-      if (!parse_token_message(f->json, m)) continue;
-      const InspectionResult r = inspect_message(m.token);
+      if (!parse_token_message(f->json(), m)) continue;
+      InspectionResult r;
+      if (remote_) {
+        if (!remote_->inspect(Bus::subject_for(f->conversation_id), m.token, m.sequence, m.timestamp, &r)) {
+          metrics().inspection_remote_errors_total.inc();
+          continue;  // fail open
+        }
+      } else {
+        r = inspect_message(m.token);
+      }
       if (r.action == InspectAction::kRedact) metrics().inspection_redacted_total.inc();
       if (r.action != InspectAction::kDrop) continue;
       // kill: terminal token for every subscriber, cancellation for the engine
       killed_.push_back(f->conversation_id);
       if (killed_.size() > 4096) killed_.erase(killed_.begin(), killed_.begin() + 2048);
       metrics().inspection_killed_total.inc();
-      TokenMessage kill{f->conversation_id, "[BLOCKED]", srv_.bus().last_sequence(f->conversation_id) + 1, true, now_ns()};
-      srv_.bus().publish(kill);
-      srv_.note_cancel(f->conversation_id);
-      log_json(LogLevel::kWarn, "conversation blocked by inspection",
-               "\"conversation_id\":" + json_quote(f->conversation_id) + ",\"reason\":" + json_quote(r.reason));
+      srv_.kill_conversation(f->conversation_id, "[BLOCKED]", "inspection: " + r.reason);
     }
+  }
+}
+
+// ------------------------------------------------------------------ remote inline / hybrid inspection
+InspectionGate::InspectionGate(Server& s, int workers) : srv_(s) {
+  for (int i = 0; i < std::max(1, workers); ++i) workers_.emplace_back(new Worker);
+}
+
+InspectionGate::~InspectionGate() { stop(); }
+
+void InspectionGate::start() {
+  for (auto& w : workers_) {
+    Worker* wp = w.get();
+    wp->thread = std::thread([this, wp] { run(*wp); });
+  }
+}
+
+void InspectionGate::stop() {
+  if (stop_.exchange(true)) return;
+  for (auto& w : workers_) {
+    w->cv.notify_all();
+    if (w->thread.joinable()) w->thread.join();
+  }
+}
+
+bool InspectionGate::admit(const FramePtr& f) {
+  if (stop_.load(std::memory_order_relaxed)) return false;
+  Worker& w = *workers_[std::hash<std::string>{}(f->conversation_id) % workers_.size()];
+  {
+    std::lock_guard<std::mutex> g(w.mu);
+    w.q.push_back(f);
+  }
+  w.cv.notify_one();
+  return true;
+}
+
+namespace {
+FramePtr with_token(const FramePtr& f, const std::string& token) {
+  TokenMessage m;
+  parse_token_message(f->json(), m);
+  m.token = token;
+  m.finish = f->finish;
+  m.prompt_tokens = f->prompt_tokens;
+  return Bus::make_frame(m);
+}
+}  // namespace
+
+void InspectionGate::inline_frame(RemoteInspector& ri, const FramePtr& f, std::vector<FramePtr>& out) {
+  TokenMessage m;
+  if (f->done || !parse_token_message(f->json(), m)) {
+    out.push_back(f);
+    return;
+  }
+  InspectionResult r;
+  if (!ri.inspect(Bus::subject_for(f->conversation_id), m.token, m.sequence, m.timestamp, &r)) {
+    metrics().inspection_remote_errors_total.inc();
+    out.push_back(f);  // fail open
+    return;
+  }
+  if (r.action == InspectAction::kDrop) {
+    metrics().inspection_dropped_total.inc();
+    return;
+  }
+  if (r.action == InspectAction::kRedact) {
+    metrics().inspection_redacted_total.inc();
+    out.push_back(with_token(f, r.redacted_content));
+    return;
+  }
+  out.push_back(f);
+}
+
+void InspectionGate::hybrid_flush(RemoteInspector& ri, const std::string& conv, Held& h, std::vector<FramePtr>& out) {
+  h.cleared = true;
+  if (h.frames.empty()) return;
+  std::string text;
+  int64_t seq = 0, ts = 0;
+  for (const auto& f : h.frames) {
+    TokenMessage m;
+    if (f->done || !parse_token_message(f->json(), m)) continue;
+    text += m.token;
+    seq = m.sequence;
+    ts = m.timestamp;
+  }
+  InspectionResult r;
+  if (text.empty()) {
+    r.action = InspectAction::kAllow;
+  } else if (!ri.inspect(Bus::subject_for(conv), text, seq, ts, &r)) {
+    metrics().inspection_remote_errors_total.inc();
+    r.action = InspectAction::kAllow;  // fail open
+  }
+  if (r.action == InspectAction::kDrop) {
+    metrics().inspection_killed_total.inc();
+    h.frames.clear();
+    srv_.kill_conversation(conv, "[BLOCKED]", "inspection: " + r.reason);
+    return;
+  }
+  if (r.action == InspectAction::kRedact) {  // the held text becomes one frame (sequence of the last token)
+    metrics().inspection_redacted_total.inc();
+    FramePtr last_tok;
+    for (const auto& f : h.frames)
+      if (!f->done) last_tok = f;
+    if (last_tok) out.push_back(with_token(last_tok, r.redacted_content));
+    for (const auto& f : h.frames)
+      if (f->done) out.push_back(f);
+  } else {
+    out.insert(out.end(), h.frames.begin(), h.frames.end());
+  }
+  h.frames.clear();
+}
+
+void InspectionGate::hybrid_frame(RemoteInspector& ri, std::unordered_map<std::string, Held>& held, const FramePtr& f,
+                                  std::vector<FramePtr>& out) {
+  auto [it, inserted] = held.try_emplace(f->conversation_id);
+  Held& h = it->second;
+  h.last_mono = mono_ns();
+  if (inserted) h.first_mono = h.last_mono;
+  if (h.cleared) {
+    out.push_back(f);
+  } else {
+    h.frames.push_back(f);
+    if (f->done) hybrid_flush(ri, f->conversation_id, h, out);
+  }
+  if (f->done) held.erase(it);
+}
+
+void InspectionGate::run(Worker& w) {
+  const ServerConfig& cfg = srv_.config();
+  RemoteInspector ri(cfg.inspection_endpoint, cfg.inspection_timeout_ms);
+  const bool hybrid = cfg.inspection == InspectionMode::kHybrid;
+  const int64_t window = (int64_t)cfg.inspection_buffer_ms * 1000000LL;
+  std::unordered_map<std::string, Held> held;
+  while (!stop_.load()) {
+    std::deque<FramePtr> batch;
+    {
+      std::unique_lock<std::mutex> lk(w.mu);
+      w.cv.wait_for(lk, std::chrono::milliseconds(hybrid ? 5 : 50), [&] { return stop_.load() || !w.q.empty(); });
+      batch.swap(w.q);
+    }
+    std::vector<FramePtr> out;
+    for (const auto& f : batch) {
+      if (hybrid) hybrid_frame(ri, held, f, out);
+      else inline_frame(ri, f, out);
+    }
+    if (hybrid) {  // buffer windows that ran out; forget conversations idle for 10 minutes
+      const int64_t now = mono_ns();
+      for (auto it = held.begin(); it != held.end();) {
+        Held& h = it->second;
+        if (!h.cleared && now - h.first_mono >= window) hybrid_flush(ri, it->first, h, out);
+        if (h.cleared && h.frames.empty() && now - h.last_mono > 600LL * 1000000000LL) it = held.erase(it);
+        else ++it;
+      }
+    }
+    if (!out.empty()) srv_.bus().deliver_gated(out);
   }
 }
 

@@ -49,6 +49,11 @@ struct ServerConfig {
   std::string model_name = "mistralai/Mistral-7B-Instruct-v0.3";
   InspectionMode inspection = InspectionMode::kDisabled;
   int inspection_buffer_ms = 150;
+  // INSPECTION_ENDPOINT: remote inspector URL (inline / hybrid / async verdicts come from it instead of the
+  // built-in keyword rules; failures fail open and are counted)
+  std::string inspection_endpoint;
+  int inspection_timeout_ms = 250;
+  int dedupe_window_s = 30;  // DEDUPE_WINDOW_SEC (the bus's duplicate window; 0 = off)
   int keepalive_ms = 15000;          // sse_handler.go:182
   int first_token_timeout_ms = 30000;  // sse_handler.go:395
   size_t max_pending_bytes = 4 << 20;  // per-connection output cap before token frames are dropped
@@ -97,6 +102,7 @@ class RequestQueue {
 
 class IoThread;
 class AsyncInspector;
+class InspectionGate;
 
 class Server {
  public:
@@ -121,6 +127,11 @@ class Server {
   // internal (used by IoThread)
   void submit_chat(ChatRequest r);
   void note_cancel(const std::string& conv_id);
+  // Kill a conversation (chat.<id>.control, chat.control.kill, or an inspection verdict): subscribers get a
+  // terminal `token` frame (done) and the engine a cancellation.  False if it had already ended.
+  bool kill_conversation(const std::string& conv_id, const std::string& token, const std::string& why);
+  // A remote inline / hybrid inspection gate holds frames before fan-out (per-connection inspection off).
+  bool remote_inspection() const { return gate_ != nullptr; }
   // A subscriber of `conv_id` crossed the high-water mark (+1), drained (-1), or the subscriber set
   // changed (0): re-evaluate whether the conversation is paused.
   void flow_update(const std::string& conv_id, int delta);
@@ -142,6 +153,7 @@ class Server {
   std::thread housekeeping_;
   std::unique_ptr<UpstreamRelay> relay_;
   std::shared_ptr<AsyncInspector> inspector_;
+  std::shared_ptr<InspectionGate> gate_;
   std::atomic<bool> running_{false};
   std::atomic<bool> local_engine_{false};
   std::atomic<bool> ready_{true};
@@ -178,6 +190,44 @@ class AsyncInspector : public Sink, public std::enable_shared_from_this<AsyncIns
   std::vector<std::string> killed_;
   bool stop_ = false;
   std::thread thread_;
+  std::unique_ptr<RemoteInspector> remote_;  // INSPECTION_ENDPOINT
+};
+
+// INSPECTION_MODE=inline|hybrid with INSPECTION_ENDPOINT: a bus gate that holds every token frame until the
+// remote inspector's verdict, so one call per token serves every subscriber (the reference's inline hook
+// ran per token per connection).  Workers are sharded by conversation, so each conversation's frames keep
+// their order.  inline: allow -> deliver, redact -> deliver redacted_content, drop -> withhold the token.
+// hybrid: the first INSPECTION_BUFFER_MS of a conversation's tokens are held and inspected as one text;
+// allow -> release them and pass the rest through, redact -> one frame with redacted_content, drop -> kill.
+class InspectionGate : public FrameGate, public std::enable_shared_from_this<InspectionGate> {
+ public:
+  InspectionGate(Server& s, int workers);
+  ~InspectionGate() override;
+  void start();
+  void stop();
+  bool admit(const FramePtr& f) override;
+
+ private:
+  struct Worker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<FramePtr> q;
+    std::thread thread;
+  };
+  struct Held {  // hybrid: per conversation
+    int64_t first_mono = 0;
+    std::vector<FramePtr> frames;
+    bool cleared = false;
+    int64_t last_mono = 0;
+  };
+  void run(Worker& w);
+  void inline_frame(RemoteInspector& ri, const FramePtr& f, std::vector<FramePtr>& out);
+  void hybrid_frame(RemoteInspector& ri, std::unordered_map<std::string, Held>& held, const FramePtr& f,
+                    std::vector<FramePtr>& out);
+  void hybrid_flush(RemoteInspector& ri, const std::string& conv, Held& h, std::vector<FramePtr>& out);
+  Server& srv_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::atomic<bool> stop_{false};
 };
 
 // Stub token generator (BASELINE config 1, CPU plumbing): consumes the request queue and streams

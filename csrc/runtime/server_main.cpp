@@ -37,11 +37,15 @@ int main() {
   }
   c.inspection = parse_inspection_mode(env_str("INSPECTION_MODE", "disabled"));
   c.inspection_buffer_ms = (int)env_long("INSPECTION_BUFFER_MS", 150);
+  c.inspection_endpoint = env_str("INSPECTION_ENDPOINT", "");
+  c.inspection_timeout_ms = (int)env_long("INSPECTION_TIMEOUT_MS", c.inspection_timeout_ms);
+  c.dedupe_window_s = (int)env_long("DEDUPE_WINDOW_SEC", c.dedupe_window_s);
   c.flow_high_water = (size_t)env_long("FLOW_HIGH_WATER", (long)c.flow_high_water);
   const int stub_tokens = (int)env_long("STUB_TOKENS", 50);
   const int stub_delay = (int)env_long("STUB_TOKEN_DELAY_MS", 50);
   c.local_engine = stub_tokens > 0;
   BusConfig bc;
+  bc.dedupe_window_s = c.dedupe_window_s;
   auto bus = std::make_shared<Bus>(bc);
   Server server(c, bus);
   std::string err;

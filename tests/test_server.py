@@ -382,3 +382,206 @@ def test_async_inspection_kills_conversation():
         assert _metric(r, "inspection_redacted_total") == redacted0 + 1
     finally:
         r.stop()
+
+
+# ---------------------------------------------------------------- control subject, dedupe, remote inspector
+def _stream_in_thread(rt, conv, timeout=5, headers=None):
+    got = []
+    th = threading.Thread(target=lambda: got.append(request(H, rt.bound_port("edge"), "GET", f"/stream/{conv}",
+                                                            headers=headers or {}, timeout=timeout)))
+    th.start()
+    time.sleep(0.3)
+    return th, got
+
+
+@pytest.mark.parametrize("how", ["http", "http-kill", "resp", "resp-kill"])
+def test_control_subject_kills_conversation(bare_rt, how):
+    """chat.<id>.control (CHAT_CONTROL stream) and chat.control.kill (the async inspector's kill signal) end a
+    live conversation: subscribers get a terminal [KILLED] frame, the engine a cancellation, and anything the
+    producer still sends is dropped."""
+    conv = f"kill-{how}"
+    th, got = _stream_in_thread(bare_rt, conv)
+    bare_rt.publish(conv, "a", 1, False, 0)
+    bare_rt.publish(conv, "b", 2, False, 0)
+    time.sleep(0.1)
+    if how == "http":
+        r = request(H, bare_rt.bound_port("edge"), "POST", f"/publish/chat.{conv}.control", {"action": "kill"})
+        assert r.status == 200 and json.loads(r.body) == {"status": "killed", "conversation_id": conv}
+    elif how == "http-kill":
+        r = request(H, bare_rt.bound_port("edge"), "POST", "/publish/chat.control.kill", conv.encode())
+        assert json.loads(r.body)["status"] == "killed"
+    else:
+        c = RespClient(H, bare_rt.bound_port("resp"))
+        if how == "resp":
+            assert c.cmd("PUBLISH", f"chat.{conv}.control", "kill") == 1
+        else:
+            assert c.cmd("PUBLISH", "chat.control.kill", json.dumps({"conversation_id": conv})) == 1
+        assert c.cmd("PUBLISH", "chat.control.kill", conv) == 0  # already ended
+        c.close()
+    bare_rt.publish(conv, "late", 3, False, 0)  # the producer had not seen the kill yet
+    th.join(5)
+    toks = tokens_of(got[0])
+    assert [(t["token"], t["sequence"], t["done"]) for t in toks] == [("a", 1, False), ("b", 2, False),
+                                                                     ("[KILLED]", 3, True)]
+    assert conv in bare_rt.pop_cancellations()
+    assert _metric(bare_rt, "control_kills_total") >= 1
+
+
+def test_dedupe_window_and_post_terminal_frames(bare_rt):
+    """A (conversation, sequence) seen within the window is delivered once (at-least-once producers retry);
+    frames after the terminal one are dropped; a new stream restarting at sequence 1 reopens the conversation."""
+    conv = "dup-1"
+    th, got = _stream_in_thread(bare_rt, conv)
+    c = RespClient(H, bare_rt.bound_port("resp"))
+    before = _metric(bare_rt, "bus_duplicates_dropped_total")
+    for seq, tok, done in [(1, "x", False), (1, "x", False), (2, "y", False), (2, "y", False), (3, "[DONE]", True),
+                           (3, "[DONE]", True), (4, "after", False)]:
+        c.cmd("PUBLISH", f"llm:tokens:{conv}", json.dumps({"conversation_id": conv, "token": tok, "sequence": seq,
+                                                           "done": done, "timestamp": time.time_ns()}))
+    th.join(5)
+    assert [(t["token"], t["sequence"]) for t in tokens_of(got[0])] == [("x", 1), ("y", 2), ("[DONE]", 3)]
+    assert _metric(bare_rt, "bus_duplicates_dropped_total") - before == 4
+    # next turn of the same conversation id
+    th, got = _stream_in_thread(bare_rt, conv)
+    bare_rt.publish(conv, "new", 1, False, 0)
+    bare_rt.publish(conv, "[DONE]", 2, True, 0)
+    th.join(5)
+    assert [t["token"] for t in tokens_of(got[0])] == ["new", "[DONE]"]
+    c.close()
+
+
+def test_dedupe_window_can_be_disabled():
+    r = make_rt(dedupe_window_s=0)
+    try:
+        th, got = _stream_in_thread(r, "nodup")
+        r.publish("nodup", "x", 1, False, 0)
+        r.publish("nodup", "x", 1, False, 0)
+        r.publish("nodup", "[DONE]", 2, True, 0)
+        th.join(5)
+        assert [t["token"] for t in tokens_of(got[0])] == ["x", "x", "[DONE]"]
+    finally:
+        r.stop()
+
+
+class _Inspector:
+    """A stand-in for the reference's Spin inspector (POST /inspect, NatsMessage -> InspectionResult):
+    "evil" -> drop, "pw" -> redact, else allow; records every call."""
+
+    def __init__(self, fail=False):
+        import http.server
+
+        calls = self.calls = []
+
+        class Handler(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):
+                pass
+
+            def do_POST(self):
+                body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+                calls.append(body)
+                if fail:
+                    self.send_response(500)
+                    self.send_header("Content-Length", "0")
+                    self.end_headers()
+                    return
+                data = body["data"].lower()
+                if "evil" in data:
+                    res = {"action": "drop", "reason": "evil", "redacted_content": None}
+                elif "pw" in data:
+                    res = {"action": "redact", "reason": "pw", "redacted_content": "[REDACTED]"}
+                else:
+                    res = {"action": "allow", "reason": None, "redacted_content": None}
+                out = json.dumps(res).encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(out)))
+                self.end_headers()
+                self.wfile.write(out)
+
+        self.srv = http.server.ThreadingHTTPServer((H, 0), Handler)
+        self.url = f"http://{H}:{self.srv.server_address[1]}/inspect"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def test_inspection_endpoint_inline_one_call_per_token_for_all_subscribers():
+    insp = _Inspector()
+    r = make_rt(inspection_mode="inline", inspection_endpoint=insp.url)
+    try:
+        d0, r0 = _metric(r, "inspection_dropped_total"), _metric(r, "inspection_redacted_total")
+        conv = "remote-inline"
+        a = _stream_in_thread(r, conv)
+        b = _stream_in_thread(r, conv)
+        for i, tok in enumerate(["hello", "my pw is x", "evil plan", "bye"]):
+            r.publish(conv, tok, i + 1, False, 0)
+        r.publish(conv, "[DONE]", 5, True, 0)
+        for th, got in (a, b):
+            th.join(5)
+            assert [t["token"] for t in tokens_of(got[0])] == ["hello", "[REDACTED]", "bye", "[DONE]"]
+        # one remote call per token (not per subscriber), the reference's NatsMessage shape
+        assert len(insp.calls) == 4
+        assert insp.calls[0] == {"subject": f"chat.{conv}.tokens", "data": "hello", "sequence": 1,
+                                 "timestamp": insp.calls[0]["timestamp"]}
+        assert _metric(r, "inspection_dropped_total") - d0 == 1 and _metric(r, "inspection_redacted_total") - r0 == 1
+    finally:
+        r.stop()
+        insp.close()
+
+
+def test_inspection_endpoint_hybrid_inspects_the_buffered_text_and_kills():
+    insp = _Inspector()
+    r = make_rt(inspection_mode="hybrid", inspection_endpoint=insp.url, inspection_buffer_ms=200)
+    r.set_local_engine(True)
+    try:
+        th, got = _stream_in_thread(r, "hyb-ok")
+        th2, got2 = _stream_in_thread(r, "hyb-bad")
+        for i, tok in enumerate(["all ", "good ", "here"]):
+            r.publish("hyb-ok", tok, i + 1, False, 0)
+            r.publish("hyb-bad", ["ev", "il ", "scheme"][i], i + 1, False, 0)
+        time.sleep(0.5)  # the buffer window passes: one verdict per conversation on the joined text
+        r.publish("hyb-ok", "after", 4, False, 0)
+        r.publish("hyb-ok", "[DONE]", 5, True, 0)
+        th.join(5)
+        th2.join(5)
+        assert [t["token"] for t in tokens_of(got[0])] == ["all ", "good ", "here", "after", "[DONE]"]
+        bad = tokens_of(got2[0])
+        assert [(t["token"], t["done"]) for t in bad] == [("[BLOCKED]", True)]  # nothing of it reached clients
+        assert "hyb-bad" in r.pop_cancellations()
+        assert sorted(c["data"] for c in insp.calls) == ["all good here", "evil scheme"]
+    finally:
+        r.stop()
+        insp.close()
+
+
+def test_inspection_endpoint_failure_fails_open_and_async_uses_it():
+    insp = _Inspector(fail=True)
+    r = make_rt(inspection_mode="inline", inspection_endpoint=insp.url)
+    try:
+        e0 = _metric(r, "inspection_remote_errors_total")
+        th, got = _stream_in_thread(r, "failopen")
+        r.publish("failopen", "evil but unchecked", 1, False, 0)
+        r.publish("failopen", "[DONE]", 2, True, 0)
+        th.join(5)
+        assert [t["token"] for t in tokens_of(got[0])] == ["evil but unchecked", "[DONE]"]
+        assert _metric(r, "inspection_remote_errors_total") - e0 == 1
+    finally:
+        r.stop()
+        insp.close()
+    insp = _Inspector()
+    r = make_rt(inspection_mode="async", inspection_endpoint=insp.url)
+    r.set_local_engine(True)
+    try:
+        th, got = _stream_in_thread(r, "async-remote")
+        r.publish("async-remote", "fine", 1, False, 0)
+        r.publish("async-remote", "evil", 2, False, 0)
+        th.join(5)
+        toks = tokens_of(got[0])
+        assert toks[-1]["token"] == "[BLOCKED]" and toks[-1]["done"]
+        assert "async-remote" in r.pop_cancellations()
+    finally:
+        r.stop()
+        insp.close()
