@@ -108,8 +108,8 @@ def _rms(x, w, eps):
 
 def _rope(x, pos, theta):
     D = x.shape[-1]
-    inv = theta ** (-torch.arange(0, D, 2, dtype=torch.float64) / D)
-    ang = pos.double()[:, None] * inv[None, :]
+    inv = theta ** (-torch.arange(0, D, 2, dtype=torch.float64, device=x.device) / D)
+    ang = pos.to(x.device).double()[:, None] * inv[None, :]
     cos, sin = ang.cos().float()[:, None, :], ang.sin().float()[:, None, :]
     x1, x2 = x[..., : D // 2], x[..., D // 2:]
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
@@ -126,7 +126,7 @@ def reference_forward(cfg: MistralConfig, w, ids: torch.Tensor, positions: torch
     D, Hq, Hkv = cfg.head_dim, cfg.num_heads, cfg.num_kv_heads
     start = 0 if not kv else kv[0][0].shape[0]
     if positions is None:
-        positions = torch.arange(start, start + T)
+        positions = torch.arange(start, start + T, device=ids.device)
     x = w["embed"][ids.long()].float()
     new_kv = []
     for li, L in enumerate(w["layers"]):
@@ -143,7 +143,7 @@ def reference_forward(cfg: MistralConfig, w, ids: torch.Tensor, positions: torch
         kk = k.repeat_interleave(cfg.group, dim=1)
         vv = v.repeat_interleave(cfg.group, dim=1)
         s = torch.einsum("qhd,khd->hqk", q, kk) / math.sqrt(D)
-        mask = torch.arange(S)[None, :] > (torch.arange(S - T, S))[:, None]
+        mask = torch.arange(S, device=x.device)[None, :] > (torch.arange(S - T, S, device=x.device))[:, None]
         s = s.masked_fill(mask[None], float("-inf"))
         o = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), vv).reshape(T, Hq * D)
         x = x + o @ L["o"].float().t()

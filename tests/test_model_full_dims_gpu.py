@@ -1,0 +1,91 @@
+"""Whole-model numerics at the real Mistral-7B dimensions (H 4096, F 14336, 32 / 8 heads, vocab 32768; two
+layers to keep the fp32 oracle fast): the full fp32 logits of the graph-captured decode step, at every decode
+path the engine picks by batch bucket (skinny 1, X-streaming 64, wide 128, hipBLASLt + wide 192 / 256), after
+plain and chunked prefill, against ``models/mistral.py:reference_forward`` of the same weights.
+
+The criterion is on whole logits rows (cosine similarity and max-abs error relative to the row's scale), not on
+the sampled token: an O(1)-wrong sub-stage shows up here even when the argmax survives it.
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
+from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+from distributed_sse_for_llm_response_amd.models.mistral import MistralConfig, init_standard_weights, reference_forward
+
+pytestmark = pytest.mark.gpu
+
+CFG = MistralConfig(name="mistral-7b-dims-2l", num_layers=2)  # every dimension of v0.3, two layers
+BUCKETS = [1, 64, 128, 192, 256]
+PAGES_PER_SEQ = 3  # prompts <= 60 tokens + 2 generated < 96
+
+
+@pytest.fixture(scope="module")
+def model():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distributed_sse_for_llm_response_amd import ops
+
+    ops.load_library(required=True)
+    gpu = torch.device("cuda", 0)
+    std = init_standard_weights(CFG, seed=3, device=gpu)
+    w = convert_standard(CFG, std, device=gpu)
+    r = ModelRunner(w, num_blocks=256 * PAGES_PER_SEQ + 8, max_batch=256, max_model_len=512, device=gpu)
+    r.capture(BUCKETS)  # before any prefill: the warm-up pass writes no KV (every slot inactive)
+    return std, r
+
+
+def _compare(ref_row, got_row, what):
+    ref_row, got_row = ref_row.float(), got_row.float()
+    cos = torch.nn.functional.cosine_similarity(ref_row, got_row, dim=0).item()
+    rel = ((ref_row - got_row).abs().max() / ref_row.abs().max()).item()
+    assert cos > 0.998 and rel < 0.05, f"{what}: cosine {cos:.5f}, max-abs err / max {rel:.4f}"
+    return cos, rel
+
+
+@pytest.mark.parametrize("B", BUCKETS)
+def test_full_dims_decode_logits_match_reference(model, gpu, B):
+    std, r = model
+    g = torch.Generator().manual_seed(B)
+    prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
+               for _ in range(B)]
+    tables = [list(range(i * PAGES_PER_SEQ, (i + 1) * PAGES_PER_SEQ)) for i in range(B)]
+    r.block_tables.zero_()
+    for i, bt in enumerate(tables):
+        r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    # every other sequence of a multi-sequence bucket is prefilled in two chunks (chunked prefill)
+    first, second = [], []
+    for i, p in enumerate(prompts):
+        if B > 1 and i % 2 == 1 and len(p) > 16:
+            first.append(PrefillSeq(i, p[:16], 0, tables[i], False))
+            second.append(PrefillSeq(i, p[16:], 16, tables[i], True))
+        else:
+            first.append(PrefillSeq(i, p, 0, tables[i], True))
+    for batch in (first, second):  # at most 64 sequences (<= 3840 tokens) per prefill call
+        for k in range(0, len(batch), 64):
+            r.prefill(batch[k:k + 64], ring_row=0)
+    r.active.zero_()
+    r.active[:B] = 1
+    r.temperature.zero_()  # greedy
+    gen = [[int(t)] for t in r.ids[:B].cpu()]
+    logits = []
+    for _ in range(2):
+        r.decode(B)
+        torch.cuda.synchronize()
+        logits.append(r.logits[:B].clone())
+        for i, t in enumerate(r.ids[:B].cpu()):
+            gen[i].append(int(t))
+    worst_cos, worst_rel = 1.0, 0.0
+    for i in range(B):
+        ids = torch.tensor(prompts[i] + gen[i][:2], device=gpu)
+        ref, _ = reference_forward(CFG, std, ids)
+        L = len(prompts[i])
+        # the prefill's sampled token is the argmax of the reference's last prompt row (up to near-ties)
+        assert float(ref[L - 1].max() - ref[L - 1, gen[i][0]]) < 0.02 * float(ref[L - 1].abs().max()), f"seq {i}"
+        for s in range(2):
+            c, e = _compare(ref[L + s], logits[s][i], f"bucket {B} seq {i} step {s}")
+            worst_cos, worst_rel = min(worst_cos, c), max(worst_rel, e)
+    print(f"bucket {B}: worst cosine {worst_cos:.6f}, worst max-abs / max {worst_rel:.4f}")
+    assert not math.isnan(worst_cos)
