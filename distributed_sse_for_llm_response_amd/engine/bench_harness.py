@@ -66,7 +66,11 @@ class PacedStubEngine:
         self.next_t = 0.0
         self.started = False
 
-    def add_request(self, conversation_id, prompt, params, arrival_ns=0):
+    def next_rid(self) -> int:
+        self._rid = getattr(self, "_rid", 0) + 1
+        return self._rid
+
+    def add_request(self, conversation_id, prompt, params, arrival_ns=0, rid=None):
         free = self.slots.index(None)
         self.slots[free] = self._Seq(conversation_id, params.max_tokens)
 
@@ -98,16 +102,16 @@ class PacedStubEngine:
 
 
 def _build_runner(model: str, device, streams: int, prompt_len: int, total_steps: int, tp: int, use_graphs: bool,
-                  rank: int, world: int):
-    cfg = get_config(model) if device.type == "cuda" else TINY
-    comm = TPComm()
-    if tp > 1:
-        import torch.distributed as dist
+                  rank: int, world: int, comm: TPComm | None = None):
+    # on CPU the 7B architecture is replaced by the tiny one (plumbing runs); named small configs are kept
+    cfg = get_config(model) if device.type == "cuda" or not model.startswith("mistral-7b") else TINY
+    if comm is None:
+        comm = TPComm()
+        if tp > 1:
+            from ..parallel.comm import make_groups
 
-        from ..parallel.comm import make_groups
-
-        grp, _ = make_groups(world, tp)
-        comm = TPComm(rank=rank % tp, size=tp, group=grp)
+            grp, _ = make_groups(world, tp)
+            comm = TPComm(rank=rank % tp, size=tp, group=grp)
     w = random_engine_weights(cfg, tp_rank=comm.rank, tp_size=comm.size, device=device, seed=1234)
     max_len = prompt_len + total_steps + 2 * PAGE
     nblk = streams * (blocks_needed(max_len) + 1) + 4
@@ -207,8 +211,10 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     rank 0) -> native runtime + data-parallel router on rank 0 -> shared-memory ring -> this rank's LLMEngine
     (scheduler, hipGraph decode, token-ring drain) -> ring -> router -> bus -> epoll writers -> sockets.
 
-    Every rank is one replica (tp == 1) and serves the `streams` conversations the router assigns it.
-    Timed: exactly `steps` engine steps on every rank once all of its streams are decoding, bracketed by
+    Every TP group of `tp` ranks is one replica (tp == 1: every rank) and serves the `streams` conversations
+    the router assigns it; inside a group the leader drives its followers with per-step plans
+    (serving/tp.py), and the decode step's all-reduces / all-gather run over the group's communicator.
+    Timed: exactly `steps` engine steps on every replica once all of its streams are decoding, bracketed by
     barrier + device synchronize.  The p50 inter-token latency is measured by the client (socket receive
     times of consecutive tokens of a stream) inside the timed window."""
     import json as _json
@@ -218,25 +224,47 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     from ..models.tokenizer import SyntheticTokenizer, prompt_for_request
     from .engine import LLMEngine, SamplingParams
 
-    if tp != 1:
-        raise ValueError("serving bench: data-parallel replicas only (tp=1); use --delivery frame for TP")
+    from ..serving.tp import PlanChannel, TPLeader, follower_loop, make_tp_groups
+
     device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    if world % tp:
+        raise ValueError(f"world size {world} is not a multiple of tp={tp}")
+    replicas, group, leader = world // tp, rank // tp, (rank // tp) * tp
+    comm, plan_ch = TPComm(), None
+    if tp > 1:
+        import torch.distributed as dist
+
+        tp_group, plan_group, group, leader = make_tp_groups(world, tp, dist.get_backend())
+        comm = TPComm(rank=rank - leader, size=tp, group=tp_group)
+        plan_ch = PlanChannel(plan_group, leader)
     # Admission prefills ~max_prefill_tokens of prompts per engine step while the already admitted streams
     # decode, so the first streams run ahead by up to `skew` steps.  Every stream must stay live through
     # the whole timed window (full batch on every timed step): budget the tokens and the KV for it.
     skew = math.ceil(streams * (prompt_len + 16) / 8192) + 4
     total = steps + warmup + skew
+    if stub_step_ms > 0 and tp > 1:
+        raise ValueError("the paced-stub rehearsal stands in for whole replicas (tp=1)")
     if stub_step_ms > 0:  # host-path rehearsal: paced stub replicas, no model
         cfg = get_config(model)
         tok = SyntheticTokenizer(cfg.vocab_size)
         engine = PacedStubEngine(streams, stub_step_ms, cfg.vocab_size)
     else:
-        cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world)
+        cfg, r = _build_runner(model, device, streams, prompt_len + 16, total + 4, tp, use_graphs, rank, world, comm)
         if use_graphs and device.type == "cuda":
             r.capture()
         tok = SyntheticTokenizer(cfg.vocab_size)
         engine = LLMEngine(r, eos_id=tok.eos_id, prefill_budget=r.max_prefill_tokens,
                            default_params=SamplingParams(temperature=1.0, top_p=1.0, max_tokens=total + 2))
+    if rank != leader:  # a TP follower: mirror the leader's plans (its syncs included) until it stops
+        follower_loop(engine, plan_ch, on_sync=lambda: _sync(device, world))
+        _sync(device, world)
+        return {"elapsed_s": 0.0, "p50_itl_ms": 0.0, "p99_itl_ms": 0.0, "delivered_in_window": None,
+                "client_errors": [], "model": cfg.name, "max_context": prompt_len + 16 + total}
+    drv = TPLeader(engine, plan_ch)
+
+    def sync():
+        drv.sync()
+        _sync(device, world)
     mod = rt_mod.load()
     prefix = f"/dsse-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid() if world > 1 else os.getpid()}"
     runtime = None
@@ -244,16 +272,16 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
         runtime = mod.Runtime({"host": "127.0.0.1", "sse_port": 0, "origin_port": -1, "metrics_port": -1,
                                "resp_port": -1, "io_threads": 4, "local_engine": True})
         runtime.set_vocab(tok.pieces())
-        runtime.start_dp_router(prefix, world, 4, 600_000)  # 4 MiB rings: /dev/shm may be small in containers
+        runtime.start_dp_router(prefix, replicas, 4, 600_000)  # 4 MiB rings: /dev/shm may be small in containers
         runtime.start()
-    chan = mod.DpWorker(prefix, rank, 600_000)
+    chan = mod.DpWorker(prefix, group, 600_000)
     chan.set_ready(True)
     if rank == 0:
-        while sum(1 for i in runtime.dp_workers() if i["ready"]) < world:
+        while sum(1 for i in runtime.dp_workers() if i["ready"]) < replicas:
             time.sleep(0.01)
         words = [f"w{i % 997}" for i in range(max(1, prompt_len - 8))]
         client.stdin.write(_json.dumps({"host": "127.0.0.1", "port": runtime.bound_port("edge"),
-                                        "streams": streams * world, "message": " ".join(words),
+                                        "streams": streams * replicas, "message": " ".join(words),
                                         "max_tokens": total + 2, "prefix": "bench-"}) + "\n")
         client.stdin.flush()
 
@@ -265,8 +293,10 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     def pump(block_ms=0):
         for req in chan.poll_requests(1024, block_ms):
             p = SamplingParams(temperature=1.0, top_p=1.0, max_tokens=req["max_tokens"], ignore_eos=True)
-            engine.add_request(req["conversation_id"], prompt_for_request(tok, req), p,
-                               arrival_ns=req["arrival_ns"])
+            drv.add(req["conversation_id"], prompt_for_request(tok, req), p, req["arrival_ns"])
+
+    def step():
+        return drv.step(run=engine.has_work() or bool(drv.plan.adds))
 
     import gc
 
@@ -277,31 +307,32 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     t_admit = time.time()
     while sum(1 for s in engine.slots if s is not None and s.state == "decode") < streams:
         pump(20 if not engine.has_work() else 0)
-        if engine.has_work():
-            publish(engine.step())
+        if engine.has_work() or drv.plan.adds:
+            publish(step())
         if time.time() - t_admit > 900:
             raise RuntimeError("bench: streams did not all start decoding")
-    _sync(device, world)
+    sync()
     for _ in range(warmup):
-        publish(engine.step())
-    _sync(device, world)
+        publish(step())
+    sync()
     t0_ns = time.time_ns()
     t0 = time.perf_counter()
     for _ in range(steps):
-        publish(engine.step())
-    _sync(device, world)
+        publish(step())
+    sync()
     elapsed = time.perf_counter() - t0
     t1_ns = time.time_ns()
     if live() < streams:
         raise RuntimeError(f"bench: only {live()} of {streams} streams were still decoding at the end of the window")
     while engine.has_work():
-        publish(engine.step())
+        publish(step())
+    drv.stop()
     res = {"arrivals": [], "errors": []}
     if rank == 0:
         out = client.stdout.readline()
         client.wait(timeout=300)
         res = _json.loads(out) if out.strip() else {"arrivals": [], "errors": ["client produced no output"]}
-    _sync(device, world)
+    _sync(device, world)  # the followers' last sync (after their loop's stop)
     if runtime is not None:
         runtime.stop()
     by_stream = {}

@@ -120,7 +120,7 @@ class _Drain:
 class LLMEngine:
     def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 2048,
                  idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
-                 pipeline_depth: int | None = None, max_pause_s: float = 30.0):
+                 pipeline_depth: int | None = None, max_pause_s: float = 30.0, deterministic: bool | None = None):
         self.r = runner
         self.eos_id = eos_id
         self.alloc = BlockAllocator(runner.kv.num_blocks)
@@ -131,6 +131,9 @@ class LLMEngine:
         # of up to one step time is absorbed instead of idling the GPU; tokens surface one step later
         self.depth = pipeline_depth if pipeline_depth is not None else int(os.environ.get("DSSE_PIPELINE_DEPTH", "2"))
         self.max_pause_s = max_pause_s
+        # TP groups (serving/tp.py): every rank must consume drained steps at the same engine step, so the
+        # count decides (len(inflight) - depth), never whether this rank's copy event has completed yet
+        self.deterministic = runner.comm.size > 1 if deterministic is None else deterministic
         self.waiting: deque = deque()
         self.slots: list = [None] * runner.max_batch
         self.by_conv: dict = {}
@@ -146,14 +149,19 @@ class LLMEngine:
         self.on_itl = None
 
     # ------------------------------------------------------------------ requests
+    def next_rid(self) -> int:
+        return next(self._rid)
+
     def add_request(self, conversation_id: str, prompt: list, params: SamplingParams | None = None,
-                    arrival_ns: int | None = None) -> Sequence:
+                    arrival_ns: int | None = None, rid: int | None = None) -> Sequence:
+        """Queue a request.  `rid` (a TP leader's request id, replayed on its followers) seeds the sampling RNG
+        when the params carry no seed, so it must be the same on every rank of a TP group."""
         p = params or self.default_params
         max_prompt = self.r.max_model_len - 1
         if len(prompt) > max_prompt:
             prompt = prompt[-max_prompt:]  # keep the tail (most recent context)
-        s = Sequence(rid=next(self._rid), conversation_id=conversation_id, prompt=list(prompt), params=p,
-                     arrival_ns=arrival_ns or time.time_ns())
+        s = Sequence(rid=next(self._rid) if rid is None else rid, conversation_id=conversation_id,
+                     prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns())
         self.waiting.append(s)
         self.by_conv[conversation_id] = s
         return s
@@ -351,9 +359,7 @@ class LLMEngine:
         while self.inflight:
             st, rrow, prods, tq = self.inflight[0]
             must = len(self.inflight) > self.depth or not ran
-            if not must and not self.drain.ready(rrow):
-                break
-            if not must and not block:
+            if not must and (self.deterministic or not block or not self.drain.ready(rrow)):
                 break
             toks = self.drain.wait(rrow)
             self.inflight.popleft()

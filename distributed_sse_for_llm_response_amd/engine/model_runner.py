@@ -253,10 +253,51 @@ class ModelRunner:
                 return b
         return self.max_batch
 
+    def _collectives_capturable(self) -> tuple:
+        """TP>1 startup self-check: an all-reduce captured into a graph and replayed must produce the sum on
+        every rank.  Decided by all ranks together (an eager MIN of the local verdicts), so either every rank
+        captures its decode step or every rank runs it eagerly -- the collectives stay matched."""
+        import torch.distributed as dist
+
+        ok, why = True, ""
+        try:
+            t = torch.ones(8, device=self.device, dtype=torch.float32)
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self.comm.all_reduce(t)  # warm the communicator outside capture
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.comm.all_reduce(t)
+            t.fill_(1.0)
+            g.replay()
+            torch.cuda.synchronize(self.device)
+            if not torch.all(t == float(self.comm.size)):
+                ok, why = False, f"replayed all-reduce gave {t.tolist()}"
+        except Exception as e:  # noqa: BLE001 - the reason is logged, decode then runs eagerly
+            ok, why = False, f"{type(e).__name__}: {e}"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+        if dist.get_backend(self.comm.group) == "gloo":
+            flag = flag.cpu()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.comm.group)
+        if ok and int(flag.item()) == 0:
+            why = "another rank of the TP group cannot capture its collectives"
+        return int(flag.item()) == 1, why
+
     def capture(self, buckets=None) -> None:
-        """Capture the decode step of each batch bucket into its own graph (shared memory pool)."""
+        """Capture the decode step of each batch bucket into its own graph (shared memory pool).  With TP > 1
+        the collectives are captured too, after a self-check (fallback: eager decode, reason logged)."""
         if not self.use_graphs:
             return
+        if self.comm.size > 1:
+            ok, why = self._collectives_capturable()
+            if not ok:
+                print(f"[engine] TP rank {self.comm.rank}: decode graphs disabled, collectives not capturable "
+                      f"({why}); decoding eagerly", flush=True)
+                self.use_graphs = False
+                return
         buckets = buckets or batch_buckets(self.max_batch)
         # Warm up on a side stream (allocator + library init) before capture.
         s = torch.cuda.Stream(self.device)

@@ -62,7 +62,11 @@ TINY = MistralConfig(name="mistral-tiny", vocab_size=2048, hidden_size=1024, int
 SMALL = MistralConfig(name="mistral-small", vocab_size=8192, hidden_size=2048, intermediate_size=5632, num_layers=4,
                       num_heads=16, num_kv_heads=4, max_position=8192)
 
-CONFIGS = {c.name: c for c in (MISTRAL_7B_V03, TINY, SMALL)}
+# Eight KV heads (one per rank at TP=8, as Mistral-7B) at toy width: the CPU rehearsal model of TP=8 / DP x TP.
+TINY_KV8 = MistralConfig(name="mistral-tiny-kv8", vocab_size=2048, hidden_size=2048, intermediate_size=2048,
+                         num_layers=2, num_heads=16, num_kv_heads=8, max_position=4096)
+
+CONFIGS = {c.name: c for c in (MISTRAL_7B_V03, TINY, SMALL, TINY_KV8)}
 CONFIGS["mistral-7b"] = MISTRAL_7B_V03
 
 

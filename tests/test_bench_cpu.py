@@ -66,3 +66,25 @@ def test_bench_host_path_rehearsal_with_paced_stubs():
     assert d["config"]["global_batch"] == 64 and d["client_errors"] == []
     assert 4.5 < d["ms_per_step"] < 8.0, d
     assert d["tokens_delivered_in_window"] >= 0.9 * 64 * 32, d
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,tp", [(2, 2), (8, 8), (8, 4)])
+def test_bench_tensor_parallel_serving_path(world, tp):
+    """bench.py with --tp over the serving path: `world / tp` replicas of `tp` ranks each (TP=8 is config 4's
+    degree; 8 = DP2 x TP4), leaders driving followers by plan broadcasts, collectives over gloo; one valid
+    JSON line with every token of every stream delivered through the router, bus and SSE."""
+    args = ["bench.py", "--gpus", str(world), "--tp", str(tp), "--steps", "3", "--warmup", "1", "--streams", "3",
+            "--prompt-len", "24", "--model", "mistral-tiny-kv8"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=840)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    replicas = world // tp
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"dp{replicas}xtp{tp}"
+    assert d["config"]["global_batch"] == 3 * replicas and d["client_errors"] == []
+    assert d["tokens_delivered_in_window"] >= 3 * replicas * 2

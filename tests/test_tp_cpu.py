@@ -170,3 +170,129 @@ def test_serve_tp2_cpu_end_to_end():
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+def _serve_torchrun(nproc, extra, sse, met):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                             "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                             "-m", "distributed_sse_for_llm_response_amd", "serve", "--engine", "cpu", *extra,
+                             "--host", "127.0.0.1", "--sse-port", str(sse), "--origin-port", "-1",
+                             "--metrics-port", str(met), "--max-tokens", "6", "--temperature", "0"],
+                            cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def _wait_ready(p, sse, what):
+    import time
+
+    from distributed_sse_for_llm_response_amd.utils.sse_client import request
+
+    deadline = time.time() + 300
+    while time.time() < deadline and p.poll() is None:
+        try:
+            if request("127.0.0.1", sse, "GET", "/readyz", timeout=2).status == 200:
+                return
+        except OSError:
+            pass
+        time.sleep(0.5)
+    raise AssertionError(p.stdout.read() if p.poll() is not None else f"{what} server never became ready")
+
+
+REQS = [{"message": "same prompt", "conversation_id": "g0"},
+        {"message": "a different prompt here", "conversation_id": "g1"},
+        {"message": "sampled one", "conversation_id": "s0", "temperature": 1.0, "seed": 7},
+        {"message": "sampled two", "conversation_id": "s1", "temperature": 0.8, "seed": 11},  # unfiltered: TP-invariant
+        {"message": "same prompt", "conversation_id": "g2"}]
+
+
+def _streams(sse):
+    import threading
+
+    from distributed_sse_for_llm_response_amd.utils.sse_client import request
+
+    outs = {}
+
+    def one(body):
+        r = request("127.0.0.1", sse, "POST", "/chat", body, timeout=180)
+        outs[body["conversation_id"]] = [(e.json()["token"], e.json()["sequence"]) for e in r.events
+                                         if e.event == "token"]
+
+    ts = [threading.Thread(target=one, args=(b,)) for b in REQS]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(180)
+    return outs
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("extra", [["--tp", "8"], ["--tp", "4", "--dp", "2"]])
+def test_serve_tp8_and_dp2xtp4_token_streams_equal_tp1(extra):
+    """Serving path at BASELINE config 4's TP degree (8 ranks, one KV head each) and as DP2 x TP4 (two replicas
+    behind the router, each led by its first rank): greedy and seeded-sampled token streams equal a TP=1
+    single-process server on the same model."""
+    import subprocess
+
+    from distributed_sse_for_llm_response_amd.serving.app import ServingApp
+    from distributed_sse_for_llm_response_amd.serving.config import ServeConfig
+
+    ref_cfg = ServeConfig(host="127.0.0.1", sse_port=0, origin_port=-1, metrics_port=0, engine="cpu",
+                          model="mistral-tiny-kv8", max_tokens=6, temperature=0.0)
+    app = ServingApp(ref_cfg).start()
+    try:
+        expect = _streams(app.port("edge"))
+    finally:
+        app.stop()
+    assert all(v and v[-1][0] == "[DONE]" for v in expect.values()), expect
+    assert expect["g0"] == expect["g2"]
+    sse, met = _free_port(), _free_port()
+    p = _serve_torchrun(8, ["--model", "mistral-tiny-kv8", *extra], sse, met)
+    try:
+        _wait_ready(p, sse, " ".join(extra))
+        got = _streams(sse)
+        assert got == expect, (got, expect)
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+def test_deterministic_engines_agree_whatever_the_drain_readiness():
+    """TP ranks consume drained steps by count, never by their own copy events: two engines fed the same plans,
+    whose drains report random (different) readiness, keep identical slots and emit identical events."""
+    import random
+
+    from distributed_sse_for_llm_response_amd.engine.engine import LLMEngine, SamplingParams
+
+    def engine(seed):
+        std = init_standard_weights(TINY, seed=3)
+        w = convert_standard(TINY, std)
+        r = ModelRunner(w, num_blocks=128, max_batch=4, max_model_len=256, device="cpu", use_graphs=False)
+        e = LLMEngine(r, eos_id=-1, prefill_budget=64, deterministic=True)
+        rng = random.Random(seed)
+        e.drain.ready = lambda row: rng.random() < 0.5
+        return e
+
+    a, b = engine(1), engine(2)
+    trace = {id(a): [], id(b): []}
+    for step in range(40):
+        for e in (a, b):
+            if step in (0, 3, 9):
+                for k in range(2):
+                    e.add_request(f"c{step}-{k}", list(range(5 + step + k)), SamplingParams(temperature=0.0,
+                                                                                         max_tokens=4 + k), rid=100 + 10 * step + k)
+            if step == 12:
+                e.abort("c9-1")
+            ev = e.step()
+            trace[id(e)].append(([s.rid if s is not None else None for s in e.slots],
+                                 [(x.conversation_id, x.token_id, x.sequence, x.done) for x in ev]))
+    assert trace[id(a)] == trace[id(b)]
+    assert any(ev for _, ev in trace[id(a)])
