@@ -117,6 +117,7 @@ def main():
             "delivery": args.delivery,
             "tokens_delivered_in_window": res.get("delivered_in_window"),
             "client_errors": res.get("client_errors", []),
+            "stalls": res.get("stalls", {}),
             "config": {"model": res.get("model", args.model), "global_batch": total_streams, "seq_len": res.get("max_context", args.prompt_len + args.steps + args.warmup),
                        "prompt_len": args.prompt_len,
                        "parallelism": f"dp{replicas}" + (f"xtp{args.tp}" if args.tp > 1 else "")},

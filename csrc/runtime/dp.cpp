@@ -301,6 +301,8 @@ void DpRouter::drain_loop(int w) {
       for (int32_t k = 0; k < nt && rd.good(); ++k) metrics().engine_ttft_seconds.observe(rd.f64());
       const int32_t ni = rd.i32();
       for (int32_t k = 0; k < ni && rd.good(); ++k) metrics().engine_itl_seconds.observe(rd.f64());
+      const int32_t nh = rd.good() ? rd.i32() : 0;
+      for (int32_t k = 0; k < nh && rd.good(); ++k) metrics().engine_host_step_seconds.observe(rd.f64());
       if (step_s > 0) metrics().engine_decode_step_seconds.observe(step_s);
       double batch = 0, kv = 0, active = 0;
       for (auto& x : info_) {
@@ -400,7 +402,7 @@ void DpWorker::bye() {
 }
 
 void DpWorker::stats(double step_s, double batch, double kv_free, double active, const std::vector<double>& ttft,
-                     const std::vector<double>& itl) {
+                     const std::vector<double>& itl, const std::vector<double>& host) {
   dpwire::Writer m;
   m.u8(dpwire::kStats);
   m.f64(step_s);
@@ -411,6 +413,8 @@ void DpWorker::stats(double step_s, double batch, double kv_free, double active,
   for (double v : ttft) m.f64(v);
   m.i32((int32_t)itl.size());
   for (double v : itl) m.f64(v);
+  m.i32((int32_t)host.size());
+  for (double v : host) m.f64(v);
   send(m.data());
 }
 

@@ -152,7 +152,7 @@ class DpWorker {
   void hello();
   void bye();
   void stats(double step_s, double batch, double kv_free, double active, const std::vector<double>& ttft,
-             const std::vector<double>& itl);
+             const std::vector<double>& itl, const std::vector<double>& host = {});
 
  private:
   void heartbeat_if_due();

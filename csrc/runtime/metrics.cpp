@@ -52,7 +52,8 @@ Metrics::Metrics()
       sse_delivery_latency_seconds({0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.5}),
       engine_decode_step_seconds({0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.015, 0.02, 0.03, 0.05, 0.1}),
       engine_ttft_seconds({0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10}),
-      engine_itl_seconds({0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.015, 0.02, 0.03, 0.05, 0.1}) {}
+      engine_itl_seconds({0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.015, 0.02, 0.03, 0.05, 0.1}),
+      engine_host_step_seconds({0.0001, 0.0002, 0.0005, 0.001, 0.002, 0.003, 0.005, 0.01, 0.02, 0.05, 0.1}) {}
 
 namespace {
 void line(std::string& out, const char* name, const char* help, const char* type, double v) {
@@ -125,6 +126,8 @@ std::string Metrics::render() const {
   hist(o, "engine_decode_step_seconds", "Engine decode step latency", engine_decode_step_seconds);
   hist(o, "engine_ttft_seconds", "Time to first token", engine_ttft_seconds);
   hist(o, "engine_itl_seconds", "Inter-token latency", engine_itl_seconds);
+  hist(o, "engine_host_step_seconds", "Host time of an engine step (scheduling, launches, token processing; drain waits excluded)",
+       engine_host_step_seconds);
   line(o, "dp_workers_alive", "Data-parallel engine workers with a live heartbeat", "gauge", dp_workers_alive.get());
   line(o, "dp_requests_routed_total", "Chat requests routed to data-parallel engine workers", "counter",
        dp_requests_routed_total.get());

@@ -81,6 +81,7 @@ class Metrics {
   Histogram engine_decode_step_seconds;
   Histogram engine_ttft_seconds;
   Histogram engine_itl_seconds;
+  Histogram engine_host_step_seconds;  // host (Python + launch) time of an engine step, drain waits excluded
   // data-parallel router (dp.h)
   Gauge dp_workers_alive;
   Counter dp_requests_routed_total;

@@ -259,9 +259,9 @@ class DpWorkerPy {
     else w_->bye();
   }
   void observe(double step_s, double batch, double kv_free, double active, const std::vector<double>& ttft,
-               const std::vector<double>& itl) {
+               const std::vector<double>& itl, const std::vector<double>& host) {
     py::gil_scoped_release nogil;
-    w_->stats(step_s, batch, kv_free, active, ttft, itl);
+    w_->stats(step_s, batch, kv_free, active, ttft, itl, host);
   }
   void set_vocab(const std::vector<std::string>&) {}  // text is resolved by the router
 
@@ -315,7 +315,8 @@ PYBIND11_MODULE(_dsse_runtime, m) {
            py::arg("texts") = std::vector<std::string>{}, py::arg("finish") = std::vector<int>{},
            py::arg("prompt_tokens") = std::vector<int>{})
       .def("set_ready", &DpWorkerPy::set_ready)
-      .def("observe", &DpWorkerPy::observe)
+      .def("observe", &DpWorkerPy::observe, py::arg("step_s"), py::arg("batch"), py::arg("kv_free"), py::arg("active"),
+           py::arg("ttft"), py::arg("itl"), py::arg("host") = std::vector<double>{})
       .def("set_vocab", &DpWorkerPy::set_vocab);
   m.def("dp_ring_name", &dp_ring_name);
 
@@ -345,11 +346,12 @@ PYBIND11_MODULE(_dsse_runtime, m) {
     return d;
   });
   m.def("inspection_json", [](const std::string& content) { return inspection_result_json(inspect_message(content)); });
-  m.def("engine_observe", [](double step_s, double batch, double kv_free) {
+  m.def("engine_observe", [](double step_s, double batch, double kv_free, double host_s) {
     if (step_s > 0) metrics().engine_decode_step_seconds.observe(step_s);
+    if (host_s >= 0) metrics().engine_host_step_seconds.observe(host_s);
     metrics().engine_batch_size.set(batch);
     metrics().engine_kv_blocks_free.set(kv_free);
-  });
+  }, py::arg("step_s"), py::arg("batch"), py::arg("kv_free"), py::arg("host_s") = -1.0);
   m.def("observe_ttft", [](double s) { metrics().engine_ttft_seconds.observe(s); });
   m.def("observe_itl", [](double s) { metrics().engine_itl_seconds.observe(s); });
   m.def("set_active_chats", [](double n) { metrics().active_chats.set(n); });

@@ -315,13 +315,28 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     for _ in range(warmup):
         publish(step())
     sync()
+    # stall attribution (timed window): per-step host / drain-wait time and start times, GC pauses
+    trace, gc_ms = [], []
+    gc_t = [0.0]
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        else:
+            gc_ms.append((time.perf_counter() - gc_t[0]) * 1000.0)
+
+    gc.callbacks.append(on_gc)
     t0_ns = time.time_ns()
     t0 = time.perf_counter()
     for _ in range(steps):
+        ts = time.perf_counter()
         publish(step())
+        st = getattr(engine, "stats", {})
+        trace.append((ts, time.perf_counter() - ts, st.get("host_s", 0.0), st.get("wait_s", 0.0)))
     sync()
     elapsed = time.perf_counter() - t0
     t1_ns = time.time_ns()
+    gc.callbacks.remove(on_gc)
     if live() < streams:
         raise RuntimeError(f"bench: only {live()} of {streams} streams were still decoding at the end of the window")
     while engine.has_work():
@@ -346,7 +361,34 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     itl = np.array(gaps) if gaps else np.array([elapsed * 1000.0 / max(1, steps)])
     return {"elapsed_s": elapsed, "p50_itl_ms": float(np.percentile(itl, 50)),
             "p99_itl_ms": float(np.percentile(itl, 99)), "delivered_in_window": delivered,
-            "client_errors": res["errors"][:5], "model": cfg.name, "max_context": prompt_len + 16 + total}
+            "client_errors": res["errors"][:5], "model": cfg.name, "max_context": prompt_len + 16 + total,
+            "stalls": _stall_report(trace, gc_ms, res["arrivals"], t0_ns, t1_ns) if rank == 0 else {}}
+
+
+def _stall_report(trace, gc_ms, arrivals, t0_ns, t1_ns) -> dict:
+    """Where inter-token time goes in the timed window: engine step cadence (host loop), its host vs
+    drain-wait split, GC pauses, and the delivery delay (engine timestamp -> client socket receive)."""
+    def pct(a, q):
+        return round(float(np.percentile(a, q)), 4) if len(a) else 0.0
+
+    starts = [t for t, *_ in trace]
+    cadence = np.diff(starts) * 1000.0 if len(starts) > 1 else np.zeros(0)
+    wall = np.array([w for _, w, _, _ in trace]) * 1000.0
+    host = np.array([h for _, _, h, _ in trace]) * 1000.0
+    wait = np.array([w for *_, w in trace]) * 1000.0
+    deliv, eng = [], {}
+    for s, _q, recv, ts in arrivals:
+        if t0_ns <= recv <= t1_ns and ts > 0:
+            deliv.append((recv - ts) / 1e6)
+            eng.setdefault(s, []).append(ts)
+    egaps = [(b - a) / 1e6 for v in eng.values() for a, b in zip(sorted(v), sorted(v)[1:])]
+    return {"step_cadence_ms": {"p50": pct(cadence, 50), "max": pct(cadence, 100)},
+            "step_wall_ms": {"p50": pct(wall, 50), "max": pct(wall, 100)},
+            "host_ms": {"p50": pct(host, 50), "max": pct(host, 100)},
+            "drain_wait_ms": {"p50": pct(wait, 50), "max": pct(wait, 100)},
+            "gc": {"count": len(gc_ms), "max_ms": round(max(gc_ms), 4) if gc_ms else 0.0},
+            "engine_token_gap_ms": {"p50": pct(egaps, 50), "p99": pct(egaps, 99)},
+            "delivery_ms": {"p50": pct(deliv, 50), "p99": pct(deliv, 99), "max": pct(deliv, 100)}}
 
 
 def _sync(device, world):

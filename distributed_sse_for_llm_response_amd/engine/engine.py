@@ -6,15 +6,22 @@ token events directly).  One engine per GPU (DP replica) or per TP group.
 
 Per ``step()`` (host, a few hundred microseconds of Python):
 
-1. admit waiting requests into free decode slots (lowest index first so live slots stay packed and
-   the smallest captured batch bucket applies), allocating KV pages for prompt + max_tokens;
-2. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
+1. give every sequence about to decode the KV page its next position lands in (pages are allocated
+   lazily, one at a time; when the pool runs dry the newest sequence -- paused ones first -- is
+   *preempted*: its pages are freed and it is requeued at the head of the queue to be re-prefilled
+   from prompt + the tokens it already published, so its stream resumes where it stopped);
+2. admit waiting requests into free decode slots (lowest index first so live slots stay packed and
+   the smallest captured batch bucket applies), allocating KV pages for the prompt only; when the
+   queue is empty, *compact*: decoding sequences above the bucket their count needs move down into
+   free slots or swap with paused ones (ids / positions move on the device), so holes left by
+   finished or paused streams do not keep the step on a bigger captured graph;
+3. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
    non-blocking copies on the compute stream;
-3. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
+4. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
    streams keep their inter-token latency while new prompts are absorbed);
-4. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
+5. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
    next step; token ring row ``t`` receives every token produced in step ``t``);
-5. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
+6. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
    earlier steps: sequence numbers, EOS / max_tokens stops, TTFT / ITL accounting.
 
 Flow control: a sequence whose subscribers all fall behind is *paused* (``set_paused``): its slot stays
@@ -37,7 +44,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from .kv_cache import BlockAllocator, blocks_needed
+from .kv_cache import PAGE, BlockAllocator, blocks_needed
 from .model_runner import RING_SIZE, ModelRunner, PrefillSeq, batch_buckets
 
 
@@ -76,7 +83,7 @@ class Sequence:
     slot: int = -1
     blocks: list = field(default_factory=list)
     prefilled: int = 0
-    state: str = "waiting"      # waiting | prefill | decode | finished
+    state: str = "waiting"      # waiting | prefill | decode | finished | preempted (replaced by a requeued copy)
     decode_enqueued: int = 0    # decode steps enqueued (tokens 2..n)
     produced: int = 0           # tokens drained and published
     first_token_ns: int = 0
@@ -85,6 +92,9 @@ class Sequence:
     stop_after_enqueue: bool = False
     paused: bool = False        # flow control: held out of the decode batch (KV and position kept)
     paused_at: float = 0.0
+    orig_len: int = 0           # prompt length as submitted (after a preemption `prompt` also holds out_ids)
+    out_ids: list = field(default_factory=list)  # tokens published so far (re-prefilled after a preemption)
+    base: int = 0               # tokens published before the latest (re-)admission
 
 
 class _Drain:
@@ -144,7 +154,11 @@ class LLMEngine:
         self._dirty_slots: set = set()
         self.ring_head = int(runner.ring_counter.item()) if runner.device.type == "cuda" else int(runner.ring_counter[0])
         self.stats = {"steps": 0, "decode_steps": 0, "prefill_tokens": 0, "tokens": 0, "last_step_s": 0.0,
-                      "pauses": 0}
+                      "pauses": 0, "preemptions": 0, "compactions": 0, "host_s": 0.0, "wait_s": 0.0}
+        # admission keeps this many pages free for running sequences to grow into (vLLM's 1% watermark)
+        self.watermark = max(1, runner.kv.num_blocks // 100)
+        self._bt_new: list = []  # (sequence, page index, block) appended since the last upload
+        self._pending: list = []  # events raised between steps (aborts of queued requests), returned by the next
         self.on_ttft = None
         self.on_itl = None
 
@@ -161,7 +175,7 @@ class LLMEngine:
         if len(prompt) > max_prompt:
             prompt = prompt[-max_prompt:]  # keep the tail (most recent context)
         s = Sequence(rid=next(self._rid) if rid is None else rid, conversation_id=conversation_id,
-                     prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns())
+                     prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns(), orig_len=len(prompt))
         self.waiting.append(s)
         self.by_conv[conversation_id] = s
         return s
@@ -171,9 +185,9 @@ class LLMEngine:
         if s is None or s.state == "finished":
             return False
         s.aborted = True
-        if s.state == "waiting":
+        if s.state == "waiting":  # never admitted, or preempted: its terminal event goes out with the next step
             self.waiting.remove(s)
-            self._finish(s, [], reason="abort")
+            self._finish(s, self._pending, reason="abort")
         return True
 
     def set_paused(self, conversation_id: str, paused: bool) -> bool:
@@ -197,11 +211,11 @@ class LLMEngine:
         return [c for c, s in self.by_conv.items() if s.paused and now - s.paused_at > self.max_pause_s]
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or any(s is not None for s in self.slots) or bool(self.inflight)
+        return bool(self.waiting or self.inflight or self._pending) or any(s is not None for s in self.slots)
 
     def runnable(self) -> bool:
         """Work a step would make progress on (paused decode sequences are not)."""
-        if self.waiting or self.inflight:
+        if self.waiting or self.inflight or self._pending:
             return True
         return any(s is not None and (not s.paused or s.aborted or s.state != "decode") for s in self.slots)
 
@@ -211,6 +225,8 @@ class LLMEngine:
     # ------------------------------------------------------------------ helpers
     def _upload(self):
         """Push host-side slot metadata changes to the device (pinned, non-blocking)."""
+        if self._bt_new:
+            self._upload_pages()
         if not self._dirty_slots:
             return
         r = self.r
@@ -255,24 +271,121 @@ class LLMEngine:
             put(r.block_tables[i], row)
         self._dirty_slots.clear()
 
+    def _upload_pages(self):
+        """Write the block-table entries of pages appended by ``_grow`` (one small copy, whatever the count).
+        Slots whose whole row is re-uploaded this step, or that changed hands, are skipped."""
+        r = self.r
+        idx, val = [], []
+        for s, j, blk in self._bt_new:
+            if s.slot >= 0 and self.slots[s.slot] is s and s.slot not in self._dirty_slots:
+                idx.append(s.slot * r.max_blocks + j)
+                val.append(blk)
+        self._bt_new.clear()
+        if not idx:
+            return
+        packed = torch.tensor(idx + val, dtype=torch.int32)
+        if r.device.type == "cuda":
+            packed = packed.pin_memory().to(r.device, non_blocking=True)
+        n = len(idx)
+        r.block_tables.view(-1).index_copy_(0, packed[:n].long(), packed[n:])
+
+    def _victim(self):
+        """The sequence to preempt: paused ones first, then the most recent request (FCFS keeps the oldest)."""
+        cands = [s for s in self.slots if s is not None and s.state in ("prefill", "decode") and not s.aborted
+                 and not s.stop_after_enqueue]
+        return max(cands, key=lambda s: (s.paused, s.rid))
+
+    def _preempt(self, v: Sequence):
+        """Free a sequence's slot and pages and requeue it (head of the queue) to be re-prefilled from its
+        prompt plus the tokens it already published.  Tokens of its steps still in flight are discarded
+        (``_consume`` skips the preempted object) and regenerated at the same positions -- with the same
+        per-(seed, position) sampling draw.  Stream order keeps the freed pages safe: their in-flight
+        writes precede anything a new owner enqueues."""
+        self.stats["preemptions"] += 1
+        n = Sequence(rid=v.rid, conversation_id=v.conversation_id, prompt=v.prompt[:v.orig_len] + v.out_ids,
+                     params=v.params, arrival_ns=v.arrival_ns, produced=v.produced, first_token_ns=v.first_token_ns,
+                     last_token_ns=v.last_token_ns, paused=v.paused, paused_at=v.paused_at, orig_len=v.orig_len,
+                     out_ids=v.out_ids, base=v.produced)
+        v.state = "preempted"
+        self.slots[v.slot] = None
+        self._dirty_slots.add(v.slot)
+        self.alloc.free(v.blocks)
+        v.blocks = []
+        if self.by_conv.get(v.conversation_id) is v:
+            self.by_conv[v.conversation_id] = n
+        self.waiting.appendleft(n)
+
+    def _grow(self):
+        """Before the decode step: every sequence in it needs the page its write position falls in."""
+        need = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
+                and not s.stop_after_enqueue and not s.paused
+                and (len(s.prompt) + s.decode_enqueued) // PAGE >= len(s.blocks)]
+        for s in sorted(need, key=lambda s: s.rid):  # oldest first: the newest are the ones preempted
+            while self.alloc.num_free == 0 and s.state == "decode":
+                self._preempt(self._victim())
+            if s.state != "decode":
+                continue
+            blk = self.alloc.allocate(1)[0]
+            self._bt_new.append((s, len(s.blocks), blk))
+            s.blocks.append(blk)
+
     def _admit(self):
         r = self.r
         while self.waiting:
             s = self.waiting[0]
-            free = [i for i, x in enumerate(self.slots) if x is None]
-            if not free:
+            free = next((i for i, x in enumerate(self.slots) if x is None), -1)
+            if free < 0:
                 return
-            max_new = max(1, min(s.params.max_tokens, r.max_model_len - len(s.prompt)))
-            s.params = SamplingParams(**{**s.params.__dict__, "max_tokens": max_new})
-            need = blocks_needed(len(s.prompt) + max_new + 1)
-            if not self.alloc.can_allocate(need):
+            if s.base == 0:  # first admission: clamp max_tokens to the context and to the whole pool
+                cap = self.alloc.num_blocks * PAGE - s.orig_len
+                max_new = max(1, min(s.params.max_tokens, r.max_model_len - s.orig_len, cap))
+                s.params = SamplingParams(**{**s.params.__dict__, "max_tokens": max_new})
+            need = blocks_needed(len(s.prompt))
+            idle = not any(x is not None for x in self.slots)
+            if need > self.alloc.num_free - (0 if idle else self.watermark):
+                if idle and need > self.alloc.num_blocks:  # can never fit: fail it rather than wait forever
+                    self.waiting.popleft()
+                    self._finish(s, self._early, reason="length")
+                    continue
                 return
             self.waiting.popleft()
             s.blocks = self.alloc.allocate(need)
-            s.slot = free[0]
+            s.slot = free
             s.state = "prefill"
+            s.prefilled = 0
+            s.decode_enqueued = 0
             self.slots[s.slot] = s
             self._dirty_slots.add(s.slot)
+
+    def _compact(self):
+        """Move decoding sequences above the bucket their count needs into lower free / paused slots."""
+        dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
+               and not s.stop_after_enqueue and not s.paused]
+        if not dec:
+            return
+        buckets = batch_buckets(self.r.max_batch)
+        hi = max(s.slot for s in dec) + 1
+        want = next(b for b in buckets if b >= len(dec))
+        if next(b for b in buckets if b >= hi) <= want:
+            return
+        holes = [i for i in range(want) if self.slots[i] is None or (
+            self.slots[i].state == "decode" and self.slots[i].paused and not self.slots[i].stop_after_enqueue)]
+        movers = sorted((s for s in dec if s.slot >= want), key=lambda s: -s.slot)
+        src, dst = [], []
+        for s, j in zip(movers, holes):
+            i, p = s.slot, self.slots[j]
+            src.append(i)
+            dst.append(j)
+            self.slots[j], s.slot = s, j
+            self.slots[i] = p
+            if p is not None:  # swap with a paused sequence: its device state goes the other way
+                p.slot = i
+                src.append(j)
+                dst.append(i)
+            self._dirty_slots.update((i, j))
+        if src:
+            self.r.move_slots(src, dst)
+            self.stats["compactions"] += 1
 
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
@@ -297,7 +410,7 @@ class LLMEngine:
         s.state = "finished"
         now = time.time_ns()
         events.append(TokenEvent(s.conversation_id, -1, s.produced + 1, True, text=text, timestamp_ns=now,
-                                 finish=reason, prompt_tokens=len(s.prompt)))
+                                 finish=reason, prompt_tokens=s.orig_len))
         if s.slot >= 0 and self.slots[s.slot] is s:
             self.slots[s.slot] = None
             self._dirty_slots.add(s.slot)
@@ -311,17 +424,21 @@ class LLMEngine:
     def step(self, block: bool = True) -> list:
         """Enqueue one engine step and return the token events of completed earlier steps."""
         t0 = time.perf_counter()
-        events: list = []
+        events, self._pending = self._pending, []
+        self._early = events
         r = self.r
         # sequences whose max_tokens budget is fully enqueued stop decoding now
         for s in self.slots:
-            if s is not None and s.state == "decode" and s.decode_enqueued + 1 >= s.params.max_tokens:
+            if s is not None and s.state == "decode" and s.base + s.decode_enqueued + 1 >= s.params.max_tokens:
                 if not s.stop_after_enqueue:
                     s.stop_after_enqueue = True
                     self._dirty_slots.add(s.slot)
             if s is not None and s.aborted and s.state != "finished":
                 self._dirty_slots.add(s.slot)
+        self._grow()
         self._admit()
+        if not self.waiting:
+            self._compact()
         row = self.ring_head % RING_SIZE
         chunks, prefill_done = self._schedule_prefill(self.step_no)
         self._upload()
@@ -356,12 +473,15 @@ class LLMEngine:
             self.ring_head += 1
             self.step_no += 1
         # ---- consume drained steps: keep `depth` steps in flight, process everything that is ready
+        wait = 0.0  # blocked on a drain event (GPU time, not host work)
         while self.inflight:
             st, rrow, prods, tq = self.inflight[0]
             must = len(self.inflight) > self.depth or not ran
             if not must and (self.deterministic or not block or not self.drain.ready(rrow)):
                 break
+            tw = time.perf_counter()
             toks = self.drain.wait(rrow)
+            wait += time.perf_counter() - tw
             self.inflight.popleft()
             self._consume(toks, prods, events)
         # aborted sequences leave at this boundary
@@ -370,14 +490,17 @@ class LLMEngine:
                     s is p for _, _, prods, _ in self.inflight for _, p in prods):
                 self._finish(s, events, reason="abort")
         self.stats["steps"] += 1
-        self.stats["last_step_s"] = time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.stats["last_step_s"] = dt
+        self.stats["wait_s"] = wait
+        self.stats["host_s"] = dt - wait
         return events
 
     def _consume(self, toks, prods, events):
         now = time.time_ns()
         tl = toks.tolist()
         for slot, s in prods:
-            if s.state == "finished" or s.aborted:
+            if s.state == "finished" or s.state == "preempted" or s.aborted:
                 continue
             tok = int(tl[slot])
             s.produced += 1
@@ -391,12 +514,13 @@ class LLMEngine:
             is_eos = tok == self.eos_id and not s.params.ignore_eos
             if not is_eos:
                 events.append(TokenEvent(s.conversation_id, tok, s.produced, False, timestamp_ns=now))
+                s.out_ids.append(tok)
                 self.stats["tokens"] += 1
             else:
                 s.produced -= 1
             if is_eos:
                 self._finish(s, events, reason="stop")
-            elif s.produced >= s.params.max_tokens or len(s.prompt) + s.produced >= self.r.max_model_len:
+            elif s.produced >= s.params.max_tokens or s.orig_len + s.produced >= self.r.max_model_len:
                 self._finish(s, events, reason="length")
 
     def run_until_idle(self, max_steps: int = 100000) -> list:

@@ -325,6 +325,14 @@ class ModelRunner:
         for t, s in zip((self.ids, self.positions, self.ring, self.ring_counter), saved):
             t.copy_(s)
 
+    def move_slots(self, src: list, dst: list) -> None:
+        """Slot compaction: decode state (last token, position) of slot src[i] -> dst[i], gathered before it
+        is scattered so swaps work; stream-ordered after every decode step already enqueued."""
+        si = torch.tensor(src, dtype=torch.long).to(self.device)
+        di = torch.tensor(dst, dtype=torch.long).to(self.device)
+        for t in (self.ids, self.positions):
+            t.index_copy_(0, di, t.index_select(0, si))
+
     def decode(self, B: int) -> None:
         g = self.graphs.get(B)
         if g is not None:

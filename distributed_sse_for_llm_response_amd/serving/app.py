@@ -76,7 +76,7 @@ class EngineLoop(threading.Thread):
         rt = rt_mod.load()
         self._rt = rt
         self._remote = hasattr(runtime, "observe")
-        self._ttft, self._itl = [], []
+        self._ttft, self._itl, self._host = [], [], []
         self._last_obs = 0.0
         self.faults = FaultPlan.from_env()
         self.tracer = StepTracer()
@@ -128,18 +128,22 @@ class EngineLoop(threading.Thread):
     def _observe(self):
         e = self.engine
         running, free = float(e.num_running()), float(e.alloc.num_free)
+        host = e.stats.get("host_s", -1.0)
         if not self._remote:
-            self._rt.engine_observe(e.stats["last_step_s"], running, free)
+            self._rt.engine_observe(e.stats["last_step_s"], running, free, host)
             self._rt.set_active_chats(running + len(e.waiting))
             return
+        if host >= 0:
+            self._host.append(host)
         now = time.monotonic()
-        if now - self._last_obs < 0.05 and len(self._itl) < 4096:
+        if now - self._last_obs < 0.05 and len(self._itl) < 4096 and len(self._host) < 4096:
             return  # batch the observations: one stats message per ~50 ms
         self._last_obs = now
-        ttft, itl = self._ttft[:], self._itl[:]
+        ttft, itl, hs = self._ttft[:], self._itl[:], self._host[:]
         self._ttft.clear()
         self._itl.clear()
-        self.rt.observe(e.stats["last_step_s"], running, free, running + len(e.waiting), ttft, itl)
+        self._host.clear()
+        self.rt.observe(e.stats["last_step_s"], running, free, running + len(e.waiting), ttft, itl, hs)
 
     def _shutdown(self) -> bool:
         f = getattr(self.rt, "shutdown_requested", None)

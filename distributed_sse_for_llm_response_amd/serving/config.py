@@ -56,7 +56,7 @@ class ServeConfig:
     tp: int = 1
     dp: int = 1
     max_model_len: int = 4096
-    max_batch: int = 64
+    max_batch: int = 256  # decode slots (captured buckets 1..64 by powers of two, then every 64); KV pages are lazy
     gpu_memory_utilization: float = 0.85
     seed: int = 0
     max_tokens: int = 256

@@ -142,6 +142,9 @@ class StepTracer:
             self.f.write(json.dumps({"t_ns": time.time_ns(), "step": step, "step_ms": round(dt_s * 1000, 4),
                                      "running": engine.num_running(), "waiting": len(engine.waiting),
                                      "tokens_out": len(events), "kv_free": engine.alloc.num_free,
+                                     "host_ms": round(engine.stats.get("host_s", 0.0) * 1000, 4),
+                                     "wait_ms": round(engine.stats.get("wait_s", 0.0) * 1000, 4),
+                                     "preemptions": engine.stats.get("preemptions", 0),
                                      "prefill_tokens": engine.stats["prefill_tokens"]}) + "\n")
 
     def close(self):

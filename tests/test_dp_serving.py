@@ -55,7 +55,7 @@ class FakeWorker(threading.Thread):
                 self.chan.publish_tokens([c] * self.n, list(range(10, 10 + self.n)), list(range(1, self.n + 1)),
                                          [False] * self.n, 0, [])
                 self.chan.publish_tokens([c], [-1], [self.n + 1], [True], 0, ["[DONE]"])
-            self.chan.observe(0.005, 1.0, 100.0, 1.0, [0.01], [0.005])
+            self.chan.observe(0.005, 1.0, 100.0, 1.0, [0.01], [0.005], [0.0004])
 
 
 def _chat(port, msg="hi", conv=None):
@@ -69,6 +69,7 @@ def _chat(port, msg="hi", conv=None):
 def test_router_spreads_requests_and_resolves_vocab():
     rt, prefix = _router(2)
     routed0 = _metric(rt, "dp_requests_routed_total")
+    host0 = _metric(rt, "engine_host_step_seconds_count")
     ws = [FakeWorker(prefix, 0), FakeWorker(prefix, 1)]
     try:
         for w in ws:
@@ -97,6 +98,10 @@ def test_router_spreads_requests_and_resolves_vocab():
         assert _metric(rt, "dp_workers_alive") == 2
         assert _metric(rt, "dp_requests_routed_total") == routed0 + 6
         assert all(i["outstanding"] == 0 for i in rt.dp_workers())
+        deadline = time.time() + 5  # workers' host step-time samples reach the router's histogram
+        while time.time() < deadline and _metric(rt, "engine_host_step_seconds_count") == host0:
+            time.sleep(0.05)
+        assert _metric(rt, "engine_host_step_seconds_count") > host0
     finally:
         for w in ws:
             w.stop.set()
