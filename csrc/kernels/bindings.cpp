@@ -7,6 +7,10 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -49,6 +53,22 @@ int env_int(const char* name, int dflt) {
   }
   return it->second == INT32_MIN ? dflt : it->second;
 }
+// DSSE_TRAP_FPE=1: print the native stack of a host SIGFPE (integer division by zero) before dying.
+void fpe_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "[dsse] SIGFPE, native stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+const bool g_fpe_trap = [] {
+  const char* v = std::getenv("DSSE_TRAP_FPE");
+  if (v && v[0] == '1') signal(SIGFPE, fpe_handler);
+  return true;
+}();
+
 void refresh_env() {
   std::lock_guard<std::mutex> lk(g_env_mu);
   g_env.clear();
@@ -185,18 +205,59 @@ WCfg pick_wide(int M, int N, int K) {
 
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
+// Tiled LDS-DMA GEMM (gemm_tiled.hip; prefill and wide batches).  Env overrides: DSSE_T_CFG (0 = 256x128,
+// 1 = 128x128, 2 = 256x64 tile), DSSE_T_SPLIT.
+struct TCfg {
+  int cfg, S;
+  bool ok;
+};
+TCfg pick_tiled(int M, int N, int K) {
+  TCfg c{};
+  int cfg = env_int("DSSE_T_CFG", -1);
+  if (cfg < 0 || cfg > 10) {
+    // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile (8 waves of 128x64, 2 LDS stages) is
+    // the fastest once it yields >= ~160 workgroups (1.20-1.24 PFLOP/s at 8192 rows); below that, the
+    // 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
+    const int big_tiles = ((M + 255) / 256) * (N / 256);
+    cfg = (N % 256 == 0 && big_tiles >= 160) ? 3 : (M > 128 ? 0 : 1);
+  }
+  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 128 for 0/1/5/7
+  const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : ((cfg <= 1 || cfg == 5 || cfg == 7) ? 128 : 256);
+  c.cfg = cfg;
+  c.S = 1;
+  c.ok = N % BN == 0 && K % 64 == 0;
+  if (!c.ok) return c;
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  int S = env_int("DSSE_T_SPLIT", 0);
+  if (S <= 0 || K % (64 * S) != 0) {
+    S = 1;  // split K only for the few-tile wide-decode shapes (slabs cost M x N x 4 B each)
+    while (M <= kMaxDecodeM && tiles * S < 160 && K % (64 * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
+  }
+  c.S = S;
+  return c;
+}
+
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
 // whole K-slice staged (gemm_xlds.hip), 2 = X streamed through LDS slices (gemm_stream.hip).
 // DSSE_GEMM_IMPL forces one.
 int gemm_impl(int M, int N, int K) {
   const int impl = env_int("DSSE_GEMM_IMPL", -1);
-  if (M > 64) {  // 3 = gemm_wide (32x32 MFMAs, M <= 256) above DSSE_WIDE_MIN_M rows, else gemm_stream
-    const bool wide_ok = pick_wide(M, N, K).ok;
+  if (M > 64) {
+    // every branch returns a kernel whose shape contract holds (or -1): prefill calls arrive with any M and
+    // tensor-parallel shard shapes
+    const bool tiled_ok = pick_tiled(M, N, K).ok;
+    if (tiled_ok && (M > kMaxDecodeM || impl == 4 || (impl < 0 && M > env_int("DSSE_TILED_MIN_M", 128)))) return 4;
+    if (M > kMaxDecodeM) return -1;  // the decode kernels stop at kMaxDecodeM rows
+    const bool wide_ok = pick_wide(M, N, K).ok, stream_ok = pick_stream(M, N, K).ok;
     if (impl == 3 && wide_ok) return 3;
-    if (impl == 2) return 2;
-    return (wide_ok && M > env_int("DSSE_WIDE_MIN_M", 64)) ? 3 : 2;
+    if (impl == 2 && stream_ok) return 2;
+    if (wide_ok && M > env_int("DSSE_WIDE_MIN_M", 64)) return 3;  // 3 = gemm_wide (32x32 MFMAs, M <= 256)
+    if (stream_ok) return 2;
+    if (wide_ok) return 3;
+    return tiled_ok ? 4 : -1;
   }
   if (impl >= 0) {
+    if (impl == 4) return pick_tiled(M, N, K).ok ? 4 : (pick_stream(M, N, K).ok ? 2 : 1);
     if (impl == 3 && !pick_wide(M, N, K).ok) return pick_stream(M, N, K).ok ? 2 : 1;
     if (impl == 2 && !pick_stream(M, N, K).ok) return 1;
     return impl;
@@ -214,11 +275,20 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "x and w must be 2-D");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch: x ", K, " vs w ", w.size(1));
-  TORCH_CHECK(M >= 1 && M <= kMaxDecodeM, "decode GEMM supports 1 <= M <= ", kMaxDecodeM, ", got ", M);
+  TORCH_CHECK(M >= 1, "GEMM needs M >= 1, got ", M);
   TORCH_CHECK(K % 128 == 0, "K must be a multiple of 128, got ", K);
   TORCH_CHECK(N % 16 == 0, "N must be a multiple of 16, got ", N);
   TORCH_CHECK((int64_t)N * K * 2 < (1LL << 31), "weight larger than 2 GiB: the decode GEMMs address it with 32-bit offsets");
   const int impl = gemm_impl(M, N, K);
+  TORCH_CHECK(impl >= 0, "no GEMM kernel for M=", M, " N=", N, " K=", K, " (tiled path needs N % 128, K % 64)");
+  if (impl == 4) {
+    const TCfg c = pick_tiled(M, N, K);
+    at::Tensor part;
+    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
+    DSSE_CHECK_HIP(dsse_gemm_tiled(mode, c.cfg, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                   c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    return;
+  }
   TORCH_CHECK(M <= 64 || impl >= 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
   if (impl == 3) {
     const WCfg c = pick_wide(M, N, K);
@@ -285,10 +355,19 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   check_gpu(part, "part");
   check_dtype(part, at::kFloat, "part");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
-  const bool shape_ok = M >= 1 && M <= kMaxDecodeM && K % 128 == 0 && N % 16 == 0 && w.size(1) == K &&
-                        (M <= 64 || pick_stream(M, N, K).ok);
+  const bool shape_ok = M >= 1 && K % 128 == 0 && N % 16 == 0 && w.size(1) == K;
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
-  if (impl == 3) {
+  if (impl == 4) {
+    const TCfg c = pick_tiled(M, N, K);
+    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      dsse::GemmEpi ep{};
+      DSSE_CHECK_HIP(dsse_gemm_tiled(dsse::kResidAdd, c.cfg, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                     part.data_ptr<float>(), cur_stream()));
+      return c.S;
+    }
+  } else if (impl == 3) {
     const WCfg c = pick_wide(M, N, K);
     if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
       check_dtype(x, at::kBFloat16, "x");
@@ -599,7 +678,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 5; }
+int64_t kernels_abi_version() { return 6; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -607,19 +686,19 @@ bool kernels_checked() { return true; }
 bool kernels_checked() { return false; }
 #endif
 
-// Checked build: [7, 4] int32 (line, value, bound, count) of the first out-of-range index per kernel file,
+// Checked build: [8, 4] int32 (line, value, bound, count) of the first out-of-range index per kernel file,
 // in the order of kCheckFiles; all zeros in the default build.  Synchronises the device.
-const char* const kCheckFiles[7] = {"gemm_skinny.hip", "gemm_stream.hip", "gemm_xlds.hip", "attention.hip",
-                                    "attention_prefill.hip", "elementwise.hip", "sampler.hip"};
+const char* const kCheckFiles[8] = {"gemm_skinny.hip", "gemm_stream.hip", "gemm_xlds.hip", "attention.hip",
+                                    "attention_prefill.hip", "elementwise.hip", "sampler.hip", "gemm_tiled.hip"};
 Tensor kernel_checks(bool clear) {
   using Reader = hipError_t (*)(int*, int);
-  static const Reader readers[7] = {dsse_check_gemm_skinny, dsse_check_gemm_stream, dsse_check_gemm_xlds,
+  static const Reader readers[8] = {dsse_check_gemm_skinny, dsse_check_gemm_stream, dsse_check_gemm_xlds,
                                     dsse_check_attention, dsse_check_attention_prefill, dsse_check_elementwise,
-                                    dsse_check_sampler};
-  Tensor out = at::zeros({7, 4}, at::kInt);
+                                    dsse_check_sampler, dsse_check_gemm_tiled};
+  Tensor out = at::zeros({8, 4}, at::kInt);
   if (!kernels_checked()) return out;
   DSSE_CHECK_HIP(hipDeviceSynchronize());
-  for (int i = 0; i < 7; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
+  for (int i = 0; i < 8; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
   return out;
 }
 std::string kernel_check_files() {

@@ -38,18 +38,11 @@ from .weights import EngineWeights
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
-# Largest decode bucket on the engine's own GEMMs (gemm_skinny / gemm_stream with fused epilogues); larger
-# buckets use hipBLASLt + separate RoPE / SiLU / norm kernels.  Measured per layer (qkv + o + gate_up + down,
-# profiles/gemm_mid_m_r1.md): 128 rows 156 vs 185 us, 192 rows 207 vs 236, 256 rows 241 vs 194.  End to end the
-# 192-row bucket is faster on the wide path (hipBLASLt o / gate_up + gemm_wide qkv / down): 192 streams 9.40 vs
-# 10.09 ms/step, 160 streams 8.56 vs 9.52; 128 rows stay here (7.01 vs 7.20) -- profiles/bucket_ab_r1.md.
+# Largest decode bucket on the fused-norm decode step (gemm_skinny / gemm_stream, split-K slabs reduced in the
+# norms); larger buckets take the wide path (_decode_layers_wide), whose projections the kernel library routes to
+# gemm_wide / gemm_tiled by row count (bindings.cpp gemm_impl).  Round 1 measured the split at 128 rows
+# (profiles/bucket_ab_r1.md).
 DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
-
-
-# Decode buckets above DECODE_GEMM_MAX_M (<= 256 rows): projections that run on the engine's 32x32-MFMA decode GEMM
-# (gemm_wide) instead of hipBLASLt -- QKV with its fused RoPE + KV-write epilogue (no separate rope kernel) and,
-# at TP=1, down with its split-K slabs reduced inside the next norm (profiles/experiments_r1.md).
-WIDE_ENGINE_OPS = frozenset(x for x in os.environ.get("DSSE_WIDE_ENGINE_OPS", "qkv,down").split(",") if x)
 
 
 def batch_buckets(max_batch: int):
@@ -187,11 +180,11 @@ class ModelRunner:
     def _decode_layers_wide(self, B: int, resid, x, part: int, nparts: int) -> None:
         """Decode step for buckets above DECODE_GEMM_MAX_M sequences (256 streams per GPU, BASELINE config 3).
 
-        At B > 192 a weight byte feeds > 192 rows and the projections become compute-heavy skinny GEMMs:
-        they run on hipBLASLt (the plain-library GEMM path, standard weight layout, same as prefill) with the
-        engine's own RoPE/KV-write, SiLU·mul and residual+RMSNorm kernels around them; attention and the
-        sampler are the decode kernels.  The LM head stays on the fp32-output decode GEMM in 256-row blocks
-        (sampling wants fp32 logits).  Still one captured graph per bucket.
+        At B > 128 a weight byte feeds > 128 rows and the projections become compute-heavy skinny GEMMs; they run
+        on the engine's tiled-layout GEMMs with fused epilogues (QKV + RoPE + KV write, residual + split-K norm,
+        SiLU·mul) -- gemm_wide or the register-blocked gemm_tiled, chosen per shape by the kernel library.  The
+        LM head stays on the fp32-output GEMM in 256-row blocks (sampling wants fp32 logits).  One captured graph
+        per bucket.
         """
         w, cfg, comm = self.w, self.cfg, self.comm
         nh, nkv = w.nh, w.nkv
@@ -200,38 +193,34 @@ class ModelRunner:
         q3 = self.q[r].view(B, nh, 128)
         a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
-        eng_qkv = "qkv" in WIDE_ENGINE_OPS and B <= 256
-        eng_down = "down" in WIDE_ENGINE_OPS and B <= 256 and comm.size == 1
         for li, L in enumerate(w.layers):
-            if eng_qkv:
-                ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
-                                  self.kv.v[li], nh, nkv)
-            else:
-                qkv = torch.matmul(x, L.wqkv.t())
-                ops.rope_kv_write(qkv, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
-                                  self.kv.v[li], nh, nkv)
+            ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+                              self.kv.v[li], nh, nkv)
             ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
                                 self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
                                 self.part_ml, part, nparts)
-            o = torch.matmul(self.attn[r], L.wo.t())
-            comm.all_reduce(o)
-            ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=o)
-            gu = torch.matmul(x, L.wgu.t())
-            ops.silu_mul(gu, self.h[r])
+            self._resid_proj(self.attn[r], L.wo_t, resid, L.ffn_norm, x, self.tmp[r])
+            ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-            if eng_down:
-                ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
-                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
-            else:
-                down = torch.matmul(self.h[r], L.wd.t())
-                comm.all_reduce(down)
-                ops.rmsnorm(resid, w_next, x, eps, delta=down)
+            self._resid_proj(self.h[r], L.wd_t, resid, w_next, x, self.tmp[r])
         step = 256 if DECODE_GEMM_MAX_M > 2 else DECODE_GEMM_MAX_M  # one 256-row call streams the head once
         for b0 in range(0, B, step):
             b1 = min(B, b0 + step)
             ops.gemm_out(x[b0:b1], w.lm_head_t, self.logits[b0:b1])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
+
+    def _resid_proj(self, a, wt, resid, norm_w, x, tmp) -> None:
+        """resid += a·wᵀ (TP: all-reduced), then x = RMSNorm(resid)·norm_w.  TP = 1: split-K slabs (if the GEMM
+        splits) are reduced inside the norm; TP > 1: the bf16 partial product is all-reduced first."""
+        eps = self.cfg.rms_eps
+        if self.comm.size == 1:
+            ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
+            ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns)
+        else:
+            ops.gemm_out(a, wt, tmp)
+            self.comm.all_reduce(tmp)
+            ops.rmsnorm(resid, norm_w, x, eps, delta=tmp)
 
     def _sample_commit(self, B: int) -> None:
         """Candidates per (row, vocab chunk) on each rank -> (TP: all-gather, 8 B per candidate) -> pick."""
@@ -341,6 +330,16 @@ class ModelRunner:
             self.decode_forward(B)
 
     # ------------------------------------------------------------------ prefill
+    def _prefill_resid(self, a, wt, resid, norm_w, x, tmp) -> None:
+        eps = self.cfg.rms_eps
+        if tmp is None:
+            ops.gemm_resid(a, wt, resid)
+            ops.rmsnorm(resid, norm_w, x, eps)
+        else:
+            ops.gemm_out(a, wt, tmp)
+            self.comm.all_reduce(tmp)
+            ops.rmsnorm(resid, norm_w, x, eps, delta=tmp)
+
     def prefill(self, seqs: list, ring_row: int) -> None:
         """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
         first token into ids[slot] and ring[ring_row, slot] and get positions[slot] set on device."""
@@ -397,34 +396,25 @@ class ModelRunner:
         part = math.ceil(max_ctx / 32) * 32
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d_ids)
         nl = len(w.layers)
+        # every projection on the engine's tiled-layout GEMMs with fused epilogues (csrc/kernels/gemm_tiled.hip
+        # for T > 256 rows): QKV + RoPE + paged KV write, residual add, SiLU·mul -- no [T, N] intermediates
+        tmp = torch.empty(T, H, **bf) if comm.size > 1 else None
         for li, L in enumerate(w.layers):
-            qkv = x @ L.wqkv.t()
-            ops.rope_kv_write(qkv, d_pos, d_slots, self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
-            del qkv
+            ops.gemm_qkv_rope(x, L.wqkv_t, d_pos, d_slots, self.rope, q.view(T, nh * 128), self.kv.k[li],
+                              self.kv.v[li], nh, nkv)
             ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
                                 self.part_o, self.part_ml, part, 1)
-            o_proj = attn.view(T, nh * 128) @ L.wo.t()
-            comm.all_reduce(o_proj)
-            ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=o_proj)
-            gu = x @ L.wgu.t()
-            ops.silu_mul(gu, h)
-            del gu
-            down = h @ L.wd.t()
-            comm.all_reduce(down)
+            self._prefill_resid(attn.view(T, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
+            ops.gemm_silu(x, L.wgu_t, h)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-            ops.rmsnorm(resid, w_next, x, eps, delta=down)
+            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
         last = [i for i, s in enumerate(seqs) if s.last_chunk]
         if not last:
             return
         rows = torch.tensor([q_start[i] + q_len[i] - 1 for i in last], dtype=torch.long, device=dev)
         xl = x.index_select(0, rows)
-        logits = (xl.float() @ w.lm_head.float().t()) if dev.type == "cpu" else None
-        if logits is None:
-            logits = torch.empty(len(last), w.vocab_local, **f32)
-            if len(last) <= 64:
-                ops.gemm_out(xl, w.lm_head_t, logits)
-            else:
-                logits = (xl @ w.lm_head.t()).float()
+        logits = torch.empty(len(last), w.vocab_local, **f32)
+        ops.gemm_out(xl, w.lm_head_t, logits)
         slot_idx = torch.tensor([seqs[i].slot for i in last], dtype=torch.long, device=dev)
         last_pos = torch.tensor([seqs[i].start_pos + len(seqs[i].tokens) - 1 for i in last], dtype=torch.int32,
                                 device=dev)

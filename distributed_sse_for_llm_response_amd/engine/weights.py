@@ -12,11 +12,12 @@ The decode kernels want, per rank (t = TP degree, r = rank):
 * ``lm_head`` [V/t, H]                 — vocab-parallel; the sampler merges per-rank candidates.
 * ``embed`` [V, H] replicated (256 MiB; HBM is plentiful, and it avoids an all-reduce per step).
 
-All matrices are row-major [out, in] bf16 and contiguous (the layout the prefill GEMMs — hipBLASLt via
-``torch.matmul`` — consume).  The decode GEMMs stream a second copy of each matrix in the tiled layout
-of :func:`ops.reference.tile_weight` (``*_t`` fields, made by :func:`attach_tiled`): every weight load
-instruction then reads 1 KiB of contiguous HBM.  The copy costs one more model's worth of HBM (14.5 GB
-for Mistral-7B at TP=1, 5 % of an MI355X's 288 GB).
+Every GEMM of the engine -- decode (gemm_skinny / gemm_stream / gemm_wide) and prefill (gemm_tiled) --
+consumes the tiled layout of :func:`ops.reference.tile_weight` (``*_t`` fields, made by :func:`attach_tiled`):
+every weight load instruction reads 1 KiB of contiguous HBM, and a (16-column, 32-deep) block is one MFMA B
+fragment.  The row-major [out, in] matrices above are only the conversion input; :func:`attach_tiled` drops
+them, so the model is resident once (round 1 kept both layouts for the library prefill GEMMs: 14.5 GB more for
+Mistral-7B at TP=1, now KV cache).
 """
 from __future__ import annotations
 
@@ -32,12 +33,12 @@ from ..ops.reference import gate_up_perm, rotary_perm, tile_weight
 @dataclass
 class LayerWeights:
     attn_norm: torch.Tensor
-    wqkv: torch.Tensor
+    wqkv: torch.Tensor   # row-major conversion inputs (None once attach_tiled has run)
     wo: torch.Tensor
     ffn_norm: torch.Tensor
     wgu: torch.Tensor
     wd: torch.Tensor
-    # decode copies in the tiled layout (attach_tiled)
+    # the engine's copies, in the tiled layout (attach_tiled)
     wqkv_t: torch.Tensor = None
     wo_t: torch.Tensor = None
     wgu_t: torch.Tensor = None
@@ -76,22 +77,24 @@ class EngineWeights:
         return self.tp_rank * self.vocab_local
 
     def nbytes(self) -> int:
-        """Bytes of one copy of the model (what a decode step streams)."""
-        n = self.embed.numel() + self.final_norm.numel() + self.lm_head.numel()
+        """Bytes of the resident model (what a decode step streams, plus the embedding table)."""
+        n = self.embed.numel() + self.final_norm.numel() + self.lm_head_t.numel()
         for L in self.layers:
-            n += sum(t.numel() for t in (L.attn_norm, L.wqkv, L.wo, L.ffn_norm, L.wgu, L.wd))
+            n += sum(t.numel() for t in (L.attn_norm, L.wqkv_t, L.wo_t, L.ffn_norm, L.wgu_t, L.wd_t))
         return 2 * n
 
 
 @torch.no_grad()
 def attach_tiled(w: EngineWeights) -> EngineWeights:
-    """Add the tiled decode copies of every GEMM weight (idempotent)."""
+    """Convert every GEMM weight to the tiled layout and drop the row-major input (idempotent)."""
     for L in w.layers:
         if L.wqkv_t is None:
             L.wqkv_t, L.wo_t = tile_weight(L.wqkv), tile_weight(L.wo)
             L.wgu_t, L.wd_t = tile_weight(L.wgu), tile_weight(L.wd)
+        L.wqkv = L.wo = L.wgu = L.wd = None
     if w.lm_head_t is None:
         w.lm_head_t = tile_weight(w.lm_head)
+    w.lm_head = None
     return w
 
 
@@ -159,8 +162,11 @@ def random_engine_weights(cfg: MistralConfig, tp_rank: int = 0, tp_size: int = 1
     embed = torch.empty(cfg.vocab_size, H, device=device, dtype=dtype).normal_(0.0, 1.0, generator=embed_gen)
     layers = []
     for _ in range(cfg.num_layers):
-        layers.append(LayerWeights(attn_norm=norm(H), wqkv=lin((nh + 2 * nkv) * D, H), wo=lin(H, nh * D),
-                                   ffn_norm=norm(H), wgu=lin(2 * F, H), wd=lin(H, F)))
+        L = LayerWeights(attn_norm=norm(H), wqkv=lin((nh + 2 * nkv) * D, H), wo=lin(H, nh * D),
+                         ffn_norm=norm(H), wgu=lin(2 * F, H), wd=lin(H, F))
+        L.wqkv_t, L.wo_t, L.wgu_t, L.wd_t = (tile_weight(t) for t in (L.wqkv, L.wo, L.wgu, L.wd))
+        L.wqkv = L.wo = L.wgu = L.wd = None  # one layer's row-major copy at a time
+        layers.append(L)
     return attach_tiled(EngineWeights(cfg=cfg, tp_rank=tp_rank, tp_size=tp_size, embed=embed, layers=layers,
                                       final_norm=norm(H), lm_head=lin(V, H)))
 

@@ -35,6 +35,9 @@ GEMM_CONFIGS = {
     "stream-nw4-split4": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "4"},
     "wide-default": {"DSSE_GEMM_IMPL": "3"},
     "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
+    "tiled-default": {"DSSE_GEMM_IMPL": "4"},
+    "tiled-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "1", "DSSE_T_SPLIT": "2"},
+    "tiled-256x64": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "2"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
@@ -380,7 +383,7 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 5
+    assert torch.ops.dsse.kernels_abi_version() == 6
     assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
 
 

@@ -64,25 +64,27 @@ def test_engine_chunked_prefill_gpu(gpu):
     assert _run(gpu, False, steps=3, chunked=True) < 0.1
 
 
-WIDE_OPS = [frozenset(), frozenset({"qkv", "down"})]
-
-
-@pytest.mark.parametrize("eng_ops", WIDE_OPS, ids=["library", "engine-qkv-down"])
-def test_engine_wide_batch_path_cpu(monkeypatch, eng_ops):
-    """Buckets above the fused decode GEMMs' row limit take the wide decode path (library GEMMs, optionally the
-    engine's QKV + RoPE and down + split-K norm)."""
+def test_engine_wide_batch_path_cpu(monkeypatch):
+    """Buckets above the fused decode GEMMs' row limit take the wide decode path (every projection on the
+    tiled-layout GEMMs: QKV + RoPE, residual + split-K norm, SiLU·mul)."""
     from distributed_sse_for_llm_response_amd.engine import model_runner
 
     monkeypatch.setattr(model_runner, "DECODE_GEMM_MAX_M", 2)
-    monkeypatch.setattr(model_runner, "WIDE_ENGINE_OPS", eng_ops)
     assert _run("cpu", False) < 0.05
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("eng_ops", WIDE_OPS, ids=["library", "engine-qkv-down"])
-def test_engine_wide_batch_path_gpu(gpu, monkeypatch, eng_ops):
+@pytest.mark.parametrize("impl", ["auto", "tiled"])
+def test_engine_wide_batch_path_gpu(gpu, monkeypatch, impl):
+    from distributed_sse_for_llm_response_amd import ops
     from distributed_sse_for_llm_response_amd.engine import model_runner
 
     monkeypatch.setattr(model_runner, "DECODE_GEMM_MAX_M", 2)
-    monkeypatch.setattr(model_runner, "WIDE_ENGINE_OPS", eng_ops)
-    assert _run(gpu, True) < 0.1
+    if impl == "tiled":
+        monkeypatch.setenv("DSSE_GEMM_IMPL", "4")
+    ops.refresh_env()
+    try:
+        assert _run(gpu, True) < 0.1
+    finally:
+        monkeypatch.delenv("DSSE_GEMM_IMPL", raising=False)
+        ops.refresh_env()
