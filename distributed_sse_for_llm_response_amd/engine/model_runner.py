@@ -331,14 +331,12 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ prefill
     def _prefill_resid(self, a, wt, resid, norm_w, x, tmp) -> None:
-        eps = self.cfg.rms_eps
-        if tmp is None:
-            ops.gemm_resid(a, wt, resid)
-            ops.rmsnorm(resid, norm_w, x, eps)
-        else:
-            ops.gemm_out(a, wt, tmp)
-            self.comm.all_reduce(tmp)
-            ops.rmsnorm(resid, norm_w, x, eps, delta=tmp)
+        """resid += a·wᵀ, x = RMSNorm(resid).  Thousands of rows: the product goes out as a bf16 tile (row-contiguous
+        stores) and the norm kernel adds it -- the fused fp32 read-modify-write epilogue measured +120 us per
+        8192-row projection (profiles/r2/prefill_kernels_8k.md)."""
+        ops.gemm_out(a, wt, tmp)
+        self.comm.all_reduce(tmp)
+        ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 
     def prefill(self, seqs: list, ring_row: int) -> None:
         """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
@@ -396,12 +394,15 @@ class ModelRunner:
         part = math.ceil(max_ctx / 32) * 32
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d_ids)
         nl = len(w.layers)
-        # every projection on the engine's tiled-layout GEMMs with fused epilogues (csrc/kernels/gemm_tiled.hip
-        # for T > 256 rows): QKV + RoPE + paged KV write, residual add, SiLU·mul -- no [T, N] intermediates
-        tmp = torch.empty(T, H, **bf) if comm.size > 1 else None
+        # every projection on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows);
+        # gate_up with its fused SiLU·mul epilogue (no [T, 2F] intermediate)
+        tmp = torch.empty(T, H, **bf)
+        qkv = torch.empty(T, (nh + 2 * nkv) * 128, **bf)
         for li, L in enumerate(w.layers):
-            ops.gemm_qkv_rope(x, L.wqkv_t, d_pos, d_slots, self.rope, q.view(T, nh * 128), self.kv.k[li],
-                              self.kv.v[li], nh, nkv)
+            # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
+            # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
+            ops.gemm_out(x, L.wqkv_t, qkv)
+            ops.rope_kv_write(qkv, d_pos, d_slots, self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
                                 self.part_o, self.part_ml, part, 1)
             self._prefill_resid(attn.view(T, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
