@@ -1,10 +1,10 @@
 """Time to first token for long prompts (BASELINE config 4: 8k-token prompts, TTFT + ITL, TP=1/2/4/8).
 
     python tools/bench_ttft.py [--prompt-len 8192] [--prompts 1] [--iters 3] [--decode-steps 16]
-    torchrun --nproc-per-node 8 tools/bench_ttft.py ...       # TP=8 (one rank per GPU, RCCL)
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_ttft.py ...   # config 4 at TP=8 (one rank per GPU, RCCL)
 
 Per iteration: prefill `--prompts` fresh random prompts of `--prompt-len` tokens in chunks of
-`--chunk` tokens (one engine prefill call per chunk; hipBLASLt GEMMs + the flash-prefill kernel +
+`--chunk` tokens (one engine prefill call per chunk; the tiled-layout GEMMs + the flash-prefill kernel +
 paged KV writes), sample the first token, copy it to the host: that wall time is the TTFT.  Then
 `--decode-steps` graph-captured decode steps give the ITL at that context length.  Rank 0 prints one
 JSON line.  Random-init Mistral-7B-v0.3 weights (bf16), synthetic prompts.
@@ -86,7 +86,7 @@ def main():
         itl = (time.perf_counter() - t1) / max(1, args.decode_steps)
         return ttft, itl, first
 
-    one_iter()  # warm-up (hipBLASLt heuristics, allocator)
+    one_iter()  # warm-up (allocator, first launches)
     ttfts, itls = [], []
     for _ in range(args.iters):
         a, b, _ = one_iter()
