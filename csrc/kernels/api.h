@@ -79,10 +79,6 @@ struct SampleParams {
 extern "C" {
 hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int ldx, int M,
                             const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
-hipError_t dsse_gemm_xlds(int mode, int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx, int M,
-                          const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
-hipError_t dsse_gemm_xlds_partial(int mt, int nt, int nw, int depth, int Ks, int tg, const void* X, int ldx, int M,
-                                  const void* W, int K, int N, float* part, hipStream_t st);
 hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X, int ldx, int M,
                             const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_wide(int mode, int mb, int rd, int S, int partial_only, const void* X, int ldx, int M, const void* W,
@@ -107,7 +103,6 @@ hipError_t dsse_ring_advance(int* counter, hipStream_t st);
 // Checked build: first out-of-range index per kernel file (line, value, bound, count); zeros otherwise.
 hipError_t dsse_check_gemm_skinny(int* out, int clear);
 hipError_t dsse_check_gemm_stream(int* out, int clear);
-hipError_t dsse_check_gemm_xlds(int* out, int clear);
 hipError_t dsse_check_attention(int* out, int clear);
 hipError_t dsse_check_attention_prefill(int* out, int clear);
 hipError_t dsse_check_elementwise(int* out, int clear);

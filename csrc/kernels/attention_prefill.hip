@@ -17,7 +17,6 @@
 //   LDS images = K [64 keys][256 B] with the XOR-swizzled 16-byte chunks of gemm_xlds, Vᵀ [128 d]
 //                [128 B] with chunk ^= (d >> 1) & 7: both read with conflict-free ds_read_b128;
 //   softmax    = online, base 2, masked scores contribute exactly 0 (fully masked columns stay 0).
-#include <cstdlib>
 #include "api.h"
 
 #ifndef DSSE_PREFILL_NOSOFTMAX
@@ -46,17 +45,18 @@ DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
 }
 }  // namespace
 
-// DIST: K/V staging mode.  1 = the next block's loads are issued at the top of an iteration and written to LDS
-// at its end (one iteration of compute to hide the load latency); 2 = two register staging sets, block j+2's
-// loads issued in iteration j and written to LDS at the end of iteration j+1; 3 (default) = two blocks per LDS
-// stage and per barrier (8k TTFT 116.1 / 116.6 / 115.5 ms for 1 / 2 / 3, profiles/experiments_r1.md).
-template <int G, int DIST>
+// K/V staging: two 64-key blocks per LDS stage and per barrier (4 x 32 KiB dynamic LDS); the next stage's loads
+// are issued into registers at the top of an iteration and written to the other LDS stage at its end.  Measured
+// against one block per stage with one or two blocks of register prefetch, and against a software-pipelined
+// variant (QKᵀ of block j+1 in the basic block of block j's softmax): 8k TTFT 115.5 vs 116.1 / 116.6 / 116.8 ms
+// (profiles/experiments_r1.md); those variants were removed in round 2.
+template <int G>
 __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   constexpr int NW = 2 * G;
   constexpr int NT = 64 * NW;
   constexpr int PIECES = kStage / 16;  // 16-byte pieces per stage = 2048
   constexpr int PPT = PIECES / NT;             // pieces per thread
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 (DIST 1, 2) or 4 (DIST 3) stages of kStage
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 4 stages of kStage
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -131,8 +131,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   bf16x8 st0[PPT], st1[PPT];
   load_block(0, st0);
   store_block(0, st0);
-  if (DIST == 2) load_block(1, st1);
-  // one key block: ld receives the block loaded in this iteration, sv holds the block written to LDS at its end
   // softmax + PV of key block j staged in LDS buffer `buf`
   auto compute_block = [&](int j, int buf) {
     const int key0 = j * kBK;
@@ -244,246 +242,23 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
         }
     }
   };
-  auto step = [&](int j, bf16x8 (&ld)[PPT], bf16x8 (&sv)[PPT]) {
+  // stage s = blocks 2s, 2s + 1 in buffers 2 (s & 1) + {0, 1}.  Loads and stores are unconditional (pages clamp
+  // to the context; blocks past the last are never read): a branch around them made the compiler's waitcnt
+  // placement drain every load in flight (vmcnt(0)).
+  load_block(1, st1);
+  store_block(1, st1);
+  for (int j = 0; j < nblk; j += 2) {
     __syncthreads();
-    // unconditional loads and stores (pages clamp to the context; the blocks past the last are never read):
-    // a branch around them made the compiler's waitcnt placement drain every load in flight (vmcnt(0))
-    load_block(j + DIST, ld);
-    compute_block(j, j & 1);
-    store_block((j + 1) & 1, DIST == 2 ? sv : ld);
-  };
-  if constexpr (DIST == 3) {
-    // two key blocks per LDS stage and per barrier (4 x 32 KiB dynamic LDS): stage s = blocks 2s, 2s + 1 in
-    // buffers 2 (s & 1) + {0, 1}; the next stage's loads are issued at the top and written at the end
-    load_block(1, st1);
-    store_block(1, st1);
-    for (int j = 0; j < nblk; j += 2) {
-      __syncthreads();
-      const int nb = ((j >> 1) + 1) & 1;
-      load_block(j + 2, st0);
-      load_block(j + 3, st1);
-      compute_block(j, 2 * (nb ^ 1));
-      compute_block(j + 1, 2 * (nb ^ 1) + 1);
-      store_block(2 * nb, st0);
-      store_block(2 * nb + 1, st1);
-    }
-  } else {
-    for (int j = 0; j < nblk; j += 2) {
-      step(j, st0, st1);
-      // also when j + 1 == nblk (no wave sees that block: loads, stores and the barrier only) -- a branch here
-      // made the loop header's waitcnt merge drain the loads in flight
-      step(j + 1, DIST == 2 ? st1 : st0, DIST == 2 ? st0 : st1);
-    }
+    const int nb = ((j >> 1) + 1) & 1;
+    load_block(j + 2, st0);
+    load_block(j + 3, st1);
+    compute_block(j, 2 * (nb ^ 1));
+    compute_block(j + 1, 2 * (nb ^ 1) + 1);
+    store_block(2 * nb, st0);
+    store_block(2 * nb + 1, st1);
   }
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = q0 + 16 * qt + r;
-    if (qi >= qlen) continue;
-    const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
-    bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + head) * kD + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      bf16x4 v;
-      v[0] = f2bf(o[dt][qt][0] * inv);
-      v[1] = f2bf(o[dt][qt][1] * inv);
-      v[2] = f2bf(o[dt][qt][2] * inv);
-      v[3] = f2bf(o[dt][qt][3] * inv);
-      *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
-    }
-  }
-}
-
-// ---- software-pipelined variant (PIPE): QKᵀ of block j+1 is issued in the same basic block as block j's
-// softmax, so each wave's MFMA and VALU streams interleave (the one barrier per block otherwise lines all waves
-// up in the same phase: every SIMD alternates an MFMA-only and a VALU-only stretch).  Three LDS stages (K/Vᵀ of
-// blocks j, j+1 and the one being written, j+2; 96 KiB dynamic LDS), masking of diagonal blocks and the
-// deferred O rescale in their own (rare) branches around the interleaved region.
-template <int G>
-__global__ void __launch_bounds__(128 * G) flash_prefill_pipe_kernel(AttnParams p) {
-  constexpr int NW = 2 * G;
-  constexpr int NT = 64 * NW;
-  constexpr int PIECES = kStage / 16;
-  constexpr int PPT = PIECES / NT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int wh = w % G, wq = w / G;
-  const int item = blockIdx.x, h = blockIdx.y;
-  const int b = p.work_seq[item];
-  const int qlen = p.q_len[b], ctx = p.ctx_len[b];
-  const int pos0 = ctx - qlen;
-  const int tile = p.work_tile[item];
-  const int q0 = tile * kBQ + wq * 32;
-  const int wg_last_q = min(qlen, (tile + 1) * kBQ) - 1;
-  if (tile * kBQ >= qlen) return;              // uniform
-  const int kmax = pos0 + wg_last_q + 1;
-  const int nblk = (kmax + kBK - 1) / kBK;
-  const int w_first_pos = pos0 + q0;
-  const int head = h * G + wh;
-  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
-  const int npages = (kmax + kBS - 1) / kBS;
-
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = min(q0 + 16 * qt + r, qlen - 1);
-    const bf16* qp = p.q + ((size_t)(p.q_start[b] + qi) * p.hq + head) * kD + 32 * g;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[qt][s] = ld_bf16x8(qp + 8 * s);
-  }
-
-  bf16x8 st[PPT];
-  auto load_block = [&](int j) {
-    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = threadIdx.x + i * NT;
-      const int v = pc >> 10, off = pc & 1023;
-      const int page = off >> 9, o2 = off & 511;
-      const int blk = page ? blk1 : blk0;
-      const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
-                               : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
-      st[i] = ld_bf16x8(src);
-    }
-  };
-  auto store_block = [&](int buf) {
-    char* base = smem + buf * kStage;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = threadIdx.x + i * NT;
-      const int v = pc >> 10, off = pc & 1023;
-      const int page = off >> 9, o2 = off & 511;
-      int dst;
-      if (v == 0) {
-        const int key = page * kBS + (o2 >> 4), c = o2 & 15;
-        dst = key * 256 + ((c ^ swz(key & 15)) << 4);
-      } else {
-        const int d = o2 >> 2, c = page * 4 + (o2 & 3);
-        dst = kKBytes + d * 128 + ((c ^ ((d >> 1) & 7)) << 4);
-      }
-      *reinterpret_cast<bf16x8*>(base + dst) = st[i];
-    }
-  };
-  // Sᵀ[key tile kt][query tile qt] = K·Qᵀ of the block staged in `buf`
-  auto qk = [&](int buf, f32x4 (&s4)[4][2]) {
-    const char* kb = smem + buf * kStage;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int row = 16 * kt + r;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 256 + (((4 * g + s) ^ swz(r)) << 4));
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
-      }
-    }
-  };
-
-  f32x4 o[8][2];
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
-  const float sc = p.scale_log2;
-
-  load_block(0);
-  store_block(0);
-  load_block(1);
-  store_block(1);
-  __syncthreads();
-  f32x4 s_cur[4][2];
-  qk(0, s_cur);
-  for (int j = 0; j < nblk; ++j) {
-    __syncthreads();  // stage (j+1)%3 written; everyone done reading stage (j+2)%3 (= block j-1)
-    load_block(j + 2);
-    const int key0 = j * kBK;
-    if (key0 + kBK - 1 > w_first_pos) {  // diagonal block (wave-uniform): causal / tail mask
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const int qpos = pos0 + q0 + 16 * qt + r;
-        const bool qvalid = q0 + 16 * qt + r < qlen;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = key0 + 16 * kt + 4 * g + i;
-            if (!(qvalid && key <= qpos)) s_cur[kt][qt][i] = -1e30f;
-          }
-      }
-    }
-    // ---- interleaved region: QKᵀ of block j+1 || softmax of block j
-    f32x4 s_next[4][2];
-    qk((j + 1) % 3, s_next);
-    float alpha[2];
-    bool rescale = false;
-    bf16x8 pf[2][2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float mx = -1e30f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s_cur[kt][qt][i]);
-      const float m_blk = rows4_max(mx) * sc;
-      const bool up = m_blk > m_run[qt] + kRescaleThr;
-      rescale |= up;
-      const float m_new = up ? fmaxf(m_run[qt], m_blk) : m_run[qt];
-      alpha[qt] = __builtin_amdgcn_exp2f(m_run[qt] - (m_new < -1e29f ? 0.f : m_new));  // 1 when unchanged
-      m_run[qt] = m_new;
-      const float m_use = m_new < -1e29f ? 0.f : m_new;
-      float sum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s_cur[kt][qt][i], sc, -m_use));
-          s_cur[kt][qt][i] = e;
-          sum += e;
-        }
-      l_run[qt] = l_run[qt] * alpha[qt] + rows4_sum(sum);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          pf[qt][t][i] = f2bf(s_cur[2 * t][qt][i]);
-          pf[qt][t][4 + i] = f2bf(s_cur[2 * t + 1][qt][i]);
-        }
-    }
-    if (__any(rescale)) {  // rare after the first blocks (deferred rescale)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          o[dt][qt][0] *= alpha[qt];
-          o[dt][qt][1] *= alpha[qt];
-          o[dt][qt][2] *= alpha[qt];
-          o[dt][qt][3] *= alpha[qt];
-        }
-    }
-    // ---- Oᵀ[d tile][query tile] += Vᵀ · Pᵀ of block j
-    const char* vb = smem + (j % 3) * kStage + kKBytes;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const int d = 16 * dt + r;
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vb + d * 128 + (((t * 4 + g) ^ ((d >> 1) & 7)) << 4));
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
-      }
-    store_block((j + 2) % 3);
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s_cur[kt][qt] = s_next[kt][qt];
-  }
-
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qi = q0 + 16 * qt + r;
@@ -509,65 +284,20 @@ extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
   const dim3 grid(num_work, p->hkv);
-  static const bool pipe = [] {
-    const char* e = getenv("DSSE_PREFILL_PIPE");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (pipe) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_pipe_kernel<1>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kStage);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_pipe_kernel<2>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kStage);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_pipe_kernel<4>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kStage);
-      attr_set = true;
-    }
-    switch (p->group) {
-      case 1: hipLaunchKernelGGL(flash_prefill_pipe_kernel<1>, grid, dim3(128), 3 * kStage, st, *p); break;
-      case 2: hipLaunchKernelGGL(flash_prefill_pipe_kernel<2>, grid, dim3(256), 3 * kStage, st, *p); break;
-      case 4: hipLaunchKernelGGL(flash_prefill_pipe_kernel<4>, grid, dim3(512), 3 * kStage, st, *p); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  static const int dist = [] {
-    const char* e = getenv("DSSE_PREFILL_DIST");
-    return e != nullptr && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 3;
-  }();
-  if (dist == 3) {
-    static bool attr3 = false;
-    if (!attr3) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<1, 3>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<2, 3>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<4, 3>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
-      attr3 = true;
-    }
-    switch (p->group) {
-      case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 3>), grid, dim3(128), 4 * kStage, st, *p); break;
-      case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 3>), grid, dim3(256), 4 * kStage, st, *p); break;
-      case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 3>), grid, dim3(512), 4 * kStage, st, *p); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  if (dist == 2) {
-    switch (p->group) {
-      case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 2>), grid, dim3(128), 2 * kStage, st, *p); break;
-      case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 2>), grid, dim3(256), 2 * kStage, st, *p); break;
-      case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 2>), grid, dim3(512), 2 * kStage, st, *p); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<4>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+    attr_set = true;
   }
   switch (p->group) {
-    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1, 1>), grid, dim3(128), 2 * kStage, st, *p); break;
-    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2, 1>), grid, dim3(256), 2 * kStage, st, *p); break;
-    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4, 1>), grid, dim3(512), 2 * kStage, st, *p); break;
+    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1>), grid, dim3(128), 4 * kStage, st, *p); break;
+    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2>), grid, dim3(256), 4 * kStage, st, *p); break;
+    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4>), grid, dim3(512), 4 * kStage, st, *p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -91,38 +91,6 @@ void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
   (void)mode;
 }
 
-// X-in-LDS kernel configuration (gemm_xlds.hip).  Env overrides: DSSE_X_KS, DSSE_X_NW, DSSE_X_NT, DSSE_X_TG,
-// DSSE_X_DEPTH.
-struct XCfg {
-  int mt, nt, nw, depth, ks, tg, S;
-};
-// Defaults from the gfx950 sweep (tools/tune_gemm.py --grid, profiles/gemm_sweep_r1.md): 8 waves, 4-deep
-// weight ring, K-slices of 1024 (512 for the small O projection, 2048 for wide layers at M <= 32), and
-// ~224 workgroups so that the one-workgroup-per-CU grid stays balanced.
-XCfg pick_xlds(int M, int N, int K) {
-  XCfg c{};
-  c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  c.nt = env_int("DSSE_X_NT", 1);
-  c.nw = env_int("DSSE_X_NW", 8);
-  c.depth = env_int("DSSE_X_DEPTH", 4);
-  int ks = env_int("DSSE_X_KS", 0);
-  if (ks <= 0) {
-    ks = 1024;
-    if (N <= 4096 && K <= 4096) ks = 512;
-    if (N >= 16384 && M <= 32) ks = 2048;
-  }
-  ks = std::min(ks, (65536 / (16 * c.mt)) / 128 * 128);  // <= 128 KiB of LDS
-  ks = std::max(128, std::min(ks, K)) / 128 * 128;
-  c.ks = ks;
-  c.S = (K + ks - 1) / ks;
-  const int TG = N / (16 * c.nt);
-  int tg = env_int("DSSE_X_TG", 0);
-  if (tg == -1) tg = (TG * c.S + 255) / 256;  // exactly one workgroup per CU
-  if (tg <= 0) tg = std::max(c.nw, (TG * c.S / 224 / c.nw) * c.nw);
-  c.tg = std::min(tg, TG);
-  return c;
-}
-
 // X-streaming kernel configuration (gemm_stream.hip).  Env overrides: DSSE_S_NT, DSSE_S_NW, DSSE_S_RD,
 // DSSE_S_SPLIT.
 struct SCfg {
@@ -214,15 +182,15 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 10) {
+  if (cfg < 0 || cfg > 3) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile (8 waves of 128x64, 2 LDS stages) is
     // the fastest once it yields >= ~160 workgroups (1.20-1.24 PFLOP/s at 8192 rows); below that, the
     // 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
     const int big_tiles = ((M + 255) / 256) * (N / 256);
     cfg = (N % 256 == 0 && big_tiles >= 160) ? 3 : (M > 128 ? 0 : 1);
   }
-  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 128 for 0/1/5/7
-  const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : ((cfg <= 1 || cfg == 5 || cfg == 7) ? 128 : 256);
+  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 256 for cfg 3
+  const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : (cfg == 3 ? 256 : 128);
   c.cfg = cfg;
   c.S = 1;
   c.ok = N % BN == 0 && K % 64 == 0;
@@ -237,9 +205,9 @@ TCfg pick_tiled(int M, int N, int K) {
   return c;
 }
 
-// 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 1 = X-in-LDS with a
-// whole K-slice staged (gemm_xlds.hip), 2 = X streamed through LDS slices (gemm_stream.hip).
-// DSSE_GEMM_IMPL forces one.
+// 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 2 = X streamed through LDS
+// slices (gemm_stream.hip), 3 = gemm_wide.hip (32x32 MFMAs), 4 = gemm_tiled.hip (register-blocked, LDS-DMA).
+// DSSE_GEMM_IMPL forces one (1, the removed whole-slice X-in-LDS kernel, maps to the fallback).
 int gemm_impl(int M, int N, int K) {
   const int impl = env_int("DSSE_GEMM_IMPL", -1);
   if (M > 64) {
@@ -256,15 +224,18 @@ int gemm_impl(int M, int N, int K) {
     if (wide_ok) return 3;
     return tiled_ok ? 4 : -1;
   }
+  // M <= 64: 0 = register-streaming skinny kernel (tiny batches), 2 = gemm_stream; a shape outside the
+  // stream kernel's contract goes to gemm_tiled, else the skinny kernel (no shape contract beyond N % 16)
+  const int fallback = pick_tiled(M, N, K).ok ? 4 : 0;
   if (impl >= 0) {
-    if (impl == 4) return pick_tiled(M, N, K).ok ? 4 : (pick_stream(M, N, K).ok ? 2 : 1);
-    if (impl == 3 && !pick_wide(M, N, K).ok) return pick_stream(M, N, K).ok ? 2 : 1;
-    if (impl == 2 && !pick_stream(M, N, K).ok) return 1;
-    return impl;
+    if (impl == 4) return fallback;
+    if (impl == 3 && !pick_wide(M, N, K).ok) return pick_stream(M, N, K).ok ? 2 : fallback;
+    if (impl == 2 && !pick_stream(M, N, K).ok) return fallback;
+    return impl == 1 ? fallback : impl;
   }
   if (M <= 8) return 0;
   if (M <= 16 && N < 16384) return 0;
-  return pick_stream(M, N, K).ok ? 2 : 1;
+  return pick_stream(M, N, K).ok ? 2 : fallback;
 }
 
 void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
@@ -304,15 +275,6 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
     DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
                                     c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
-    return;
-  }
-  if (impl == 1) {
-    XCfg c = pick_xlds(M, N, K);
-    if (N % (16 * c.nt) != 0) c.nt = 1;
-    at::Tensor part;
-    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
-    DSSE_CHECK_HIP(dsse_gemm_xlds(mode, c.mt, c.nt, c.nw, c.depth, c.ks, c.tg, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
-                                  c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
     return;
   }
   int mt, nt, kw;
@@ -385,16 +347,6 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
       dsse::GemmEpi ep{};
       DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kResidAdd, c.mt, c.nt, c.nw, c.rd, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N,
                                       &ep, part.data_ptr<float>(), cur_stream()));
-      return c.S;
-    }
-  } else if (impl == 1) {
-    XCfg c = pick_xlds(M, N, K);
-    if (N % (16 * c.nt) != 0) c.nt = 1;
-    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
-      check_dtype(x, at::kBFloat16, "x");
-      check_dtype(w, at::kBFloat16, "w");
-      DSSE_CHECK_HIP(dsse_gemm_xlds_partial(c.mt, c.nt, c.nw, c.depth, c.ks, c.tg, x.data_ptr(), K, M, w.data_ptr(), K,
-                                            N, part.data_ptr<float>(), cur_stream()));
       return c.S;
     }
   }
@@ -678,7 +630,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 6; }
+int64_t kernels_abi_version() { return 7; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -686,19 +638,19 @@ bool kernels_checked() { return true; }
 bool kernels_checked() { return false; }
 #endif
 
-// Checked build: [8, 4] int32 (line, value, bound, count) of the first out-of-range index per kernel file,
+// Checked build: [7, 4] int32 (line, value, bound, count) of the first out-of-range index per kernel file,
 // in the order of kCheckFiles; all zeros in the default build.  Synchronises the device.
-const char* const kCheckFiles[8] = {"gemm_skinny.hip", "gemm_stream.hip", "gemm_xlds.hip", "attention.hip",
-                                    "attention_prefill.hip", "elementwise.hip", "sampler.hip", "gemm_tiled.hip"};
+const char* const kCheckFiles[7] = {"gemm_skinny.hip", "gemm_stream.hip", "attention.hip", "attention_prefill.hip",
+                                    "elementwise.hip", "sampler.hip", "gemm_tiled.hip"};
 Tensor kernel_checks(bool clear) {
   using Reader = hipError_t (*)(int*, int);
-  static const Reader readers[8] = {dsse_check_gemm_skinny, dsse_check_gemm_stream, dsse_check_gemm_xlds,
-                                    dsse_check_attention, dsse_check_attention_prefill, dsse_check_elementwise,
-                                    dsse_check_sampler, dsse_check_gemm_tiled};
-  Tensor out = at::zeros({8, 4}, at::kInt);
+  static const Reader readers[7] = {dsse_check_gemm_skinny, dsse_check_gemm_stream, dsse_check_attention,
+                                    dsse_check_attention_prefill, dsse_check_elementwise, dsse_check_sampler,
+                                    dsse_check_gemm_tiled};
+  Tensor out = at::zeros({7, 4}, at::kInt);
   if (!kernels_checked()) return out;
   DSSE_CHECK_HIP(hipDeviceSynchronize());
-  for (int i = 0; i < 8; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
+  for (int i = 0; i < 7; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
   return out;
 }
 std::string kernel_check_files() {

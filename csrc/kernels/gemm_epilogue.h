@@ -1,4 +1,4 @@
-// Fused epilogues shared by the X-in-LDS decode GEMMs (gemm_xlds.hip, gemm_stream.hip) and their
+// Fused epilogues shared by the engine GEMMs (gemm_stream.hip, gemm_wide.hip, gemm_tiled.hip) and their
 // split-K reduction.  Output element (m, n = 16·tile + r) with `partner` = the value of column
 // n ^ 8 of the same row (the gate/up or rotary partner under the engine's row permutations).
 #pragma once

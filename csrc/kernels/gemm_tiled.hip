@@ -180,166 +180,6 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
       }
 }
 
-// ---- register ping-pong variant: 32-deep K stages in an NQ-deep LDS ring ---------------------------------
-// Each iteration publishes stage t+1 (barrier), issues the DMA of stage t+NQ-1 into the buffer stage t-1 used,
-// reads stage t+1's fragments into one register set and runs stage t's MFMAs from the other: the LDS read
-// latency hides under the MFMA cluster, and every stage's DMA has NQ-2 iterations to land.
-// A stage: X [BM rows][64 B] (4 pieces per row, piece q of row `row` at slot q ^ ((row >> 2) & 3)) + the
-// (tile, k-step) 1 KiB weight blocks of the BN/16 tiles.
-template <int WM, int WN, int MT, int NT, int NQ>
-struct PPGeom {
-  static constexpr int BM = WM * MT * 16, BN = WN * NT * 16, NTHR = 64 * WM * WN;
-  static constexpr int A_BYTES = BM * 64, B_BYTES = (BN / 16) * 1024, STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_INS = A_BYTES / 1024 / (WM * WN), B_INS = B_BYTES / 1024 / (WM * WN);
-  static_assert(A_BYTES % (1024 * WM * WN) == 0 && B_BYTES % (1024 * WM * WN) == 0, "stage not divisible");
-  static constexpr size_t LDS = (size_t)NQ * STAGE;
-};
-
-template <int WM, int WN, int MT, int NT, int NQ, int MODE>
-__global__ void __launch_bounds__(64 * WM * WN)
-gemm_tiled_pp_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
-                     GemmEpi ep, float* __restrict__ part) {
-  using G = PPGeom<WM, WN, MT, NT, NQ>;
-  static_assert(NQ >= 3, "ring of at least 3 stages");
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = w / WN, wn = w % WN;
-
-  const int nbm = (M + G::BM - 1) / G::BM, nbn = N / G::BN, ntile = nbm * nbn;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
-  const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
-  const int ks = lid / ntile, tl = lid % ntile;
-  constexpr int GM = 8;
-  const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
-  const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
-  const int m0 = bm * G::BM, n0 = bn * G::BN;
-  const int k0 = ks * Kr, nk = Kr >> 5;
-  const int KC = K >> 7;
-
-  const bf16* a_src[G::A_INS];
-#pragma unroll
-  for (int i = 0; i < G::A_INS; ++i) {
-    const int row = (w * G::A_INS + i) * 16 + (lane >> 2);
-    const int gp = (lane & 3) ^ ((row >> 2) & 3);
-    a_src[i] = X + (size_t)min(m0 + row, M - 1) * ldx + 32 * gp;
-  }
-  const bf16* b_src[G::B_INS];
-#pragma unroll
-  for (int i = 0; i < G::B_INS; ++i)
-    b_src[i] = W + ((size_t)(n0 / 16 + w * G::B_INS + i) * KC) * kTileChunk + lane * 8;
-
-  // DMA of stage t into buffer t % NQ.  Stages past the end (t >= nk) re-load the last stage into a buffer
-  // no real stage uses any more: every iteration then issues exactly one stage, so the counted waits are
-  // constants and the loop has no data-dependent branch (hipcc's waitcnt pass merges paths conservatively).
-  auto issue = [&](int t) {
-    const int kk = k0 + 32 * min(t, nk - 1), c = kk >> 7, sb = (kk >> 5) & 3;
-    char* base = smem + (t % NQ) * G::STAGE;
-#pragma unroll
-    for (int i = 0; i < G::A_INS; ++i) glds16(a_src[i] + c * 128 + 8 * sb, base + (w * G::A_INS + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < G::B_INS; ++i)
-      glds16(b_src[i] + (size_t)c * kTileChunk + sb * 512, base + G::A_BYTES + (w * G::B_INS + i) * 1024);
-  };
-
-  int a_off[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = wm * MT * 16 + 16 * mt + r;
-    a_off[mt] = row * 64 + ((g ^ ((row >> 2) & 3)) << 4);
-  }
-  auto read = [&](int t, bf16x8 (&a)[MT], bf16x8 (&b)[NT]) {
-    const char* As = smem + (t % NQ) * G::STAGE;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-      b[nt] = *reinterpret_cast<const bf16x8*>(As + G::A_BYTES + (wn * NT + nt) * 1024 + lane * 16);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt] = *reinterpret_cast<const bf16x8*>(As + a_off[mt]);
-  };
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&a)[MT], const bf16x8 (&b)[NT]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(a[mt], b[nt], acc[mt][nt]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  constexpr int INS = G::A_INS + G::B_INS;
-  // wait until at most n stages of this wave's DMA are outstanding, then barrier (n: 0..3, wave-uniform)
-  auto wait_barrier = [&](int n) {
-    if (n >= 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(3 * INS) : "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * INS) : "memory");
-    else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  static_assert(NQ <= 6, "wait_barrier counts up to 3 stages in flight");
-  // prologue: stages 0 .. NQ-2 in flight; stage 0 landed everywhere before its fragments are read
-#pragma unroll
-  for (int q = 0; q < NQ - 1; ++q) issue(q);
-  wait_barrier(NQ - 2);
-  bf16x8 aX[MT], bX[NT], aY[MT], bY[NT];
-  read(0, aX, bX);
-
-  // iteration t: publish stage t+1 (issued so far: stages <= min(t + NQ - 2, nk - 1)), DMA stage t+NQ-1 into
-  // the buffer of stage t-1 (every wave consumed its fragments in iteration t-1, before this barrier), read
-  // stage t+1 into one register set, MFMAs of stage t from the other
-  // The barrier, the DMA and the fragment reads are unconditional (the last iteration reads a buffer it never
-  // uses): a read skipped on one path makes hipcc wait lgkmcnt(0) before the MFMAs -- for the reads of
-  // stage t+1 too -- instead of only for stage t's.
-  // lgkmcnt(0) after the barrier (stage t's fragment reads, issued a whole MFMA cluster ago, are long done):
-  // with 2 x 12 reads in flight the 4-bit LDS counter cannot single out the older set, and hipcc would wait
-  // lgkmcnt(0) AFTER issuing stage t+1's reads instead (measured in the .s: no overlap).  As the builtin,
-  // the waitcnt pass sees it.  Encoding (gfx9): vmcnt 63 / expcnt 7 = no wait, lgkmcnt 0.
-  auto step = [&](int t, bf16x8 (&ac)[MT], bf16x8 (&bc)[NT], bf16x8 (&an)[MT], bf16x8 (&bn_)[NT]) {
-    wait_barrier(NQ - 3);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    issue(t + NQ - 1);
-    read(t + 1, an, bn_);
-    mma(ac, bc);
-  };
-  for (int t = 0; t < nk; t += 2) {
-    step(t, aX, bX, aY, bY);
-    step(t + 1, aY, bY, aX, bX);  // nk is even (Kr % 64 == 0, host-checked)
-  }
-
-  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
-  const int row0 = m0 + wm * MT * 16, tile0 = n0 / 16 + wn * NT;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = acc[mt][nt][i];
-        const float partner = (MODE == kSiluMul || MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
-        epilogue<MODE>(ep, part_ks, M, N, row0 + 16 * mt + 4 * g + i, tile0 + nt, r, v, partner);
-      }
-}
-
-template <int WM, int WN, int MT, int NT, int NQ, int MODE>
-static hipError_t launch_pp(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
-                            float* part, hipStream_t st) {
-  using G = PPGeom<WM, WN, MT, NT, NQ>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tiled_pp_kernel<WM, WN, MT, NT, NQ, MODE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
-    attr_set = true;
-  }
-  const int nbm = (M + G::BM - 1) / G::BM, nbn = N / G::BN;
-  hipLaunchKernelGGL((gemm_tiled_pp_kernel<WM, WN, MT, NT, NQ, MODE>), dim3(nbm * nbn * S), dim3(G::NTHR), G::LDS, st,
-                     X, ldx, M, W, K, N, K / S, ep, part);
-  return hipGetLastError();
-}
-
 template <int WM, int WN, int MT, int NT, int NS, int FB, int MODE>
 static hipError_t launch_t(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
@@ -360,24 +200,20 @@ template <int MODE>
 static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                                 const GemmEpi& ep, float* part, hipStream_t st) {
   switch (cfg) {
+    // measured on MI355X (profiles/r2/gemm_tiled_v*.log); other tile / ring shapes tried and removed are listed
+    // in profiles/experiments_r2.md
     case 0: return launch_t<4, 2, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 128, 8 waves
     case 1: return launch_t<2, 2, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 128, 4 waves
     case 2: return launch_t<4, 1, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 waves
     case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
-    case 4: return launch_t<4, 2, 4, 8, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
-    case 5: return launch_t<4, 2, 4, 4, 3, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // cfg 0, FB 1
-    case 6: return launch_pp<2, 4, 8, 4, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);   // 256 x 256 ping-pong
-    case 7: return launch_pp<4, 2, 4, 4, 5, MODE>(X, ldx, M, W, K, N, S, ep, part, st);   // 256 x 128 ping-pong
-    case 8: return launch_pp<2, 4, 8, 4, 5, MODE>(X, ldx, M, W, K, N, S, ep, part, st);   // 256 x 256, 5 stages
-    case 9: return launch_pp<2, 2, 8, 8, 4, MODE>(X, ldx, M, W, K, N, S, ep, part, st);   // 256 x 256, 4 waves
-    case 10: return launch_pp<2, 2, 8, 8, 5, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 4 waves, 5 st
   }
   return hipErrorInvalidValue;
 }
 
 }  // namespace dsse
 
-// cfg: 0 = 256 x 128 tile (8 waves), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves).
+// cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves),
+// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages: the prefill shape).
 // Shape contract (checked by the caller): N % BN == 0, K % (64 S) == 0, the tiled weight layout (api.h).
 // S > 1: fp32 slabs [S, M, N] into `part`, reduced by launch_splitk_reduce unless partial_only.
 extern "C" hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M,

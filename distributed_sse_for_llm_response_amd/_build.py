@@ -69,7 +69,6 @@ def _parallel(jobs, verbose):
 
 
 KERNEL_VARIANTS = {
-    "nt": ["-DDSSE_W_NT=1"],           # experiment build (non-temporal weight loads everywhere)
     "checked": ["-DDSSE_KERNEL_CHECKS=1"],
     "noxcd": ["-DDSSE_XCD_SPLITK=0"],  # experiment build (split-K workgroups in plain dispatch order)
     "pfnosm": ["-DDSSE_PREFILL_NOSOFTMAX=1"],  # timing experiment only: flash prefill without the softmax (wrong output)

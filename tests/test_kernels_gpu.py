@@ -25,10 +25,6 @@ def _close(a, b, atol, rtol, what=""):
 
 GEMM_CONFIGS = {
     "auto": {},
-    "xlds-default": {"DSSE_GEMM_IMPL": "1"},
-    "xlds-ks256-nw4": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "256", "DSSE_X_NW": "4"},
-    "xlds-ks512-nt2": {"DSSE_GEMM_IMPL": "1", "DSSE_X_KS": "512", "DSSE_X_NT": "2", "DSSE_X_TG": "3"},
-    "xlds-d8": {"DSSE_GEMM_IMPL": "1", "DSSE_X_DEPTH": "8", "DSSE_X_TG": "16"},
     "stream-default": {"DSSE_GEMM_IMPL": "2"},
     "stream-nt2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NT": "2"},
     "stream-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
@@ -38,6 +34,7 @@ GEMM_CONFIGS = {
     "tiled-default": {"DSSE_GEMM_IMPL": "4"},
     "tiled-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "1", "DSSE_T_SPLIT": "2"},
     "tiled-256x64": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "2"},
+    "tiled-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "3"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
@@ -383,7 +380,7 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 6
+    assert torch.ops.dsse.kernels_abi_version() == 7
     assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
 
 
