@@ -23,9 +23,21 @@
 #define DSSE_PREFILL_NOSOFTMAX 0
 #endif
 
+// K/V staging by LDS-DMA (global_load_lds, no VGPRs, no ds_write pass) -- 1, default -- or through registers
+// (0, variant build "pfregs": the round-1 form, kept for A/B).
+#ifndef DSSE_PREFILL_GLDS
+#define DSSE_PREFILL_GLDS 1
+#endif
+
 namespace dsse {
 
 namespace {
+DEV void glds16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(src),
+                                   reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                       reinterpret_cast<uintptr_t>(lds_base)),
+                                   16, 0, 0);
+}
 constexpr int kD = 128;
 constexpr int kBQ = 64;    // query tokens per workgroup
 constexpr int kBK = 64;    // keys per iteration (2 pages)
@@ -120,6 +132,30 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
     }
   };
 
+  // LDS-DMA form: a stage is 32 x 1 KiB DMA instructions, IPW per wave.  Instruction q < 16 fills keys 4q..4q+3
+  // (lane -> key 4q + lane / 16, LDS slot lane % 16 = chunk ^ swz(key)); q >= 16 fills Vᵀ rows d = 8 (q - 16)
+  // + lane / 8 (slot lane % 8 = chunk ^ ((d >> 1) & 7), chunk = page * 4 + 8-token group).  The swizzles sit
+  // on the source address because the DMA writes LDS lane-linearly; the reads are unchanged.
+  constexpr int IPW = 32 / NW;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue_block = [&](int j, int buf) {
+    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
+    char* base = smem + buf * kStage;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int q = wu * IPW + i;  // wave-uniform
+      const bf16* src;
+      if (q < 16) {
+        const int key = 4 * q + (lane >> 4), c = (lane & 15) ^ swz(key & 15);
+        src = p.k_cache + (((size_t)(q >= 8 ? blk1 : blk0) * p.hkv + h) * kBS + (key & 31)) * kD + 8 * c;
+      } else {
+        const int d = 8 * (q - 16) + (lane >> 3), c = (lane & 7) ^ ((d >> 1) & 7);
+        src = p.v_cache + (((size_t)(c >= 4 ? blk1 : blk0) * p.hkv + h) * kD + d) * kBS + 8 * (c & 3);
+      }
+      glds16(src, base + q * 1024);
+    }
+  };
+
   f32x4 o[8][2];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt)
@@ -128,9 +164,14 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
   const float sc = p.scale_log2;
 
+#if !DSSE_PREFILL_GLDS
   bf16x8 st0[PPT], st1[PPT];
   load_block(0, st0);
   store_block(0, st0);
+#else
+  (void)load_block;
+  (void)store_block;
+#endif
   // softmax + PV of key block j staged in LDS buffer `buf`
   auto compute_block = [&](int j, int buf) {
     const int key0 = j * kBK;
@@ -245,6 +286,20 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   // stage s = blocks 2s, 2s + 1 in buffers 2 (s & 1) + {0, 1}.  Loads and stores are unconditional (pages clamp
   // to the context; blocks past the last are never read): a branch around them made the compiler's waitcnt
   // placement drain every load in flight (vmcnt(0)).
+#if DSSE_PREFILL_GLDS
+  // the barrier's fence waits vmcnt(0): the pair's DMA (issued an iteration earlier) has landed everywhere, and
+  // every wave is done reading the other pair, which this iteration's DMA then overwrites
+  issue_block(0, 0);
+  issue_block(1, 1);
+  for (int j = 0; j < nblk; j += 2) {
+    __syncthreads();
+    const int nb = ((j >> 1) + 1) & 1;
+    issue_block(j + 2, 2 * nb);
+    issue_block(j + 3, 2 * nb + 1);
+    compute_block(j, 2 * (nb ^ 1));
+    compute_block(j + 1, 2 * (nb ^ 1) + 1);
+  }
+#else
   load_block(1, st1);
   store_block(1, st1);
   for (int j = 0; j < nblk; j += 2) {
@@ -257,6 +312,7 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
     store_block(2 * nb, st0);
     store_block(2 * nb + 1, st1);
   }
+#endif
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
 #pragma unroll
