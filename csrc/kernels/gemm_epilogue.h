@@ -49,6 +49,24 @@ DEV void epilogue(const GemmEpi& ep, float* part, int M, int N, int m, int tile,
   }
 }
 
+// SiLU·mul epilogue of one 16x16 accumulator (rows m0 + i, i = 0..3, column 16·tile + r) for the 16x16x32 MFMA
+// layout: lanes r < 8 hold gate columns, lanes r >= 8 the matching up columns (partner = lane ^ 8).  After the
+// exchange both lanes of a pair hold the four (gate, up) pairs; the low lane finishes rows 0-1 and the high lane
+// rows 2-3, so every lane does useful SiLU work (the per-element form ran it on half the lanes).
+DEV void silu_epilogue4(const GemmEpi& ep, int M, int m0, int tile, int r, const f32x4& v) {
+  float p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p[i] = __shfl_xor(v[i], 8);
+  const bool lo = r < 8;
+  bf16* out = reinterpret_cast<bf16*>(ep.out) + tile * 8 + (r & 7);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float gate = lo ? v[k] : p[2 + k], up = lo ? p[k] : v[2 + k];
+    const int m = m0 + (lo ? k : 2 + k);
+    if (m < M) out[(size_t)m * ep.ldo] = f2bf(silu(gate) * up);
+  }
+}
+
 // Sum the S partial slabs and apply the epilogue.  One thread per (row, 16-column tile, j < 8):
 // it owns columns tile*16 + j and tile*16 + 8 + j (the epilogue partners).
 template <int MODE>

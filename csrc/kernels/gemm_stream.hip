@@ -216,6 +216,13 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
   if (TOUCH && M < 0) part[touch & 1] = (float)touch;  // never runs: keeps the warm-up loads
 
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
+  if constexpr (MODE == kSiluMul) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) silu_epilogue4(ep, M, m0 + 16 * mt + 4 * g, tgi * NT + t, r, acc[mt][t]);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

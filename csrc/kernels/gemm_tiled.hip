@@ -168,6 +168,13 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
 
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
   const int row0 = m0 + wm * MT * 16, tile0 = n0 / 16 + wn * NT;
+  if constexpr (MODE == kSiluMul) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) silu_epilogue4(ep, M, row0 + 16 * mt + 4 * g, tile0 + nt, r, acc[mt][nt]);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

@@ -88,3 +88,22 @@ def test_engine_wide_batch_path_gpu(gpu, monkeypatch, impl):
     finally:
         monkeypatch.delenv("DSSE_GEMM_IMPL", raising=False)
         ops.refresh_env()
+
+
+def test_engine_forward_has_no_library_gemm():
+    """Every projection of prefill and decode goes through the engine's GEMM ops (tiled weight layout): the
+    model runner never calls a library matmul, and the engine weights hold no row-major copy."""
+    import ast
+    import inspect
+
+    from distributed_sse_for_llm_response_amd.engine import model_runner
+
+    tree = ast.parse(inspect.getsource(model_runner))
+    for node in ast.walk(tree):
+        assert not isinstance(node, ast.BinOp) or not isinstance(node.op, ast.MatMult), ast.unparse(node)
+        if isinstance(node, ast.Attribute):
+            assert node.attr not in ("matmul", "mm", "bmm", "addmm", "linear"), ast.unparse(node)
+    w = convert_standard(TINY, init_standard_weights(TINY, seed=1))
+    assert w.lm_head is None and all(L.wqkv is None and L.wo is None and L.wgu is None and L.wd is None
+                                     for L in w.layers)
+    assert w.nbytes() > 0
