@@ -197,12 +197,19 @@ def run_decode_bench(model="mistral-7b-v0.3", device=None, streams=64, prompt_le
 
 
 def spawn_client():
-    """Start the SSE client process (call BEFORE the GPU is initialised in this process)."""
+    """Start the SSE client process (call BEFORE the GPU is initialised in this process).  The package's parent
+    directory goes on the child's PYTHONPATH, so the client starts whatever the working directory is (e.g.
+    under rocprofv3 run from /tmp)."""
+    import os
     import subprocess
     import sys
+    from pathlib import Path
 
+    env = dict(os.environ)
+    root = str(Path(__file__).resolve().parents[2])
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     return subprocess.Popen([sys.executable, "-m", "distributed_sse_for_llm_response_amd.engine.bench_client"],
-                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
 
 
 def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, prompt_len=512, steps=64, warmup=8,
