@@ -188,7 +188,13 @@ TCfg pick_tiled(int M, int N, int K) {
     // 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
     const int big_tiles = ((M + 255) / 256) * (N / 256);
     cfg = (N % 256 == 0 && big_tiles >= 160) ? 3 : (M > 128 ? 0 : 1);
+    // narrow projections of the wide decode buckets (N <= 8192, 128 < M <= 512: qkv / o / down at 192-256
+    // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
+    // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
+    const int narrow = env_int("DSSE_T_NARROW_CFG", 1);
+    if (narrow >= 0 && narrow <= 3 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
   }
+  const int min_wgs = env_int("DSSE_T_MIN_WGS", 160);  // split K until this many workgroups (M <= 512)
   // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 256 for cfg 3
   const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : (cfg == 3 ? 256 : 128);
   c.cfg = cfg;
@@ -199,7 +205,7 @@ TCfg pick_tiled(int M, int N, int K) {
   int S = env_int("DSSE_T_SPLIT", 0);
   if (S <= 0 || K % (64 * S) != 0) {
     S = 1;  // split K only for the few-tile wide-decode shapes (slabs cost M x N x 4 B each)
-    while (M <= kMaxDecodeM && tiles * S < 160 && K % (64 * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
+    while (M <= kMaxDecodeM && tiles * S < min_wgs && K % (64 * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
   }
   c.S = S;
   return c;
