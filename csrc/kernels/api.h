@@ -52,6 +52,16 @@ struct AttnParams {
   int nparts;               // grid.z
   float scale_log2;         // log2(e) / sqrt(128)
   int kwv;                  // decode: waves per workgroup splitting the keys (0 = by grid size)
+  // mode 3 (decode with the QKV epilogue folded in): q comes from the QKV GEMM's fp32 split-K slabs instead
+  // of `q`; the workgroup holding a sequence's newest key also writes that token's K / V into the cache.
+  const float* qkv_part;    // [qkv_S, qkv_M, (hq + 2 hkv) * 128], columns in the engine's rotary-pair order
+  int qkv_S, qkv_M;
+  const int* positions;     // [qkv_M] absolute position of row m (RoPE)
+  const int* slots;         // [qkv_M] KV slot of row m (-1 = do not write)
+  const float2* rope;       // [rope_len, 64] (cos, sin)
+  int rope_len, num_slots;
+  bf16* k_out;              // = k_cache, writable
+  bf16* v_out;              // = v_cache, writable
 };
 
 struct SampleParams {

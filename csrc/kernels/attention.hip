@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "api.h"
+#include "gemm_epilogue.h"
 
 namespace dsse {
 
@@ -27,9 +28,12 @@ constexpr int kPage = 32;
 constexpr int kD = 128;
 
 
-template <int QW, int KWV, bool PF = false>
-__global__ void __launch_bounds__(64 * QW * KWV)
+// One-wave decode workgroups (256+ streams) are held to 4 waves per SIMD: the folded QKV epilogue (FQ) otherwise
+// raises the register peak from 127 to 159 and costs a wave per SIMD; 104 VGPRs, no spills.
+template <int QW, int KWV, bool PF = false, bool FQ = false>
+__global__ void __launch_bounds__(64 * QW * KWV, QW * KWV == 1 ? 4 : 1)
 paged_attention_kernel(AttnParams p) {
+  static_assert(!(PF && FQ), "the folded QKV epilogue patches the non-prefetching page loop");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int qw = w / KWV, kw = w % KWV;
@@ -57,7 +61,97 @@ paged_attention_kernel(AttnParams p) {
   // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32s + 8g + j] in k-step s — the same head-dim
   // order as the K fragments, so each K load instruction reads 64 contiguous bytes of 16 key rows.
   bf16x8 qf[4];
-  {
+  // FQ: the newest key's K row / V row, computed from the slabs by the key-split wave that attends over its
+  // page.  That wave starts its online softmax with this key and masks it out of the page loop (its cache slot
+  // is written in this launch, by the same wave, for later steps).  Patching the page's fragments in registers
+  // instead cost 50-80 VGPRs (a wave per SIMD).
+  constexpr int kMaxG = 8;  // GQA group bound of the folded path (the bindings fall back above it)
+  __shared__ __attribute__((aligned(16))) bf16 s_fq[FQ ? KWV : 1][FQ ? (kMaxG + 2) * kD : 1];  // q heads | k | v
+  float sc_new = -INFINITY;  // newest key's score (log2 units) for column r
+  int kb_new = -1;            // first key of the newest key's page, or -1 when this wave does not hold it
+  int key_limit = col_limit;  // keys below are attended in the page loop
+  if constexpr (FQ) {
+    // QKV epilogue folded in (decode, one query per sequence = QKV row q_start[b]): sum the split-K slabs,
+    // rotate, round to bf16 -- the arithmetic of splitk_reduce_kernel<kQkvRope>, in the same order.  Head
+    // columns are in rotary-pair order: 16-column tile t of a head holds d = 8t + j (j < 8) and, 8 columns on,
+    // its partner d + 64.  Lane l sums the pair (t, j) = (l / 8, l % 8) of every unit it needs -- all slab
+    // loads of the wave are independent, so the slab latency is paid once -- and the rotated values are
+    // regrouped into MFMA fragments through the wave's LDS rows.
+    const int m = p.q_start[b];
+    const int N = (p.hq + 2 * p.hkv) * kD;
+    const size_t slab = (size_t)p.qkv_M * N;
+    const int kn_page = (ctx - 1) & ~(kPage - 1);
+    const int sl = p.slots[m];
+    // wave-uniform: this partition holds the newest key, and the key-split wave visiting its page is this one
+    const bool owner = pz == (ctx - 1) / p.part && sl >= 0 && ((kn_page - kbeg) / kPage) % KWV == kw;
+    const int t = lane >> 3, j = lane & 7;
+    const float* base = p.qkv_part + (size_t)m * N + 16 * t + j;
+    float qa[kMaxG][2], ka[2] = {0.f, 0.f}, va[2] = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kMaxG; ++u) qa[u][0] = qa[u][1] = 0.f;
+    // unconditional loads (heads past the group re-read its last head): a guarded load is a branch, and hipcc
+    // drains vmcnt at every branch -- one slab latency per head
+#pragma unroll 2
+    for (int k = 0; k < p.qkv_S; ++k) {
+      const float* sk = base + k * slab;
+#pragma unroll
+      for (int u = 0; u < kMaxG; ++u) {
+        const int uu = min(u, G - 1);
+        qa[u][0] += sk[(h * G + uu) * kD];
+        qa[u][1] += sk[(h * G + uu) * kD + 8];
+      }
+      ka[0] += sk[(p.hq + h) * kD];
+      ka[1] += sk[(p.hq + h) * kD + 8];
+      va[0] += sk[(p.hq + p.hkv + h) * kD];
+      va[1] += sk[(p.hq + p.hkv + h) * kD + 8];
+    }
+    const float2 c = p.rope[(size_t)DSSE_IDX(p.positions[m], p.rope_len, 0) * 64 + 8 * t + j];
+    bf16* fq = s_fq[kw];
+    const int d = 8 * t + j;  // this lane's head dims: d and d + 64
+#pragma unroll
+    for (int u = 0; u < kMaxG; ++u)
+      if (u < G) {
+        fq[u * kD + d] = f2bf(qa[u][0] * c.x - qa[u][1] * c.y);
+        fq[u * kD + 64 + d] = f2bf(qa[u][1] * c.x + qa[u][0] * c.y);
+      }
+    if (owner) {
+      fq[kMaxG * kD + d] = f2bf(ka[0] * c.x - ka[1] * c.y);
+      fq[kMaxG * kD + 64 + d] = f2bf(ka[1] * c.x + ka[0] * c.y);
+      fq[(kMaxG + 1) * kD + d] = f2bf(va[0]);
+      fq[(kMaxG + 1) * kD + 64 + d] = f2bf(va[1]);
+    }
+    // LDS rows written and read by this wave only: in-order LDS, no barrier; keep the compiler from hoisting
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[s] = col_valid ? *reinterpret_cast<const bf16x8*>(&fq[(r % G) * kD + 32 * s + 8 * g]) : zero_bf16x8();
+    if (owner) {
+      kb_new = kn_page;
+      key_limit = col_limit - 1;  // decode: the newest key is the last visible one
+      bf16x8 kn[4];
+      float dot = 0.f;  // q · k over this lane's 32 head dims, then over the 4 lane groups
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kn[q] = *reinterpret_cast<const bf16x8*>(&fq[kMaxG * kD + 32 * q + 8 * g]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot += bf2f(qf[q][e]) * bf2f(kn[q][e]);
+      }
+      dot += __shfl_xor(dot, 16);
+      dot += __shfl_xor(dot, 32);
+      sc_new = col_valid ? dot * p.scale_log2 : -INFINITY;
+      // cache copies for later steps
+      const int sidx = DSSE_IDX(sl, p.num_slots, 0), blk = sidx / kPage, off = sidx % kPage;
+      if (r == (off & 15)) {
+        bf16* kdst = p.k_out + (((size_t)blk * p.hkv + h) * kPage + off) * kD + 8 * g;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(kdst + 32 * q) = kn[q];
+      }
+      bf16* vdst = p.v_out + ((size_t)blk * p.hkv + h) * kD * kPage + vperm_tok(off);
+      vdst[(size_t)d * kPage] = f2bf(va[0]);
+      vdst[(size_t)(64 + d) * kPage] = f2bf(va[1]);
+    }
+  } else {
     const int qrow = p.q_start[b] + (col_valid ? qi : 0);
     const bf16* qp = p.q + ((size_t)qrow * p.hq + h * G + (r % G)) * kD + 8 * g;
 #pragma unroll
@@ -68,6 +162,19 @@ paged_attention_kernel(AttnParams p) {
   f32x4 o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (FQ) {
+    // the newest key opens the online softmax: m = its score, p = 1 (exact in bf16 too), o = its V row
+    if (kb_new >= 0 && col_valid) {
+      m_run = sc_new;
+      l_run = g == 0 ? 1.f : 0.f;  // per-lane partial: counted once per column
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16x4 vq = *reinterpret_cast<const bf16x4*>(&s_fq[kw][(kMaxG + 1) * kD + 16 * dt + 4 * g]);  // d = 16dt + 4g + i
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[dt][i] = bf2f(vq[i]);
+      }
+    }
+  }
 
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
@@ -104,8 +211,8 @@ paged_attention_kernel(AttnParams p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ka = kb + 4 * g + i, kb2 = kb + 16 + 4 * g + i;
-      s0[i] = (ka < col_limit) ? s0[i] * p.scale_log2 : -INFINITY;
-      s1[i] = (kb2 < col_limit) ? s1[i] * p.scale_log2 : -INFINITY;
+      s0[i] = (ka < key_limit) ? s0[i] * p.scale_log2 : -INFINITY;
+      s1[i] = (kb2 < key_limit) ? s1[i] * p.scale_log2 : -INFINITY;
       tmax = fmaxf(tmax, fmaxf(s0[i], s1[i]));
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
@@ -258,12 +365,23 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
 
 }  // namespace dsse
 
-// mode 0 = decode (QW = 1, KWV = 4), mode 1 = prefill (QW = 4, KWV = 1).
+// mode 0 = decode (QW = 1, KWV = 4), mode 1 = prefill (QW = 4, KWV = 1), mode 3 = decode reading q from the
+// QKV GEMM's split-K slabs and writing the step's K / V (AttnParams::qkv_part).
 extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p,
                                            hipStream_t st) {
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
-  if (mode == 0) {
+  if (mode == 3) {
+    // decode with the QKV epilogue folded in (same key-split choice as mode 0)
+    const dim3 grid(num_work, p->hkv, p->nparts);
+    const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
+    if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false, true>), grid, dim3(512), 0, st, *p);
+    else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false, true>), grid, dim3(64), 0, st, *p);
+    else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false, true>), grid, dim3(128), 0, st, *p);
+    else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false, true>), grid, dim3(256), 0, st, *p);
+    if (p->nparts > 1)
+      hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
+  } else if (mode == 0) {
     // decode: p->kwv (DSSE_ATTN_KWV, read by the bindings) = waves per workgroup splitting the keys (1/2/4/8).
     // Measured (profiles/attention_decode_r1.md): 4 key-split waves are best up to ~1k workgroups (64 streams x
     // 8 kv heads: 29 us at 560 keys, 5.1 TB/s), one wave per (sequence, kv head) above (256 streams: 100 vs

@@ -495,11 +495,13 @@ void ring_advance(Tensor& counter) {
   DSSE_CHECK_HIP(dsse_ring_advance(counter.data_ptr<int>(), cur_stream()));
 }
 
-void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
-                     const Tensor& block_tables, const Tensor& q_start, const Tensor& q_len,
-                     const Tensor& ctx_len, const Tensor& work_seq, const Tensor& work_tile,
-                     Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part, int64_t nparts) {
-  for (const Tensor* t : {&q, &k_cache, &v_cache, (const Tensor*)&out}) {
+// Checks and parameter block shared by the paged-attention entry points (hq query heads, QW query tiles per
+// workgroup, KWV key-split waves in the partition-size check).
+dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                             const Tensor& q_start, const Tensor& q_len, const Tensor& ctx_len, const Tensor& work_seq,
+                             const Tensor& work_tile, Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part,
+                             int64_t nparts, int qw, int kwv) {
+  for (const Tensor* t : {&k_cache, &v_cache, (const Tensor*)&out}) {
     check_gpu(*t, "attention tensor");
     check_dtype(*t, at::kBFloat16, "attention tensor");
   }
@@ -507,17 +509,15 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
     check_gpu(*t, "attention metadata");
     check_dtype(*t, at::kInt, "attention metadata");
   }
-  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == dsse::kBS && k_cache.size(3) == 128,
               "k_cache must be [blocks, Hkv, 32, 128]");
-  const int hq = (int)q.size(1), hkv = (int)k_cache.size(1);
+  const int hkv = (int)k_cache.size(1);
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), hkv, 128, dsse::kBS}),
+              "v_cache must be [blocks, Hkv, 128, 32]");
   TORCH_CHECK(hq % hkv == 0 && 16 % (hq / hkv) == 0, "GQA group must divide 16");
-  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  TORCH_CHECK(out.dim() == 3 && out.size(1) == hq && out.size(2) == 128, "out must be [T, Hq, 128]");
   const int num_work = (int)work_seq.numel();
   TORCH_CHECK(work_tile.numel() == num_work, "work lists differ in length");
-  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 decode, 1 prefill (16-query tiles), 2 flash prefill (64-query tiles)");
-  if (mode == 2) TORCH_CHECK(hq / hkv == 1 || hq / hkv == 2 || hq / hkv == 4, "flash prefill supports G in {1, 2, 4}");
-  const int kwv = mode == 0 ? 4 : 1, qw = mode == 0 ? 1 : 4;
   TORCH_CHECK(part % (32 * kwv) == 0 && part > 0, "partition size must be a multiple of ", 32 * kwv);
   TORCH_CHECK(nparts >= 1, "nparts >= 1");
   if (nparts > 1) {
@@ -527,7 +527,6 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
     TORCH_CHECK(part_ml.numel() >= (int64_t)num_work * hkv * nparts * qw * 16 * 2, "part_ml too small");
   }
   dsse::AttnParams p{};
-  p.q = reinterpret_cast<const bf16*>(q.data_ptr());
   p.k_cache = reinterpret_cast<const bf16*>(k_cache.data_ptr());
   p.v_cache = reinterpret_cast<const bf16*>(v_cache.data_ptr());
   p.block_tables = block_tables.data_ptr<int>();
@@ -547,12 +546,102 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   p.part = (int)part;
   p.nparts = (int)nparts;
   p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
-  {
-    const int kwv = env_int("DSSE_ATTN_KWV", 0);
-    p.kwv = (kwv == 1 || kwv == 2 || kwv == 4 || kwv == 8) ? kwv : 0;
-  }
+  const int env_kwv = env_int("DSSE_ATTN_KWV", 0);
+  p.kwv = (env_kwv == 1 || env_kwv == 2 || env_kwv == 4 || env_kwv == 8) ? env_kwv : 0;
+  return p;
+}
+
+void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                     const Tensor& block_tables, const Tensor& q_start, const Tensor& q_len,
+                     const Tensor& ctx_len, const Tensor& work_seq, const Tensor& work_tile,
+                     Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part, int64_t nparts) {
+  check_gpu(q, "q");
+  check_dtype(q, at::kBFloat16, "q");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 decode, 1 prefill (16-query tiles), 2 flash prefill (64-query tiles)");
+  const int hq = (int)q.size(1), hkv = (int)k_cache.size(1);
+  if (mode == 2) TORCH_CHECK(hq % hkv == 0 && (hq / hkv == 1 || hq / hkv == 2 || hq / hkv == 4),
+                             "flash prefill supports G in {1, 2, 4}");
+  dsse::AttnParams p = attn_params(hq, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile,
+                                   out, part_o, part_ml, part, nparts, mode == 0 ? 1 : 4, mode == 0 ? 4 : 1);
+  p.q = reinterpret_cast<const bf16*>(q.data_ptr());
+  const int num_work = (int)work_seq.numel();
   if (mode == 2) DSSE_CHECK_HIP(dsse_flash_prefill(num_work, &p, cur_stream()));
   else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
+}
+
+// Decode QKV projection + attention with the projection's epilogue folded into the attention kernel: the GEMM
+// leaves fp32 split-K slabs in `slabs` and attention mode 3 sums them, applies RoPE, writes this step's K / V
+// into the cache and attends -- one launch (the split-K reduce) fewer per layer.  Falls back to gemm_qkv_rope
+// + decode attention when the chosen GEMM cannot leave slabs (the register-streaming kernel of tiny batches),
+// when `slabs` is too small, or with DSSE_FUSED_QKV_ATTN=0.  Returns the number of slabs (0 = fallback).
+int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
+                             const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
+                             int64_t nkv, Tensor& slabs, const Tensor& block_tables, const Tensor& q_start,
+                             const Tensor& q_len, const Tensor& ctx_len, const Tensor& work_seq,
+                             const Tensor& work_tile, Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part,
+                             int64_t nparts) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(slabs, "slabs");
+  check_dtype(slabs, at::kFloat, "slabs");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const bool shape_ok = x.dim() == 2 && w.dim() == 2 && M >= 1 && K % 128 == 0 && w.size(1) == K &&
+                        N == (nh + 2 * nkv) * 128;
+  const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
+  int S = 0;
+  if (impl == 4) S = pick_tiled(M, N, K).S;
+  else if (impl == 3) S = pick_wide(M, N, K).S;
+  else if (impl == 2) S = pick_stream(M, N, K, dsse::kQkvRope).S;
+  auto q3 = q_out.view({-1, nh, 128});
+  auto o3 = out.view({-1, nh, 128});
+  if (S <= 0 || slabs.numel() < (int64_t)S * M * N || env_int("DSSE_FUSED_QKV_ATTN", 1) == 0) {
+    gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv);
+    paged_attention(0, q3, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, o3, part_o,
+                    part_ml, part, nparts);
+    return 0;
+  }
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  for (auto* t : {&positions, &slots}) {
+    check_gpu(*t, "metadata");
+    check_dtype(*t, at::kInt, "metadata");
+  }
+  check_gpu(rope, "rope");
+  check_dtype(rope, at::kFloat, "rope");
+  TORCH_CHECK(rope.dim() == 3 && rope.size(1) == 64 && rope.size(2) == 2, "rope must be [P, 64, 2]");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "metadata too short");
+  TORCH_CHECK(k_cache.size(1) == nkv, "k_cache heads must be nkv");
+  TORCH_CHECK(o3.size(0) == M, "out must hold the M query rows");
+  dsse::AttnParams p = attn_params((int)nh, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
+                                   work_tile, o3, part_o, part_ml, part, nparts, 1, 4);
+  dsse::GemmEpi ep{};
+  const void* X = x.data_ptr();
+  float* sl = slabs.data_ptr<float>();
+  if (impl == 4) {
+    const TCfg c = pick_tiled(M, N, K);
+    DSSE_CHECK_HIP(dsse_gemm_tiled(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
+  } else if (impl == 3) {
+    const WCfg c = pick_wide(M, N, K);
+    DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
+  } else {
+    const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
+    DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kQkvRope, c.mt, c.nt, c.nw, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl,
+                                    cur_stream()));
+  }
+  p.qkv_part = sl;
+  p.qkv_S = S;
+  p.qkv_M = M;
+  p.positions = positions.data_ptr<int>();
+  p.slots = slots.data_ptr<int>();
+  p.rope = reinterpret_cast<const float2*>(rope.data_ptr<float>());
+  p.rope_len = (int)rope.size(0);
+  p.num_slots = (int)(k_cache.size(0) * dsse::kBS);
+  p.k_out = reinterpret_cast<bf16*>(k_cache.data_ptr());
+  p.v_out = reinterpret_cast<bf16*>(v_cache.data_ptr());
+  DSSE_CHECK_HIP(dsse_paged_attention(3, (int)work_seq.numel(), &p, cur_stream()));
+  return S;
 }
 
 dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
@@ -636,7 +725,7 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 7; }
+int64_t kernels_abi_version() { return 8; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -686,6 +775,10 @@ TORCH_LIBRARY(dsse, m) {
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
         "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
+  m.def("qkv_attention_decode(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor(d!) slabs, Tensor block_tables, "
+        "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(e!) out, "
+        "Tensor(f!) part_o, Tensor(g!) part_ml, int part, int nparts) -> int");
   m.def("sample_candidates(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
@@ -708,6 +801,7 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("decode_prep", &decode_prep);
   m.impl("ring_advance", &ring_advance);
   m.impl("paged_attention", &paged_attention);
+  m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
 }

@@ -301,7 +301,7 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
-  if (S == 1) {
+  if (S == 1 && !partial_only) {
     switch (mode) {
       case kStoreBf16: return launch_s_mode<kStoreBf16>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
       case kStoreF32: return launch_s_mode<kStoreF32>(mt, nt, nw, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);

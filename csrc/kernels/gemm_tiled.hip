@@ -229,7 +229,7 @@ extern "C" hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
-  if (S == 1) {
+  if (S == 1 && !partial_only) {
     switch (mode) {
       case kStoreBf16: return launch_t_mode<kStoreBf16>(cfg, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
       case kStoreF32: return launch_t_mode<kStoreF32>(cfg, x, ldx, M, w, K, N, 1, *ep, nullptr, st);

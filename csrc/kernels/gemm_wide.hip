@@ -194,7 +194,7 @@ extern "C" hipError_t dsse_gemm_wide(int mode, int mb, int rd, int S, int partia
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
-  if (S == 1) {
+  if (S == 1 && !partial_only) {
     switch (mode) {
       case kStoreBf16: return launch_w_mode<kStoreBf16>(mb, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
       case kStoreF32: return launch_w_mode<kStoreF32>(mb, rd, x, ldx, M, w, K, N, 1, *ep, nullptr, st);

@@ -5,8 +5,9 @@ Decode step for a batch bucket of B slots (all device-resident, no host round tr
     decode_prep          slots / ctx_len / q_len from positions + block tables
     embed+rmsnorm        resid = E[ids]; x = norm(resid)
     per layer:
-      gemm_qkv_rope      x·Wqkvᵀ, RoPE, K/V written into the paged cache, q for attention
-      paged_attention    flash-decoding over the pages (+ partition combine)
+      qkv GEMM           x·Wqkvᵀ as fp32 split-K slabs
+      paged_attention    sums the slabs, RoPE, writes this token's K/V into the paged cache, then
+                         flash-decoding over the pages (+ partition combine)
       gemm_resid         resid += attn·Woᵀ          (TP>1: gemm_out + RCCL all-reduce + add)
       rmsnorm            x = norm(resid)
       gemm_silu          h = silu(x·Wgᵀ)·(x·Wuᵀ)
@@ -145,18 +146,12 @@ class ModelRunner:
         resid, x = self.resid[r], self.x[r]
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=self.ids[r])
         part, nparts = decode_partitioning(B, nkv, self.max_model_len)
-        q3 = self.q[r].view(B, nh, 128)
-        a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
         if B > DECODE_GEMM_MAX_M:
             self._decode_layers_wide(B, resid, x, part, nparts)
             return
         for li, L in enumerate(w.layers):
-            ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
-                              self.kv.v[li], nh, nkv)
-            ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
-                                self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
-                                self.part_ml, part, nparts)
+            self._qkv_attention(li, L, B, x, part, nparts)
             if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
                 ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
                 ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
@@ -190,15 +185,9 @@ class ModelRunner:
         nh, nkv = w.nh, w.nkv
         r = slice(0, B)
         eps = cfg.rms_eps
-        q3 = self.q[r].view(B, nh, 128)
-        a3 = self.attn[r].view(B, nh, 128)
         nl = len(w.layers)
         for li, L in enumerate(w.layers):
-            ops.gemm_qkv_rope(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
-                              self.kv.v[li], nh, nkv)
-            ops.paged_attention(0, q3, self.kv.k[li], self.kv.v[li], self.block_tables[r], self.q_start[r],
-                                self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], a3, self.part_o,
-                                self.part_ml, part, nparts)
+            self._qkv_attention(li, L, B, x, part, nparts)
             self._resid_proj(self.attn[r], L.wo_t, resid, L.ffn_norm, x, self.tmp[r])
             ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
@@ -209,6 +198,17 @@ class ModelRunner:
             ops.gemm_out(x[b0:b1], w.lm_head_t, self.logits[b0:b1])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
+
+    def _qkv_attention(self, li: int, L, B: int, x, part: int, nparts: int) -> None:
+        """QKV projection + RoPE + KV write + decode attention of layer li.  The projection's split-K slabs go
+        to split_part (free here: the previous norm consumed it) and the attention kernel folds their reduction,
+        RoPE and the K/V write in (ops.qkv_attention_decode)."""
+        r = slice(0, B)
+        nh, nkv = self.w.nh, self.w.nkv
+        ops.qkv_attention_decode(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
+                                 self.kv.v[li], nh, nkv, self.split_part, self.block_tables[r], self.q_start[r],
+                                 self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], self.attn[r],
+                                 self.part_o, self.part_ml, part, nparts)
 
     def _resid_proj(self, a, wt, resid, norm_w, x, tmp) -> None:
         """resid += a·wᵀ (TP: all-reduced), then x = RMSNorm(resid)·norm_w.  TP = 1: split-K slabs (if the GEMM

@@ -156,6 +156,22 @@ def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx
                             out, part_o, part_ml, part, nparts)
 
 
+def qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, slabs, block_tables, q_start,
+                         q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts) -> int:
+    """Decode QKV projection + RoPE + KV write + attention.  HIP: the GEMM leaves fp32 split-K slabs in `slabs`
+    and the attention kernel folds the reduction, RoPE and the K/V write in (returns the slab count; 0 = it ran
+    gemm_qkv_rope + paged_attention instead).  Same result as those two ops."""
+    if _hip(x):
+        return int(torch.ops.dsse.qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv,
+                                                       slabs, block_tables, q_start, q_len, ctx_len, work_seq,
+                                                       work_tile, out, part_o, part_ml, part, nparts))
+    B = x.shape[0]
+    ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
+    ref.paged_attention(0, q_out.view(B, nh, 128), k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
+                        work_tile, out.view(B, nh, 128), part_o, part_ml, part, nparts)
+    return 0
+
+
 def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):
     """Per-rank pass: cand [B, C, 2] <- best (score, index) of each vocab chunk (Gumbel-max / argmax)."""
     if _hip(logits):

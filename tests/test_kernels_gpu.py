@@ -261,6 +261,55 @@ def test_paged_attention_decode(gpu, ctxs, part):
     _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention")
 
 
+@pytest.mark.parametrize("cfg", ["auto", "stream-nw4-split4", "wide-split2-rd", "tiled-default", "tiled-128-split2",
+                                 "skinny-default"])
+@pytest.mark.parametrize("M,part", [(1, 128), (9, 512), (64, 128), (64, 8192), (200, 256), (256, 8192)])
+def test_qkv_attention_decode_folded_epilogue(gpu, monkeypatch, cfg, M, part):
+    """Attention mode 3 (QKV split-K reduce + RoPE + K/V write folded into the decode attention kernel) against
+    the two-op path (gemm_qkv_rope + decode attention): same K/V cache bytes, same attention output."""
+    for k, v in GEMM_CONFIGS[cfg].items():
+        monkeypatch.setenv(k, v)
+    nh, nkv, H = 32, 8, 1024
+    g = torch.Generator().manual_seed(M * 31 + part)
+    ctxs = torch.randint(1, 700, (M,), generator=g).tolist()
+    kc, vc, bt, _, _ = _attn_setup(ctxs, [1] * M, hq=nh, hkv=nkv, gen=g)
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    qlen = torch.ones(M, dtype=torch.int32)
+    pos = ctx - 1
+    slots = torch.tensor([int(bt[b, (c - 1) // 32]) * 32 + (c - 1) % 32 for b, c in enumerate(ctxs)], dtype=torch.int32)
+    if M > 1:  # an inactive slot: no query, no key, no K/V write
+        qlen[-1], ctx[-1], slots[-1] = 0, 0, -1
+    x = _rand(M, H, dev=gpu, gen=g)
+    w = R.tile_weight(_rand((nh + 2 * nkv) * 128, H, dev=gpu, scale=1 / 32, gen=g))
+    rope = R.rope_table(1024, 1e6, gpu)
+    nparts = math.ceil(int(ctx.max()) / part)
+    dev = {k: t.to(gpu) for k, t in dict(bt=bt, ctx=ctx, qlen=qlen, pos=pos, slots=slots,
+                                         qs=torch.arange(M, dtype=torch.int32), ws=torch.arange(M, dtype=torch.int32),
+                                         wt=torch.zeros(M, dtype=torch.int32)).items()}
+    res = {}
+    for fused in (1, 0):
+        monkeypatch.setenv("DSSE_FUSED_QKV_ATTN", str(fused))
+        ops.refresh_env()
+        k_, v_ = kc.clone().to(gpu), vc.clone().to(gpu)
+        q = torch.zeros(M, nh * 128, device=gpu, dtype=torch.bfloat16)
+        out = torch.zeros(M, nh * 128, device=gpu, dtype=torch.bfloat16)
+        slabs = torch.full((16 * M * (nh + 2 * nkv) * 128,), float("nan"), device=gpu)
+        po = torch.zeros(M * nkv * nparts * 16 * 128, device=gpu)
+        pml = torch.zeros(M * nkv * nparts * 16 * 2, device=gpu)
+        S = ops.qkv_attention_decode(x, w, dev["pos"], dev["slots"], rope, q, k_, v_, nh, nkv, slabs, dev["bt"],
+                                     dev["qs"], dev["qlen"], dev["ctx"], dev["ws"], dev["wt"], out, po, pml, part,
+                                     nparts)
+        res[fused] = (S, out.cpu(), k_.cpu(), v_.cpu())
+    assert res[0][0] == 0
+    if cfg != "skinny-default" and M > 16:
+        assert res[1][0] >= 1, "the folded path did not run"
+    live = qlen.bool()
+    # the newest key's score is an fp32 dot instead of an MFMA column: bf16 outputs may round one ulp apart
+    _close(res[1][1][live], res[0][1][live], 1.6e-2, 1e-2, "attention out")
+    _close(res[1][2], res[0][2], 1e-2, 1e-2, "k cache")  # RoPE: fma contraction may differ by an ulp
+    _close(res[1][3], res[0][3], 0, 0, "v cache")
+
+
 @pytest.mark.parametrize("mode,hq", [(1, 32), (2, 32), (2, 16), (2, 8)])
 @pytest.mark.parametrize("case", [([45], [45]), ([300, 17], [300, 17]), ([700, 64], [100, 64]), ([4096], [1000]),
                                   ([129, 1], [65, 1])])
@@ -380,7 +429,7 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 7
+    assert torch.ops.dsse.kernels_abi_version() == 8
     assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
 
 
