@@ -30,10 +30,11 @@ constexpr int kD = 128;
 
 // One-wave decode workgroups (256+ streams) are held to 4 waves per SIMD: the folded QKV epilogue (FQ) otherwise
 // raises the register peak from 127 to 159 and costs a wave per SIMD; 104 VGPRs, no spills.
-template <int QW, int KWV, bool PF = false, bool FQ = false>
+template <int QW, int KWV, bool PF = false, int FQG = 0>
 __global__ void __launch_bounds__(64 * QW * KWV, QW * KWV == 1 ? 4 : 1)
 paged_attention_kernel(AttnParams p) {
-  static_assert(!(PF && FQ), "the folded QKV epilogue patches the non-prefetching page loop");
+  constexpr bool FQ = FQG > 0;  // QKV epilogue folded in, GQA group FQG (= p.group)
+  static_assert(!(PF && FQ), "the folded QKV epilogue has its own page loop");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int qw = w / KWV, kw = w % KWV;
@@ -58,6 +59,38 @@ paged_attention_kernel(AttnParams p) {
   const int kend = min(kmax, kbeg + p.part);
   if (kbeg >= kend) return;  // uniform for the whole workgroup
 
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
+  // while the current one is computed (measured slower for decode: VGPRs 100 -> 140 cost occupancy).
+  // KV page of key kb: a wave-uniform index, read through the constant address space (the block table is
+  // read-only for the kernel) so it is an s_load_dword -- a per-lane block-table load made every page wait
+  // vmcnt(0) behind it, draining the K/V loads in flight.
+  auto page_of = [&](int kb) {
+    const int i = __builtin_amdgcn_readfirstlane(DSSE_IDX(kb / kPage, p.max_blocks, 0));
+    const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
+    return DSSE_IDX(cbt[i], p.num_blocks, 0);
+  };
+  auto load_k = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4]) {
+    const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
+    // K rows for keys kb + r and kb + 16 + r; k-step s of the 4 lane groups = 64 contiguous bytes of a row.
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * s + 8 * g);
+      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * s + 8 * g);
+    }
+  };
+  auto load_v = [&](int page, bf16x8 (&vf)[8]) {
+    const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_bf16x8(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
+  };
+  auto load_page = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
+    load_k(page, k0, k1);
+    load_v(page, vf);
+  };
+  constexpr int kStep = 32 * KWV;
+  const int kb0 = kbeg + 32 * kw;  // this wave's first page: keys kb0 + i * kStep
+  bf16x8 pk0[4], pk1[4];           // FQ: the first page's K rows, loaded under the slab sums
   // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32s + 8g + j] in k-step s — the same head-dim
   // order as the K fragments, so each K load instruction reads 64 contiguous bytes of 16 key rows.
   bf16x8 qf[4];
@@ -65,7 +98,7 @@ paged_attention_kernel(AttnParams p) {
   // page.  That wave starts its online softmax with this key and masks it out of the page loop (its cache slot
   // is written in this launch, by the same wave, for later steps).  Patching the page's fragments in registers
   // instead cost 50-80 VGPRs (a wave per SIMD).
-  constexpr int kMaxG = 8;  // GQA group bound of the folded path (the bindings fall back above it)
+  constexpr int kMaxG = FQ ? FQG : 1;  // the folded path is instantiated per GQA group (1, 2, 4)
   __shared__ __attribute__((aligned(16))) bf16 s_fq[FQ ? KWV : 1][FQ ? (kMaxG + 2) * kD : 1];  // q heads | k | v
   float sc_new = -INFINITY;  // newest key's score (log2 units) for column r
   int kb_new = -1;            // first key of the newest key's page, or -1 when this wave does not hold it
@@ -86,34 +119,53 @@ paged_attention_kernel(AttnParams p) {
     const bool owner = pz == (ctx - 1) / p.part && sl >= 0 && ((kn_page - kbeg) / kPage) % KWV == kw;
     const int t = lane >> 3, j = lane & 7;
     const float* base = p.qkv_part + (size_t)m * N + 16 * t + j;
-    float qa[kMaxG][2], ka[2] = {0.f, 0.f}, va[2] = {0.f, 0.f};
+    // Slabs 0 and 1 (slab 0 again when S == 1, masked below) are loaded unconditionally -- a guarded load is a
+    // branch, and hipcc drains vmcnt at every branch -- then the K rows of the wave's first page are issued, so
+    // their HBM latency overlaps the slab sums (K only: the V rows as well cost a wave per SIMD in registers).
+    // Units: the group's kMaxG q heads, k, v.
+    auto unit_col = [&](int u) {
+      return u < kMaxG ? (h * kMaxG + u) * kD : (u == kMaxG ? p.hq + h : p.hq + p.hkv + h) * kD;
+    };
+    float xa[kMaxG + 2][2], xb[kMaxG + 2][2];
+    {
+      const float* s0 = base;
+      const float* s1 = base + (p.qkv_S > 1 ? slab : 0);
 #pragma unroll
-    for (int u = 0; u < kMaxG; ++u) qa[u][0] = qa[u][1] = 0.f;
-    // unconditional loads (heads past the group re-read its last head): a guarded load is a branch, and hipcc
-    // drains vmcnt at every branch -- one slab latency per head
-#pragma unroll 2
-    for (int k = 0; k < p.qkv_S; ++k) {
+      for (int u = 0; u < kMaxG + 2; ++u) {
+        const int c0 = unit_col(u);
+        xa[u][0] = s0[c0];
+        xa[u][1] = s0[c0 + 8];
+        xb[u][0] = s1[c0];
+        xb[u][1] = s1[c0 + 8];
+      }
+    }
+    load_k(page_of(min(kb0, kend - 1)), pk0, pk1);
+    const bool two = p.qkv_S > 1;
+#pragma unroll
+    for (int u = 0; u < kMaxG + 2; ++u) {
+      xa[u][0] += two ? xb[u][0] : 0.f;  // x + 0 = x: the same sums as the reduce kernel's 0 + x0 + x1 + ...
+      xa[u][1] += two ? xb[u][1] : 0.f;
+    }
+    for (int k = 2; k < p.qkv_S; ++k) {
       const float* sk = base + k * slab;
 #pragma unroll
-      for (int u = 0; u < kMaxG; ++u) {
-        const int uu = min(u, G - 1);
-        qa[u][0] += sk[(h * G + uu) * kD];
-        qa[u][1] += sk[(h * G + uu) * kD + 8];
+      for (int u = 0; u < kMaxG + 2; ++u) {
+        const int c0 = unit_col(u);
+        xa[u][0] += sk[c0];
+        xa[u][1] += sk[c0 + 8];
       }
-      ka[0] += sk[(p.hq + h) * kD];
-      ka[1] += sk[(p.hq + h) * kD + 8];
-      va[0] += sk[(p.hq + p.hkv + h) * kD];
-      va[1] += sk[(p.hq + p.hkv + h) * kD + 8];
     }
+    float (&qa)[kMaxG + 2][2] = xa;
+    const float* ka = xa[kMaxG];
+    const float* va = xa[kMaxG + 1];
     const float2 c = p.rope[(size_t)DSSE_IDX(p.positions[m], p.rope_len, 0) * 64 + 8 * t + j];
     bf16* fq = s_fq[kw];
     const int d = 8 * t + j;  // this lane's head dims: d and d + 64
 #pragma unroll
-    for (int u = 0; u < kMaxG; ++u)
-      if (u < G) {
-        fq[u * kD + d] = f2bf(qa[u][0] * c.x - qa[u][1] * c.y);
-        fq[u * kD + 64 + d] = f2bf(qa[u][1] * c.x + qa[u][0] * c.y);
-      }
+    for (int u = 0; u < kMaxG; ++u) {
+      fq[u * kD + d] = f2bf(qa[u][0] * c.x - qa[u][1] * c.y);
+      fq[u * kD + 64 + d] = f2bf(qa[u][1] * c.x + qa[u][0] * c.y);
+    }
     if (owner) {
       fq[kMaxG * kD + d] = f2bf(ka[0] * c.x - ka[1] * c.y);
       fq[kMaxG * kD + 64 + d] = f2bf(ka[1] * c.x + ka[0] * c.y);
@@ -176,29 +228,6 @@ paged_attention_kernel(AttnParams p) {
     }
   }
 
-  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
-  // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
-  // while the current one is computed (measured slower for decode: VGPRs 100 -> 140 cost occupancy).
-  // KV page of key kb: a wave-uniform index, read through the constant address space (the block table is
-  // read-only for the kernel) so it is an s_load_dword -- a per-lane block-table load made every page wait
-  // vmcnt(0) behind it, draining the K/V loads in flight.
-  auto page_of = [&](int kb) {
-    const int i = __builtin_amdgcn_readfirstlane(DSSE_IDX(kb / kPage, p.max_blocks, 0));
-    const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
-    return DSSE_IDX(cbt[i], p.num_blocks, 0);
-  };
-  auto load_page = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
-    const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
-    const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
-    // K rows for keys kb + r and kb + 16 + r; k-step s of the 4 lane groups = 64 contiguous bytes of a row.
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * s + 8 * g);
-      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * s + 8 * g);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_bf16x8(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
-  };
   auto compute_page = [&](int kb, const bf16x8 (&k0)[4], const bf16x8 (&k1)[4], const bf16x8 (&vf)[8]) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -236,11 +265,19 @@ paged_attention_kernel(AttnParams p) {
       o[dt] = mfma16x16x32(vf[dt], pf, acc);
     }
   };
-  constexpr int kStep = 32 * KWV;
-  int kb = kbeg + 32 * kw;
+  int kb = kb0;
   if constexpr (!PF) {
     // the next page's index is fetched one page ahead (scalar load under this page's compute)
     int page = kb < kend ? page_of(kb) : 0;
+    if constexpr (FQ) {
+      if (kb < kend) {  // the first page's K has been in flight since the slab sums
+        bf16x8 vf[8];
+        load_v(page, vf);
+        page = page_of(min(kb + kStep, kend - 1));
+        compute_page(kb, pk0, pk1, vf);
+        kb += kStep;
+      }
+    }
     for (; kb < kend; kb += kStep) {
       bf16x8 k0[4], k1[4], vf[8];
       load_page(page, k0, k1, vf);
@@ -363,6 +400,15 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
   *reinterpret_cast<bf16x8*>(op) = ov;
 }
 
+template <int G>
+hipError_t launch_folded(int kwv, dim3 grid, const AttnParams& p, hipStream_t st) {
+  if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false, G>), grid, dim3(512), 0, st, p);
+  else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false, G>), grid, dim3(64), 0, st, p);
+  else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false, G>), grid, dim3(128), 0, st, p);
+  else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false, G>), grid, dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
 }  // namespace dsse
 
 // mode 0 = decode (QW = 1, KWV = 4), mode 1 = prefill (QW = 4, KWV = 1), mode 3 = decode reading q from the
@@ -372,13 +418,15 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
   if (mode == 3) {
-    // decode with the QKV epilogue folded in (same key-split choice as mode 0)
+    // decode with the QKV epilogue folded in (same key-split choice as mode 0); GQA group 1, 2 or 4
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
-    if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false, true>), grid, dim3(512), 0, st, *p);
-    else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false, true>), grid, dim3(64), 0, st, *p);
-    else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false, true>), grid, dim3(128), 0, st, *p);
-    else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false, true>), grid, dim3(256), 0, st, *p);
+    hipError_t e;
+    if (p->group == 1) e = launch_folded<1>(kwv, grid, *p, st);
+    else if (p->group == 2) e = launch_folded<2>(kwv, grid, *p, st);
+    else if (p->group == 4) e = launch_folded<4>(kwv, grid, *p, st);
+    else return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
     if (p->nparts > 1)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else if (mode == 0) {

@@ -575,7 +575,7 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
 // leaves fp32 split-K slabs in `slabs` and attention mode 3 sums them, applies RoPE, writes this step's K / V
 // into the cache and attends -- one launch (the split-K reduce) fewer per layer.  Falls back to gemm_qkv_rope
 // + decode attention when the chosen GEMM cannot leave slabs (the register-streaming kernel of tiny batches),
-// for GQA groups above 8 heads, when `slabs` is too small, or with DSSE_FUSED_QKV_ATTN=0.  Returns the number of slabs (0 = fallback).
+// for GQA groups other than 1, 2, 4 heads, when `slabs` is too small, or with DSSE_FUSED_QKV_ATTN=0.  Returns the number of slabs (0 = fallback).
 int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
                              const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
                              int64_t nkv, Tensor& slabs, const Tensor& block_tables, const Tensor& q_start,
@@ -593,10 +593,16 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   int S = 0;
   if (impl == 4) S = pick_tiled(M, N, K).S;
   else if (impl == 3) S = pick_wide(M, N, K).S;
-  else if (impl == 2) S = pick_stream(M, N, K, dsse::kQkvRope).S;
+  else if (impl == 2) {
+    S = pick_stream(M, N, K, dsse::kQkvRope).S;
+    // DSSE_QKV_SPLIT: split-K of the QKV projection alone (its slabs are read by the attention kernel)
+    const int qs = env_int("DSSE_QKV_SPLIT", 0);
+    const int slices = K / (128 * ((M <= 64 || M > 256) ? 4 : (M <= 128 ? 2 : 1)));  // gemm_stream.hip stream_cps
+    if (qs > 0 && slices % qs == 0) S = qs;
+  }
   auto q3 = q_out.view({-1, nh, 128});
   auto o3 = out.view({-1, nh, 128});
-  const bool group_ok = nkv > 0 && nh % nkv == 0 && nh / nkv <= 8;  // attention.hip kMaxG
+  const bool group_ok = nkv > 0 && nh % nkv == 0 && (nh / nkv == 1 || nh / nkv == 2 || nh / nkv == 4);  // attention.hip
   if (S <= 0 || !group_ok || slabs.numel() < (int64_t)S * M * N || env_int("DSSE_FUSED_QKV_ATTN", 1) == 0) {
     gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv);
     paged_attention(0, q3, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, o3, part_o,
