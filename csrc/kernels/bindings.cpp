@@ -182,7 +182,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 3) {
+  if (cfg < 0 || cfg > 4) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile (8 waves of 128x64, 2 LDS stages) is
     // the fastest once it yields >= ~160 workgroups (1.20-1.24 PFLOP/s at 8192 rows); below that, the
     // 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
@@ -195,8 +195,8 @@ TCfg pick_tiled(int M, int N, int K) {
     if (narrow >= 0 && narrow <= 3 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
   }
   const int min_wgs = env_int("DSSE_T_MIN_WGS", 160);  // split K until this many workgroups (M <= 512)
-  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 256 for cfg 3
-  const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : (cfg == 3 ? 256 : 128);
+  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 256 for cfg 3 / 4
+  const int BM = cfg == 1 ? 128 : 256, BN = cfg == 2 ? 64 : (cfg >= 3 ? 256 : 128);
   c.cfg = cfg;
   c.S = 1;
   c.ok = N % BN == 0 && K % 64 == 0;
