@@ -183,11 +183,12 @@ TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
   if (cfg < 0 || cfg > 4) {
-    // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile (8 waves of 128x64, 2 LDS stages) is
-    // the fastest once it yields >= ~160 workgroups (1.20-1.24 PFLOP/s at 8192 rows); below that, the
-    // 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
+    // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
+    // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
+    // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
+    // fills more CUs; 128x128 for tiny M
     const int big_tiles = ((M + 255) / 256) * (N / 256);
-    cfg = (N % 256 == 0 && big_tiles >= 160) ? 3 : (M > 128 ? 0 : 1);
+    cfg = (N % 256 == 0 && big_tiles >= 160) ? 4 : (M > 128 ? 0 : 1);
     // narrow projections of the wide decode buckets (N <= 8192, 128 < M <= 512: qkv / o / down at 192-256
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
