@@ -110,7 +110,7 @@ paged_attention_kernel(AttnParams p) {
     // its partner d + 64.  Lane l sums the pair (t, j) = (l / 8, l % 8) of every unit it needs -- all slab
     // loads of the wave are independent, so the slab latency is paid once -- and the rotated values are
     // regrouped into MFMA fragments through the wave's LDS rows.
-    const int m = p.q_start[b];
+    const int m = DSSE_IDX(p.q_start[b], p.qkv_M, 0);  // this sequence's QKV row
     const int N = (p.hq + 2 * p.hkv) * kD;
     const size_t slab = (size_t)p.qkv_M * N;
     const int kn_page = (ctx - 1) & ~(kPage - 1);
