@@ -418,9 +418,12 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
   if (mode == 3) {
-    // decode with the QKV epilogue folded in (same key-split choice as mode 0); GQA group 1, 2 or 4
+    // decode with the QKV epilogue folded in; GQA group 1, 2 or 4.  Every key-split wave sums its q slabs, so
+    // fewer waves per workgroup than mode 0 pay off: 2 from 512 workgroups (64 streams: 4.58 vs 4.60 ms/step,
+    // 8 waves 4.67-4.71; profiles/experiments_r2.md), 1 from 2048 (256 streams: 9.95 vs 10.20 with 2)
     const dim3 grid(num_work, p->hkv, p->nparts);
-    const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
+    const int nwg = grid.x * grid.y * grid.z;
+    const int kwv = p->kwv ? p->kwv : (nwg >= 2048 ? 1 : (nwg >= 512 ? 2 : 4));
     hipError_t e;
     if (p->group == 1) e = launch_folded<1>(kwv, grid, *p, st);
     else if (p->group == 2) e = launch_folded<2>(kwv, grid, *p, st);
