@@ -52,6 +52,7 @@ struct AttnParams {
   int nparts;               // grid.z
   float scale_log2;         // log2(e) / sqrt(128)
   int kwv;                  // decode: waves per workgroup splitting the keys (0 = by grid size)
+  int pd;                   // mode 3: KV pages in flight per wave (0 = by occupancy, 1 = no look-ahead)
   // mode 3 (decode with the QKV epilogue folded in): q comes from the QKV GEMM's fp32 split-K slabs instead
   // of `q`; the workgroup holding a sequence's newest key also writes that token's K / V into the cache.
   const float* qkv_part;    // [qkv_S, qkv_M, (hq + 2 hkv) * 128], columns in the engine's rotary-pair order
@@ -91,6 +92,8 @@ hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int
                             const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
 hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X, int ldx, int M,
                             const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
+hipError_t dsse_gemm_ring(int mode, int nw, int d, int S, int partial_only, const void* X, int ldx, int M,
+                          const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_wide(int mode, int mb, int rd, int S, int partial_only, const void* X, int ldx, int M, const void* W,
                           int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W,

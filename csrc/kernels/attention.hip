@@ -30,11 +30,14 @@ constexpr int kD = 128;
 
 // One-wave decode workgroups (256+ streams) are held to 4 waves per SIMD: the folded QKV epilogue (FQ) otherwise
 // raises the register peak from 127 to 159 and costs a wave per SIMD; 104 VGPRs, no spills.
-template <int QW, int KWV, bool PF = false, int FQG = 0>
-__global__ void __launch_bounds__(64 * QW * KWV, QW * KWV == 1 ? 4 : 1)
+// PD: KV pages in flight per wave (a register ring of PD pages, each wave's next PD-1 pages issued before the
+// current one is computed).  One-wave workgroups with PD > 1 are held to 2 waves per SIMD (256 VGPRs): the
+// 2048-workgroup grid they serve (256 streams x 8 kv heads) puts 2 waves on each SIMD anyway.
+template <int QW, int KWV, int PD = 1, int FQG = 0>
+__global__ void __launch_bounds__(64 * QW * KWV, QW * KWV == 1 ? (PD > 1 ? 2 : 4) : 1)
 paged_attention_kernel(AttnParams p) {
   constexpr bool FQ = FQG > 0;  // QKV epilogue folded in, GQA group FQG (= p.group)
-  static_assert(!(PF && FQ), "the folded QKV epilogue has its own page loop");
+  static_assert(PD == 1 || PD == 2, "1 or 2 pages in flight");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int qw = w / KWV, kw = w % KWV;
@@ -60,8 +63,7 @@ paged_attention_kernel(AttnParams p) {
   if (kbeg >= kend) return;  // uniform for the whole workgroup
 
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
-  // One page (32 keys) per wave step.  PF: the next page's K/V are loaded into a second register set
-  // while the current one is computed (measured slower for decode: VGPRs 100 -> 140 cost occupancy).
+  // One page (32 keys) per wave step.
   // KV page of key kb: a wave-uniform index, read through the constant address space (the block table is
   // read-only for the kernel) so it is an s_load_dword -- a per-lane block-table load made every page wait
   // vmcnt(0) behind it, draining the K/V loads in flight.
@@ -90,7 +92,7 @@ paged_attention_kernel(AttnParams p) {
   };
   constexpr int kStep = 32 * KWV;
   const int kb0 = kbeg + 32 * kw;  // this wave's first page: keys kb0 + i * kStep
-  bf16x8 pk0[4], pk1[4];           // FQ: the first page's K rows, loaded under the slab sums
+  bf16x8 rk0[PD][4], rk1[PD][4];   // K rows of the pages in flight (FQ: slot 0 loaded under the slab sums)
   // Q fragments (B operand): lane (r, g) holds Q[col r][d = 32s + 8g + j] in k-step s — the same head-dim
   // order as the K fragments, so each K load instruction reads 64 contiguous bytes of 16 key rows.
   bf16x8 qf[4];
@@ -139,7 +141,7 @@ paged_attention_kernel(AttnParams p) {
         xb[u][1] = s1[c0 + 8];
       }
     }
-    load_k(page_of(min(kb0, kend - 1)), pk0, pk1);
+    load_k(page_of(min(kb0, kend - 1)), rk0[0], rk1[0]);
     const bool two = p.qkv_S > 1;
 #pragma unroll
     for (int u = 0; u < kMaxG + 2; ++u) {
@@ -266,7 +268,7 @@ paged_attention_kernel(AttnParams p) {
     }
   };
   int kb = kb0;
-  if constexpr (!PF) {
+  if constexpr (PD == 1) {
     // the next page's index is fetched one page ahead (scalar load under this page's compute)
     int page = kb < kend ? page_of(kb) : 0;
     if constexpr (FQ) {
@@ -274,7 +276,7 @@ paged_attention_kernel(AttnParams p) {
         bf16x8 vf[8];
         load_v(page, vf);
         page = page_of(min(kb + kStep, kend - 1));
-        compute_page(kb, pk0, pk1, vf);
+        compute_page(kb, rk0[0], rk1[0], vf);
         kb += kStep;
       }
     }
@@ -285,20 +287,26 @@ paged_attention_kernel(AttnParams p) {
       compute_page(kb, k0, k1, vf);
     }
   } else if (kb < kend) {
-    // The next-page loads are unconditional (the last page is re-read once at the end): a branch around
-    // them made hipcc wait vmcnt(0) at the join, which serialised the prefetch away.
-    bf16x8 ka0[4], ka1[4], va[8], kc0[4], kc1[4], vc[8];
+    // Register ring of PD pages: page i + PD - 1 is issued before page i is computed.  Look-ahead loads past the
+    // wave's last page re-read that page (an L2 hit) instead of branching around them -- hipcc waits vmcnt(0)
+    // at such a join, which would serialise the ring.  Page indices are fetched one issue ahead.
+    bf16x8 rv[PD][8];
     const int n = (kend - kb + kStep - 1) / kStep;  // pages of this wave
-    const int kb_last = kb + (n - 1) * kStep;
-    load_page(page_of(kb), ka0, ka1, va);
-    for (int i = 0; i < n; i += 2) {
-      load_page(page_of(min(kb + kStep, kb_last)), kc0, kc1, vc);
-      compute_page(kb, ka0, ka1, va);
-      kb += kStep;
-      if (i + 1 >= n) break;
-      load_page(page_of(min(kb + kStep, kb_last)), ka0, ka1, va);
-      compute_page(kb, kc0, kc1, vc);
-      kb += kStep;
+    auto pg = [&](int i) { return page_of(kb0 + min(i, n - 1) * kStep); };
+    if constexpr (FQ) load_v(pg(0), rv[0]);
+    else load_page(pg(0), rk0[0], rk1[0], rv[0]);
+#pragma unroll
+    for (int d = 1; d < PD - 1; ++d) load_page(pg(d), rk0[d], rk1[d], rv[d]);
+    int pnext = pg(PD - 1);
+    for (int i = 0; i < n; i += PD) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        const int ls = (u + PD - 1) % PD;
+        load_page(pnext, rk0[ls], rk1[ls], rv[ls]);
+        pnext = pg(i + u + PD);
+        compute_page(kb0 + (i + u) * kStep, rk0[u], rk1[u], rv[u]);
+        if (i + u + 1 >= n) break;
+      }
     }
   }
   // l_run is a per-lane partial over this lane's keys: sum the 4 lane groups of the column.
@@ -401,11 +409,13 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
 }
 
 template <int G>
-hipError_t launch_folded(int kwv, dim3 grid, const AttnParams& p, hipStream_t st) {
-  if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false, G>), grid, dim3(512), 0, st, p);
-  else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false, G>), grid, dim3(64), 0, st, p);
-  else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false, G>), grid, dim3(128), 0, st, p);
-  else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false, G>), grid, dim3(256), 0, st, p);
+hipError_t launch_folded(int kwv, int pd, dim3 grid, const AttnParams& p, hipStream_t st) {
+  if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, 1, G>), grid, dim3(512), 0, st, p);
+  else if (kwv == 1 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 2, G>), grid, dim3(64), 0, st, p);
+  else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 1, G>), grid, dim3(64), 0, st, p);
+  else if (kwv == 2 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 2, G>), grid, dim3(128), 0, st, p);
+  else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 1, G>), grid, dim3(128), 0, st, p);
+  else hipLaunchKernelGGL((paged_attention_kernel<1, 4, 1, G>), grid, dim3(256), 0, st, p);
   return hipGetLastError();
 }
 
@@ -420,14 +430,18 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
   if (mode == 3) {
     // decode with the QKV epilogue folded in; GQA group 1, 2 or 4.  Every key-split wave sums its q slabs, so
     // fewer waves per workgroup than mode 0 pay off: 2 from 512 workgroups (64 streams: 4.58 vs 4.60 ms/step,
-    // 8 waves 4.67-4.71; profiles/experiments_r2.md), 1 from 2048 (256 streams: 9.95 vs 10.20 with 2)
+    // 8 waves 4.67-4.71; profiles/experiments_r2.md); from 2048 one wave without look-ahead beat two (9.95 vs
+    // 10.20), two with a 2-page ring beat both (below)
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int nwg = grid.x * grid.y * grid.z;
-    const int kwv = p->kwv ? p->kwv : (nwg >= 2048 ? 1 : (nwg >= 512 ? 2 : 4));
+    // 2048+ workgroups (256 streams): 2 key-split waves, each with 2 KV pages in flight (9.82 / 9.87 ms/step vs
+    // 9.91 / 9.91 for one wave without look-ahead; 64 streams: look-ahead measured slower, 4.65-4.69 vs 4.63)
+    const int kwv = p->kwv ? p->kwv : (nwg >= 2048 ? 2 : (nwg >= 512 ? 2 : 4));
+    const int pd = p->pd ? p->pd : (nwg >= 2048 && kwv == 2 ? 2 : 1);
     hipError_t e;
-    if (p->group == 1) e = launch_folded<1>(kwv, grid, *p, st);
-    else if (p->group == 2) e = launch_folded<2>(kwv, grid, *p, st);
-    else if (p->group == 4) e = launch_folded<4>(kwv, grid, *p, st);
+    if (p->group == 1) e = launch_folded<1>(kwv, pd, grid, *p, st);
+    else if (p->group == 2) e = launch_folded<2>(kwv, pd, grid, *p, st);
+    else if (p->group == 4) e = launch_folded<4>(kwv, pd, grid, *p, st);
     else return hipErrorInvalidValue;
     if (e != hipSuccess) return e;
     if (p->nparts > 1)
@@ -439,10 +453,10 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     // 109 us, 5.9 TB/s).  (A next-page register prefetch variant cost 2-10 % and was removed.)
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
-    if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, false>), grid, dim3(512), 0, st, *p);
-    else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, false>), grid, dim3(64), 0, st, *p);
-    else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, false>), grid, dim3(128), 0, st, *p);
-    else hipLaunchKernelGGL((paged_attention_kernel<1, 4, false>), grid, dim3(256), 0, st, *p);
+    if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, 1>), grid, dim3(512), 0, st, *p);
+    else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 1>), grid, dim3(64), 0, st, *p);
+    else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 1>), grid, dim3(128), 0, st, *p);
+    else hipLaunchKernelGGL((paged_attention_kernel<1, 4, 1>), grid, dim3(256), 0, st, *p);
     if (p->nparts > 1)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else {

@@ -141,6 +141,21 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
   return c;
 }
 
+// gemm_stream launch, or its LDS-DMA ring form (gemm_ring_kernel) where that applies: 33-64 rows, one 16-column
+// tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 8 (the 7-8-wave shapes; LDS).  DSSE_S_RING=0
+// turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
+// waves 4.55 / 4.66 (gate_up 45.8 -> 43.5 us, LM head 52.5 -> 48.3; profiles/r2/ring_*.log).
+hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const void* X, int M, const void* W, int K,
+                         int N, const dsse::GemmEpi* ep, float* part) {
+  const int ring = env_int("DSSE_S_RING", 1);
+  if (ring > 0 && c.mt == 4 && c.nt == 1 && M > 32 && M <= 64 && K % (128 * S) == 0) {
+    const int nw = c.nw >= 7 ? 8 : 4, d = nw == 8 ? 3 : 4;
+    if ((N / 16) % nw == 0)
+      return dsse_gemm_ring(mode, nw, d, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
+  }
+  return dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
+}
+
 // Wide-batch kernel configuration (gemm_wide.hip, 32x32x16 MFMAs, 128 columns per workgroup).  Env
 // overrides: DSSE_W_SPLIT, DSSE_W_RD.
 struct WCfg {
@@ -280,8 +295,8 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
     const SCfg c = pick_stream(M, N, K, mode);
     at::Tensor part;
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
-    DSSE_CHECK_HIP(dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
-                                    c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    DSSE_CHECK_HIP(stream_launch(mode, c, c.S, 0, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
+                                 c.S > 1 ? part.data_ptr<float>() : nullptr));
     return;
   }
   int mt, nt, kw;
@@ -352,8 +367,8 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
       check_dtype(x, at::kBFloat16, "x");
       check_dtype(w, at::kBFloat16, "w");
       dsse::GemmEpi ep{};
-      DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kResidAdd, c.mt, c.nt, c.nw, c.rd, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N,
-                                      &ep, part.data_ptr<float>(), cur_stream()));
+      DSSE_CHECK_HIP(stream_launch(dsse::kResidAdd, c, c.S, 1, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
+                                   part.data_ptr<float>()));
       return c.S;
     }
   }
@@ -549,6 +564,8 @@ dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cach
   p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
   const int env_kwv = env_int("DSSE_ATTN_KWV", 0);
   p.kwv = (env_kwv == 1 || env_kwv == 2 || env_kwv == 4 || env_kwv == 8) ? env_kwv : 0;
+  const int env_pd = env_int("DSSE_ATTN_PD", 0);
+  p.pd = (env_pd == 1 || env_pd == 2) ? env_pd : 0;
   return p;
 }
 
@@ -634,9 +651,14 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
     const WCfg c = pick_wide(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
   } else {
-    const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
-    DSSE_CHECK_HIP(dsse_gemm_stream(dsse::kQkvRope, c.mt, c.nt, c.nw, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl,
-                                    cur_stream()));
+    SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
+    // DSSE_QKV_NW: waves per workgroup of the QKV projection alone (odd counts instantiated for mt 4, nt 1, rd 1)
+    const int qnw = env_int("DSSE_QKV_NW", 0);
+    if (qnw >= 2 && qnw <= 8 && c.mt == 4 && c.nt == 1 && M <= 64 && (N / 16) % qnw == 0) {
+      c.nw = qnw;
+      c.rd = 1;
+    }
+    DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, S, 1, X, M, w.data_ptr(), K, N, &ep, sl));
   }
   p.qkv_part = sl;
   p.qkv_S = S;

@@ -287,6 +287,160 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
   return hipErrorInvalidValue;
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// gemm_ring: the X-streaming GEMM with X AND the weights staged by LDS-DMA in one ordered stream (M <= 16 MT).
+//
+// gemm_stream stages X through VGPRs one slice ahead; the `s_waitcnt vmcnt` that store_x needs for those loads
+// also retires every weight load issued before them (VMEM completes in order), and at its loop heads hipcc
+// waits vmcnt(0) for the register ring: the weight stream drains to a few chunks per wave.  Here nothing VMEM
+// has a VGPR destination: for K-chunk c (128 columns) every wave issues its share of the chunk's X rows
+// (global_load_lds) and its own 4 KiB weight chunk (buffer_load ... lds, range-checked) into LDS slot c % D,
+// D - 1 chunks ahead of the MFMAs.  One counted vmcnt + barrier per chunk publishes chunk c (all waves' shares
+// landed) while chunks c+1 .. c+D-2 stay in flight; the slot refilled after the MFMAs of chunk c held chunk
+// c - 1, which every wave finished before that barrier.  Look-ahead issues past the last chunk keep the per-wave
+// load count uniform (the vmcnt literal depends on it): the weight loads fail the buffer range check (no
+// traffic), the X loads re-read the last chunk into a slot nobody reads.
+// Slot = [X image: 16 MT rows x 256 B, 16-B pieces XOR-swizzled by swz() on the source address -- the DMA writes
+// LDS lane-linearly -- and read back with the same XOR (gemm_stream's X image)] [NW x 4 KiB weight chunks in
+// MFMA B-fragment order, read back lane-linearly].
+template <int MT, int NW, int D>
+struct RingGeom {
+  static constexpr int SLOTX = 16 * MT * 256, SLOT = SLOTX + NW * 4096;
+  static constexpr size_t LDS = (size_t)D * SLOT;
+};
+
+DEV void glds16_s(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(src),
+                                   reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                       reinterpret_cast<uintptr_t>(lds_base)),
+                                   16, 0, 0);
+}
+
+template <int MT, int NW, int D, int MODE>
+__global__ void __launch_bounds__(64 * NW)
+gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
+                 GemmEpi ep, float* __restrict__ part) {
+  using G = RingGeom<MT, NW, D>;
+  constexpr int MP = 16 * MT;
+  constexpr int XI = MP / 4 / NW;         // 1 KiB X DMA instructions per wave per chunk (4 rows each)
+  static_assert(MP / 4 % NW == 0 && XI >= 1, "X chunk rows must split evenly over the waves");
+  static_assert(D >= 3 && G::LDS <= 160 * 1024, "ring of >= 3 slots within the CU's LDS");
+  constexpr int PER = XI + 4;             // VMEM instructions per wave per chunk
+  constexpr int WAUX = DSSE_W_DEFAULT ? 0 : kAuxNT;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  int wg = blockIdx.x, ks = blockIdx.y;
+  if (DSSE_XCD_SPLITK && gridDim.y > 1 && 8 % gridDim.y == 0 && (gridDim.x * gridDim.y) % 8 == 0) {
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x, xcd = lin % 8, slot = lin / 8, per = 8 / gridDim.y;
+    ks = xcd / per;
+    wg = slot * per + xcd % per;
+  }
+  const int tgi = wg * NW + w;  // this wave's 16-column tile
+  const int k0 = ks * Kr;
+  const int nch = Kr >> 7;
+  const int KC = K >> 7;
+
+  const int tgu = __builtin_amdgcn_readfirstlane(tgi), k0u = __builtin_amdgcn_readfirstlane(k0);
+  const __amdgpu_buffer_rsrc_t wrs =
+      make_rsrc(W + ((size_t)tgu * KC + (k0u >> 7)) * kTileChunk, (uint32_t)nch * kTileChunk * 2);
+
+  // this lane's X source per DMA instruction: row 4 (w XI + i) + g, logical piece r ^ swz(row & 15)
+  const bf16* xsrc[XI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int row = 4 * (w * XI + i) + g;
+    xsrc[i] = X + (size_t)min(row, M - 1) * ldx + k0 + 8 * (r ^ swz(row & 15));
+  }
+  auto issue = [&](int c, int slot) {
+    const int cc = min(c, nch - 1);
+    char* base = smem + slot * G::SLOT;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) glds16_s(xsrc[i] + cc * 128, base + (w * XI + i) * 1024);
+    char* wb = base + G::SLOTX + w * 4096;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(wb + 1024 * s)),
+          16, (uint32_t)c * (kTileChunk * 2) + 1024 * s + lane * 16, 0, 0, WAUX);
+  };
+
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) issue(d, d);
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      if (u > 0 && c0 + u >= nch) break;
+      // chunk c0 + u landed for every wave, chunks up to c0 + u + D - 2 still in flight
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((D - 2) * PER) : "memory");
+      const char* xb = smem + u * G::SLOT;
+      const char* wb = xb + G::SLOTX + w * 4096 + lane * 16;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 xf[MT];
+        const int ch = ((4 * g + s) ^ swz(r)) << 4;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * 256 + ch);
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wb + 1024 * s);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16x16x32(xf[mt], wf, acc[mt]);
+      }
+      // refill the slot of chunk c - 1 (every wave finished it before the barrier above); the LDS reads of this
+      // chunk must be done before the slot is reused D - 1 chunks later: the next barriers order that
+      issue(c0 + u + D - 1, (u + D - 1) % D);
+    }
+  }
+  // no LDS-DMA may still be landing when the workgroup's LDS is handed to the next workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
+  if constexpr (MODE == kSiluMul) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) silu_epilogue4(ep, M, 16 * mt + 4 * g, tgi, r, acc[mt]);
+    return;
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = acc[mt][i];
+      const float partner = MODE == kQkvRope ? __shfl_xor(v, 8) : 0.f;
+      epilogue<MODE>(ep, part_ks, M, N, 16 * mt + 4 * g + i, tgi, r, v, partner);
+    }
+}
+
+template <int MT, int NW, int D, int MODE>
+static hipError_t launch_r(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
+                           float* part, hipStream_t st) {
+  const size_t lds = RingGeom<MT, NW, D>::LDS;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<MT, NW, D, MODE>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  dim3 grid(N / 16 / NW, S), block(64 * NW);
+  hipLaunchKernelGGL((gemm_ring_kernel<MT, NW, D, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep, part);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_r_mode(int nw, int d, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
+                                const GemmEpi& ep, float* part, hipStream_t st) {
+#define DSSE_R_CASE(NW_, D_) \
+  if (nw == NW_ && d == D_) return launch_r<4, NW_, D_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  DSSE_R_CASE(4, 4) DSSE_R_CASE(8, 3)
+#undef DSSE_R_CASE
+  return hipErrorInvalidValue;
+}
+
 }  // namespace dsse
 
 // rd: weight-ring depth in LDS slices (mt <= 4: 1 = 4 chunks = 16 KiB per wave in flight, 2 = 8 chunks;
@@ -312,6 +466,30 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
     return hipErrorInvalidValue;
   }
   hipError_t e = launch_s_mode<kPartial>(mt, nt, nw, rd, x, ldx, M, w, K, N, S, *ep, part, st);
+  if (e != hipSuccess || partial_only) return e;
+  return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
+}
+
+// Ring variant (gemm_ring_kernel): 33 <= M <= 64 rows, (nw, ring depth d) in {(4, 4), (8, 3)};
+// K % (128 S) == 0, (N / 16) % nw == 0.
+extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int d, int S, int partial_only, const void* X, int ldx, int M,
+                                     const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
+                                     hipStream_t st) {
+  using namespace dsse;
+  const bf16* x = reinterpret_cast<const bf16*>(X);
+  const bf16* w = reinterpret_cast<const bf16*>(W);
+  if (M > 64 || M < 1 || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
+  if (S == 1 && !partial_only) {
+    switch (mode) {
+      case kStoreBf16: return launch_r_mode<kStoreBf16>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_r_mode<kStoreF32>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_r_mode<kResidAdd>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_r_mode<kSiluMul>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_r_mode<kQkvRope>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+    }
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = launch_r_mode<kPartial>(nw, d, x, ldx, M, w, K, N, S, *ep, part, st);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

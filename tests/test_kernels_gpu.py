@@ -25,10 +25,13 @@ def _close(a, b, atol, rtol, what=""):
 
 GEMM_CONFIGS = {
     "auto": {},
-    "stream-default": {"DSSE_GEMM_IMPL": "2"},
+    "stream-default": {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": "0"},
     "stream-nt2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NT": "2"},
     "stream-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
     "stream-nw4-split4": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "4"},
+    "ring": {"DSSE_GEMM_IMPL": "2"},
+    "ring-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
+    "ring-nw8": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "8"},
     "wide-default": {"DSSE_GEMM_IMPL": "3"},
     "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
     "tiled-default": {"DSSE_GEMM_IMPL": "4"},
@@ -119,6 +122,35 @@ def test_gemm_silu(gpu, tiles, M):
     _close(out, ref, 2e-2, 2e-2, "gemm_silu")
 
 
+@pytest.mark.parametrize("ring,nw", [("1", "4"), ("1", "8")])
+@pytest.mark.parametrize("M,K,S", [(33, 14336, "1"), (64, 14336, "4"), (48, 1536, "3"), (64, 4096, "2")])
+def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S):
+    """LDS-DMA ring GEMM (gemm_ring_kernel): chunk counts per workgroup that are not multiples of the ring depth,
+    split-K slabs reduced by the library, every epilogue against the fp32 reference."""
+    g = torch.Generator().manual_seed(M * 7 + K + int(nw))
+    N = 16 * int(nw) * 5
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
+    for k, v in {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": ring, "DSSE_S_NW": nw, "DSSE_S_SPLIT": S}.items():
+        monkeypatch.setenv(k, v)
+    ops.refresh_env()
+    out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
+    ref = torch.zeros(M, N, dtype=torch.float32)
+    ops.gemm_out(x, w, out)
+    R.gemm_out(x.cpu(), w.cpu(), ref)
+    _close(out, ref, 1e-3, 1e-2, f"ring gemm_out d={ring} nw={nw} S={S}")
+    r0 = torch.randn(M, N, generator=g)
+    rr = r0.clone().to(gpu)
+    ops.gemm_resid(x, w, rr)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    _close(rr, r0, 1e-3, 1e-3, "ring gemm_resid")
+    h = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+    hr = torch.zeros(M, N // 2, dtype=torch.bfloat16)
+    ops.gemm_silu(x, w, h)
+    R.gemm_silu(x.cpu(), w.cpu(), hr)
+    _close(h, hr, 2e-2, 2e-2, "ring gemm_silu")
+
+
 @pytest.mark.parametrize("nw", [2, 3, 5, 6, 7])
 @pytest.mark.parametrize("M", [33, 64])
 def test_gemm_stream_odd_wave_counts(gpu, monkeypatch, nw, M):
@@ -128,6 +160,7 @@ def test_gemm_stream_odd_wave_counts(gpu, monkeypatch, nw, M):
     x = _rand(M, K, dev=gpu, gen=g)
     w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / 45, gen=g))
     monkeypatch.setenv("DSSE_GEMM_IMPL", "2")
+    monkeypatch.setenv("DSSE_S_RING", "0")  # the gemm_stream kernel itself (the ring form takes 4 / 8 waves)
     monkeypatch.setenv("DSSE_S_NW", str(nw))
     ops.refresh_env()
     for split in ("1", "2"):

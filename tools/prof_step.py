@@ -1,6 +1,6 @@
 """Per-decode-step kernel breakdown from a rocprofv3 kernel trace.
 
-Usage: python tools/prof_step.py gpurun_out/prof/run_kernel_trace.csv [--marker sample_pick] [--last 6]
+Usage: python tools/prof_step.py gpurun_out/prof/run_kernel_trace.csv (or rocprofv3's run_results.db) [--marker sample_pick] [--last 6]
 
 A decode step ends with the sampler's pick kernel; the last `--last` steady-state steps (no admission,
 prefill or slot-metadata uploads) are averaged: per kernel name, calls and GPU time per step, plus the step's wall time (end of one pick to
@@ -27,9 +27,15 @@ def main():
     ap.add_argument("--last", type=int, default=6)
     args = ap.parse_args()
     rows = []
-    with open(args.trace) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    if args.trace.endswith(".db"):  # rocprofv3's default SQLite output (ROCm 7)
+        import sqlite3
+
+        con = sqlite3.connect(args.trace)
+        rows = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+    else:
+        with open(args.trace) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     ends = [i for i, (_, _, n) in enumerate(rows) if args.marker in n]
     # steady-state steps only: no slot-metadata uploads (at most the one token-ring drain copy) and the
