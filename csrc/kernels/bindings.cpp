@@ -651,13 +651,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
     const WCfg c = pick_wide(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
   } else {
-    SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
-    // DSSE_QKV_NW: waves per workgroup of the QKV projection alone (odd counts instantiated for mt 4, nt 1, rd 1)
-    const int qnw = env_int("DSSE_QKV_NW", 0);
-    if (qnw >= 2 && qnw <= 8 && c.mt == 4 && c.nt == 1 && M <= 64 && (N / 16) % qnw == 0) {
-      c.nw = qnw;
-      c.rd = 1;
-    }
+    const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
     DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, S, 1, X, M, w.data_ptr(), K, N, &ep, sl));
   }
   p.qkv_part = sl;
