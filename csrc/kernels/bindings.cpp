@@ -142,14 +142,14 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
 }
 
 // gemm_stream launch, or its LDS-DMA ring form (gemm_ring_kernel) where that applies: 33-64 rows, one 16-column
-// tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 8 (the 7-8-wave shapes; LDS).  DSSE_S_RING=0
-// turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
+// tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 7 / 8 (the 7-8-wave shapes; LDS; gate_up on 7
+// waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8, DSSE_S_RING7=0).  DSSE_S_RING=0 turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
 // waves 4.55 / 4.66 (gate_up 45.8 -> 43.5 us, LM head 52.5 -> 48.3; profiles/r2/ring_*.log).
 hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const void* X, int M, const void* W, int K,
                          int N, const dsse::GemmEpi* ep, float* part) {
   const int ring = env_int("DSSE_S_RING", 1);
   if (ring > 0 && c.mt == 4 && c.nt == 1 && M > 32 && M <= 64 && K % (128 * S) == 0) {
-    const int nw = c.nw >= 7 ? 8 : 4, d = nw == 8 ? 3 : 4;
+    const int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4, d = nw >= 7 ? 3 : 4;
     if ((N / 16) % nw == 0)
       return dsse_gemm_ring(mode, nw, d, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
   }

@@ -323,8 +323,9 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
                  GemmEpi ep, float* __restrict__ part) {
   using G = RingGeom<MT, NW, D>;
   constexpr int MP = 16 * MT;
-  constexpr int XI = MP / 4 / NW;         // 1 KiB X DMA instructions per wave per chunk (4 rows each)
-  static_assert(MP / 4 % NW == 0 && XI >= 1, "X chunk rows must split evenly over the waves");
+  constexpr int XN = MP / 4;               // 1 KiB X DMA instructions per chunk (4 rows each)
+  constexpr int XI = (XN + NW - 1) / NW;  // per wave; with NW not dividing XN the surplus instructions repeat the
+                                          // last one (same bytes to the same LDS address: a benign duplicate)
   static_assert(D >= 3 && G::LDS <= 160 * 1024, "ring of >= 3 slots within the CU's LDS");
   constexpr int PER = XI + 4;             // VMEM instructions per wave per chunk
   constexpr int WAUX = DSSE_W_DEFAULT ? 0 : kAuxNT;
@@ -349,16 +350,18 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 
   // this lane's X source per DMA instruction: row 4 (w XI + i) + g, logical piece r ^ swz(row & 15)
   const bf16* xsrc[XI];
+  int xdst[XI];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
-    const int row = 4 * (w * XI + i) + g;
+    xdst[i] = __builtin_amdgcn_readfirstlane(min(w * XI + i, XN - 1));
+    const int row = 4 * xdst[i] + g;
     xsrc[i] = X + (size_t)min(row, M - 1) * ldx + k0 + 8 * (r ^ swz(row & 15));
   }
   auto issue = [&](int c, int slot) {
     const int cc = min(c, nch - 1);
     char* base = smem + slot * G::SLOT;
 #pragma unroll
-    for (int i = 0; i < XI; ++i) glds16_s(xsrc[i] + cc * 128, base + (w * XI + i) * 1024);
+    for (int i = 0; i < XI; ++i) glds16_s(xsrc[i] + cc * 128, base + xdst[i] * 1024);
     char* wb = base + G::SLOTX + w * 4096;
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -436,7 +439,7 @@ static hipError_t launch_r_mode(int nw, int d, const bf16* X, int ldx, int M, co
                                 const GemmEpi& ep, float* part, hipStream_t st) {
 #define DSSE_R_CASE(NW_, D_) \
   if (nw == NW_ && d == D_) return launch_r<4, NW_, D_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-  DSSE_R_CASE(4, 4) DSSE_R_CASE(8, 3)
+  DSSE_R_CASE(4, 4) DSSE_R_CASE(7, 3) DSSE_R_CASE(8, 3)
 #undef DSSE_R_CASE
   return hipErrorInvalidValue;
 }
@@ -470,7 +473,7 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }
 
-// Ring variant (gemm_ring_kernel): 33 <= M <= 64 rows, (nw, ring depth d) in {(4, 4), (8, 3)};
+// Ring variant (gemm_ring_kernel): 33 <= M <= 64 rows, (nw, ring depth d) in {(4, 4), (7, 3), (8, 3)};
 // K % (128 S) == 0, (N / 16) % nw == 0.
 extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int d, int S, int partial_only, const void* X, int ldx, int M,
                                      const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,

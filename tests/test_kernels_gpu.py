@@ -122,7 +122,7 @@ def test_gemm_silu(gpu, tiles, M):
     _close(out, ref, 2e-2, 2e-2, "gemm_silu")
 
 
-@pytest.mark.parametrize("ring,nw", [("1", "4"), ("1", "8")])
+@pytest.mark.parametrize("ring,nw", [("1", "4"), ("1", "7"), ("1", "8")])
 @pytest.mark.parametrize("M,K,S", [(33, 14336, "1"), (64, 14336, "4"), (48, 1536, "3"), (64, 4096, "2")])
 def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S):
     """LDS-DMA ring GEMM (gemm_ring_kernel): chunk counts per workgroup that are not multiples of the ring depth,
