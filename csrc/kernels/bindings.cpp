@@ -148,10 +148,11 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
 hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const void* X, int M, const void* W, int K,
                          int N, const dsse::GemmEpi* ep, float* part) {
   const int ring = env_int("DSSE_S_RING", 1);
-  if (ring > 0 && c.mt == 4 && c.nt == 1 && M > 32 && M <= 64 && K % (128 * S) == 0) {
-    const int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4, d = nw >= 7 ? 3 : 4;
-    if ((N / 16) % nw == 0)
-      return dsse_gemm_ring(mode, nw, d, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
+  // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
+  const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32);
+  if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
+    const int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
+    if ((N / 16) % nw == 0) return dsse_gemm_ring(mode, nw, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
   }
   return dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
 }

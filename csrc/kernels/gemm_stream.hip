@@ -434,12 +434,19 @@ static hipError_t launch_r(const bf16* X, int ldx, int M, const bf16* W, int K, 
   return hipGetLastError();
 }
 
+// Ring depth per (rows, waves): as many 128-column chunks as the LDS holds (slot = 16 MT rows x 256 B of X +
+// NW x 4 KiB of weights, <= 160 KiB in all).
+constexpr int ring_depth(int mt, int nw) { return mt == 4 ? (nw == 4 ? 4 : 3) : (nw == 4 ? 6 : 4); }
+
 template <int MODE>
-static hipError_t launch_r_mode(int nw, int d, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
+static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                                 const GemmEpi& ep, float* part, hipStream_t st) {
-#define DSSE_R_CASE(NW_, D_) \
-  if (nw == NW_ && d == D_) return launch_r<4, NW_, D_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-  DSSE_R_CASE(4, 4) DSSE_R_CASE(7, 3) DSSE_R_CASE(8, 3)
+#define DSSE_R_CASE(MT_, NW_) \
+  if (mt == MT_ && nw == NW_)  \
+    return launch_r<MT_, NW_, ring_depth(MT_, NW_), MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  const int mt = M <= 32 ? 2 : 4;
+  DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
+  DSSE_R_CASE(2, 4) DSSE_R_CASE(2, 7) DSSE_R_CASE(2, 8)
 #undef DSSE_R_CASE
   return hipErrorInvalidValue;
 }
@@ -473,26 +480,26 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }
 
-// Ring variant (gemm_ring_kernel): 33 <= M <= 64 rows, (nw, ring depth d) in {(4, 4), (7, 3), (8, 3)};
+// Ring variant (gemm_ring_kernel): 17 <= M <= 64 rows (16 MT-row MFMA tiles, MT = 2 / 4 by M), nw in {4, 7, 8};
 // K % (128 S) == 0, (N / 16) % nw == 0.
-extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int d, int S, int partial_only, const void* X, int ldx, int M,
+extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, const void* X, int ldx, int M,
                                      const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
                                      hipStream_t st) {
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
-  if (M > 64 || M < 1 || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
+  if (M > 64 || M < 17 || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
   if (S == 1 && !partial_only) {
     switch (mode) {
-      case kStoreBf16: return launch_r_mode<kStoreBf16>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kStoreF32: return launch_r_mode<kStoreF32>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kResidAdd: return launch_r_mode<kResidAdd>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kSiluMul: return launch_r_mode<kSiluMul>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kQkvRope: return launch_r_mode<kQkvRope>(nw, d, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreBf16: return launch_r_mode<kStoreBf16>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_r_mode<kStoreF32>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_r_mode<kResidAdd>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_r_mode<kSiluMul>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_r_mode<kQkvRope>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
     }
     return hipErrorInvalidValue;
   }
-  hipError_t e = launch_r_mode<kPartial>(nw, d, x, ldx, M, w, K, N, S, *ep, part, st);
+  hipError_t e = launch_r_mode<kPartial>(nw, x, ldx, M, w, K, N, S, *ep, part, st);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

@@ -123,7 +123,8 @@ def test_gemm_silu(gpu, tiles, M):
 
 
 @pytest.mark.parametrize("ring,nw", [("1", "4"), ("1", "7"), ("1", "8")])
-@pytest.mark.parametrize("M,K,S", [(33, 14336, "1"), (64, 14336, "4"), (48, 1536, "3"), (64, 4096, "2")])
+@pytest.mark.parametrize("M,K,S", [(33, 14336, "1"), (64, 14336, "4"), (48, 1536, "3"), (64, 4096, "2"),
+                                   (17, 4096, "2"), (32, 14336, "4")])
 def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S):
     """LDS-DMA ring GEMM (gemm_ring_kernel): chunk counts per workgroup that are not multiples of the ring depth,
     split-K slabs reduced by the library, every epilogue against the fp32 reference."""
