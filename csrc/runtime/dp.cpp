@@ -135,12 +135,15 @@ std::vector<DpWorkerInfo> DpRouter::workers() {
 int DpRouter::pick_worker_locked(const std::string& conv_id) {
   auto it = convs_.find(conv_id);
   if (it != convs_.end() && it->second.worker >= 0 && info_[(size_t)it->second.worker].alive) return it->second.worker;
+  // least outstanding; ties rotate (a low request rate would otherwise always land on the lowest index)
   int best = -1;
-  for (int w = 0; w < n_; ++w) {
+  for (int k = 0; k < n_; ++k) {
+    const int w = (rr_ + k) % n_;
     const auto& i = info_[(size_t)w];
     if (!i.ready || !i.alive) continue;
     if (best < 0 || i.outstanding < info_[(size_t)best].outstanding) best = w;
   }
+  if (best >= 0) rr_ = (best + 1) % n_;
   return best;
 }
 

@@ -121,6 +121,7 @@ class DpRouter {
   Server& server_;
   std::string prefix_;
   int n_;
+  int rr_ = 0;  // first worker examined by the next pick: ties on outstanding rotate over the replicas
   size_t ring_bytes_;
   int timeout_ms_;
   std::vector<std::unique_ptr<ShmRing>> to_w_, from_w_;
