@@ -151,7 +151,10 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
   // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
   const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32);
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
-    const int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
+    int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
+    // QKV at 33-64 rows: 3 waves (384 tiles -> 128 x S 2 = 256 workgroups instead of 192; 64-stream step
+    // 4.38-4.40 vs 4.41-4.42 ms, profiles/r2/qkv_ring3_ab.log; DSSE_QKV_RING3=0 = 4 waves)
+    if (mode == dsse::kQkvRope && c.mt == 4 && env_int("DSSE_QKV_RING3", 1) && (N / 16) % 3 == 0) nw = 3;
     if ((N / 16) % nw == 0) return dsse_gemm_ring(mode, nw, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
   }
   return dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
