@@ -149,7 +149,8 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
                          int N, const dsse::GemmEpi* ep, float* part) {
   const int ring = env_int("DSSE_S_RING", 1);
   // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
-  const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32);
+  const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32) ||
+                         (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4 && env_int("DSSE_RING128", 1));
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
     int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
     // QKV at 33-64 rows: 3 waves (384 tiles -> 128 x S 2 = 256 workgroups instead of 192; 64-stream step
@@ -239,6 +240,12 @@ int gemm_impl(int M, int N, int K) {
   if (M > 64) {
     // every branch returns a kernel whose shape contract holds (or -1): prefill calls arrive with any M and
     // tensor-parallel shard shapes
+    // 65-128 rows, narrow N (4-wave stream shapes: qkv / o / down): the ring kernel with 8 row tiles, 3 slots;
+    // 128-stream step 6.19 / 6.23 vs 6.36 / 6.37 ms on gemm_wide (profiles/r2/ring128_ab.log); DSSE_RING128=0
+    if (impl < 0 && M <= 128 && env_int("DSSE_RING128", 1)) {
+      const SCfg sc = pick_stream(M, N, K);
+      if (sc.ok && sc.mt == 8 && sc.nt == 1 && sc.nw == 4) return 2;
+    }
     const bool tiled_ok = pick_tiled(M, N, K).ok;
     if (tiled_ok && (M > kMaxDecodeM || impl == 4 || (impl < 0 && M > env_int("DSSE_TILED_MIN_M", 128)))) return 4;
     if (M > kMaxDecodeM) return -1;  // the decode kernels stop at kMaxDecodeM rows

@@ -436,7 +436,9 @@ static hipError_t launch_r(const bf16* X, int ldx, int M, const bf16* W, int K, 
 
 // Ring depth per (rows, waves): as many 128-column chunks as the LDS holds (slot = 16 MT rows x 256 B of X +
 // NW x 4 KiB of weights, <= 160 KiB in all).
-constexpr int ring_depth(int mt, int nw) { return mt == 4 ? (nw == 3 ? 5 : (nw == 4 ? 4 : 3)) : (nw == 4 ? 6 : 4); }
+constexpr int ring_depth(int mt, int nw) {
+  return mt == 8 ? 3 : (mt == 4 ? (nw == 3 ? 5 : (nw == 4 ? 4 : 3)) : (nw == 4 ? 6 : 4));
+}
 
 template <int MODE>
 static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
@@ -444,7 +446,8 @@ static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf1
 #define DSSE_R_CASE(MT_, NW_) \
   if (mt == MT_ && nw == NW_)  \
     return launch_r<MT_, NW_, ring_depth(MT_, NW_), MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-  const int mt = M <= 32 ? 2 : 4;
+  const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
+  DSSE_R_CASE(8, 4)
   DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
   DSSE_R_CASE(2, 4) DSSE_R_CASE(2, 7) DSSE_R_CASE(2, 8)
 #undef DSSE_R_CASE
@@ -480,7 +483,8 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }
 
-// Ring variant (gemm_ring_kernel): 17 <= M <= 64 rows (16 MT-row MFMA tiles, MT = 2 / 4 by M), nw in {4, 7, 8};
+// Ring variant (gemm_ring_kernel): 17 <= M <= 64 rows (16 MT-row MFMA tiles, MT = 2 / 4 by M), nw in {3, 4, 7, 8};
+// 65-128 rows (MT 8) with nw = 4;
 // K % (128 S) == 0, (N / 16) % nw == 0.
 extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, const void* X, int ldx, int M,
                                      const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
@@ -488,7 +492,7 @@ extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, 
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
-  if (M > 64 || M < 17 || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
+  if (M > 128 || M < 17 || (M > 64 && nw != 4) || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
   if (S == 1 && !partial_only) {
     switch (mode) {
       case kStoreBf16: return launch_r_mode<kStoreBf16>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
