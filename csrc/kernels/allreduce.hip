@@ -1,0 +1,159 @@
+// Tensor-parallel decode all-reduce over IPC-mapped peer buffers, fused with residual-add + RMSNorm
+// (C1 / C2 of SURVEY.md §2.4; VERDICT round 2 "next 3b").
+//
+// RCCL's small-message all-reduce costs tens of microseconds and at TP = 8 the decode step runs
+// 64 of them (two per layer) against ~0.3 ms of per-rank weight streaming; the round-2 chain was also three
+// launches per all-reduce (gemm_out -> RCCL -> rmsnorm(delta)).  Here the O / down projection's bf16 partial
+// product [M, H] (gemm_out) goes straight into ONE kernel per all-reduce:
+//
+//   workgroup b (row b of the decode batch), rank r of T:
+//     1. e = ++epoch[b] (a per-row call counter only this workgroup touches), parity p = e & 1
+//     2. copy its partial row into its OWN IPC buffer, data[p][b] (write-through sc0 sc1 stores)
+//     3. system-scope release, then one flag store per peer q: peer_q.flags[r][b] = e
+//     4. wait for flags[q][b] >= e from every peer (system-scope relaxed polls, bounded)
+//     5. read data[p][b] of every rank q = 0..T-1 over xGMI (sc0 sc1 loads), sum in rank order in fp32 (the same
+//        bits on every rank), resid[b] += sum, y[b] = rmsnorm(resid[b]) * w
+//
+// Double buffering by parity makes one flag exchange per call enough: rank r writes data[p][b] again only at
+// call e + 2, after it passed the barrier of call e + 1, which every peer entered after it finished reading call
+// e's data (stream order).  Peers are at most one call ahead (they cannot pass call e + 1 without r's flag), so
+// `flags >= e` is exact.  All workgroups of a launch are independent (row b only waits for row b of the
+// peers), so the grid needs no co-residency; every wait is bounded (kArSpinLimit sleeps, ~1 s) and a timeout
+// sets err[0] instead of hanging the GPU (the engine checks it and falls back to RCCL).
+//
+// IPC buffer of one rank (ar_buffer_bytes): [flags: kArMaxRanks x rows uint32][pad to 4 KiB][data: 2 x rows x H
+// bf16].  Allocated uncached (hipDeviceMallocUncached) when the runtime allows it, so neither side's L2 holds
+// a stale copy of another process's writes; the sc0 sc1 cache-policy bits are set on every access anyway.
+#include "api.h"
+
+#include <cstring>
+
+namespace dsse {
+
+constexpr int kArMaxRanks = 8;
+constexpr int kArSpinLimit = 1 << 22;
+constexpr int kAuxSys = 1 | 16;  // sc0 | sc1: system-coherent (bypass the non-coherent caches)
+
+__host__ __device__ inline size_t ar_data_off(int rows) { return ((size_t)kArMaxRanks * rows * 4 + 4095) & ~(size_t)4095; }
+
+// H / 8 threads per workgroup (16 bytes of bf16 per lane), H <= 8192.
+__global__ void __launch_bounds__(1024)
+ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const bf16* __restrict__ w,
+                  bf16* __restrict__ y, int H, float eps, const unsigned long long* __restrict__ peers, int rank,
+                  int world, int rows, unsigned int* __restrict__ epoch, unsigned int* __restrict__ err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ unsigned int e_s;
+  __shared__ float red[16];
+  if (tid == 0) e_s = epoch[b] + 1;
+  __syncthreads();
+  const unsigned int e = e_s;
+  const size_t doff = ar_data_off(rows) + (((size_t)(e & 1) * rows + b) * H + (size_t)tid * 8) * 2;
+  // 2. partial row -> own IPC buffer (write-through stores, drained before the barrier)
+  const unsigned long long mine_u = peers[rank];
+  char* mine = reinterpret_cast<char*>(mine_u);
+  const __amdgpu_buffer_rsrc_t mrs = make_rsrc(
+      reinterpret_cast<const void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(mine_u >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mine_u)), 0x7FFFFFFF);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = *reinterpret_cast<const u32x4*>(tmp + (size_t)b * H + tid * 8);
+  __builtin_amdgcn_raw_buffer_store_b128(v, mrs, (uint32_t)doff, 0, kAuxSys);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // 3. flags to every peer (after a system-scope release), 4. wait for every peer's
+  if (tid < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int* pf = reinterpret_cast<unsigned int*>(peers[tid]) + (size_t)rank * rows + b;
+    __hip_atomic_store(pf, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned int* mf = reinterpret_cast<const unsigned int*>(mine) + (size_t)tid * rows + b;
+    int spins = 0;
+    while (__hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e && ++spins < kArSpinLimit)
+      __builtin_amdgcn_s_sleep(2);
+    if (spins >= kArSpinLimit) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();  // every peer's row is in its memory: read it with system-coherent loads only
+  // 5. sum the T partial rows in rank order (identical bits on every rank)
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  bf16x8 d[kArMaxRanks];
+#pragma unroll
+  for (int q = 0; q < kArMaxRanks; ++q) {  // every peer's load in flight before the first use
+    if (q < world) {
+      const unsigned long long pq = peers[q];
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(
+          reinterpret_cast<const void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pq >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pq)), 0x7FFFFFFF);
+      d[q] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)doff, 0, kAuxSys));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kArMaxRanks; ++q)
+    if (q < world)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(d[q][j]);
+  float* rp = resid + (size_t)b * H + tid * 8;
+  float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+  r0.x += acc[0]; r0.y += acc[1]; r0.z += acc[2]; r0.w += acc[3];
+  r1.x += acc[4]; r1.y += acc[5]; r1.z += acc[6]; r1.w += acc[7];
+  *reinterpret_cast<float4*>(rp) = r0;
+  *reinterpret_cast<float4*>(rp + 4) = r1;
+  float ss = r0.x * r0.x + r0.y * r0.y + r0.z * r0.z + r0.w * r0.w + r1.x * r1.x + r1.y * r1.y + r1.z * r1.z +
+             r1.w * r1.w;
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
+  const float inv = rsqrtf(tot / (float)H + eps);
+  const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + tid * 8);
+  const float rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(rv[j] * inv * bf2f(wv[j]));
+  *reinterpret_cast<bf16x8*>(y + (size_t)b * H + tid * 8) = o;
+  if (tid == 0) epoch[b] = e;
+}
+
+}  // namespace dsse
+
+using namespace dsse;
+
+extern "C" size_t dsse_ar_buffer_bytes(int rows, int H) {
+  return ar_data_off(rows) + (size_t)2 * rows * H * 2;
+}
+
+// Allocate one rank's zeroed IPC buffer; *uncached = 1 when hipDeviceMallocUncached was honoured.
+extern "C" hipError_t dsse_ar_alloc(size_t bytes, void** ptr, void* handle64, int* uncached) {
+  *uncached = 1;
+  hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *uncached = 0;
+    e = hipMalloc(ptr, bytes);
+  }
+  if (e != hipSuccess) return e;
+  if ((e = hipMemset(*ptr, 0, bytes)) != hipSuccess) return e;
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle64), *ptr);
+}
+
+extern "C" hipError_t dsse_ar_open(const void* handle64, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle64, sizeof h);
+  return hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" hipError_t dsse_ar_close(void* ptr, int opened) { return opened ? hipIpcCloseMemHandle(ptr) : hipFree(ptr); }
+
+extern "C" hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, const void* w, void* y, int H, float eps,
+                                      const unsigned long long* peers, int rank, int world, int rows,
+                                      unsigned int* epoch, unsigned int* err, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (M > rows || world > kArMaxRanks || world < 1 || rank < 0 || rank >= world || H % 512 != 0 || H / 8 > 1024)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ar_rmsnorm_kernel, dim3(M), dim3(H / 8), 0, st, reinterpret_cast<const bf16*>(tmp), resid,
+                     reinterpret_cast<const bf16*>(w), reinterpret_cast<bf16*>(y), H, eps, peers, rank, world, rows,
+                     epoch, err);
+  return hipGetLastError();
+}

@@ -105,7 +105,7 @@ hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::Samp
                             hipStream_t st);
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
                         const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
-                        int vocab, hipStream_t st);
+                        int vocab, void* sync, int sync_rows, hipStream_t st);
 hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                               const int* slots, const float2* rope, void* q_out, void* k_cache,
                               void* v_cache, int num_slots, int rope_len, hipStream_t st);
@@ -113,6 +113,14 @@ hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
 hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
                             int max_blocks, int num_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
 hipError_t dsse_ring_advance(int* counter, hipStream_t st);
+// TP all-reduce + residual + RMSNorm over IPC peer buffers (allreduce.hip)
+size_t dsse_ar_buffer_bytes(int rows, int H);
+hipError_t dsse_ar_alloc(size_t bytes, void** ptr, void* handle64, int* uncached);
+hipError_t dsse_ar_open(const void* handle64, void** ptr);
+hipError_t dsse_ar_close(void* ptr, int opened);
+hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, const void* w, void* y, int H, float eps,
+                           const unsigned long long* peers, int rank, int world, int rows, unsigned int* epoch,
+                           unsigned int* err, hipStream_t st);
 // Checked build: first out-of-range index per kernel file (line, value, bound, count); zeros otherwise.
 hipError_t dsse_check_gemm_skinny(int* out, int clear);
 hipError_t dsse_check_gemm_stream(int* out, int clear);

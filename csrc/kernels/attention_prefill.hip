@@ -19,10 +19,6 @@
 //   softmax    = online, base 2, masked scores contribute exactly 0 (fully masked columns stay 0).
 #include "api.h"
 
-#ifndef DSSE_PREFILL_NOSOFTMAX
-#define DSSE_PREFILL_NOSOFTMAX 0
-#endif
-
 // K/V staging by LDS-DMA (global_load_lds, no VGPRs, no ds_write pass) -- 1, default -- or through registers
 // (0, variant build "pfregs": the round-1 form, kept for A/B).
 #ifndef DSSE_PREFILL_GLDS
@@ -192,19 +188,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
         }
       }
-#if DSSE_PREFILL_NOSOFTMAX  // timing experiment (variant build "pfnosm"): MFMA + staging cost without the softmax
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            pf[qt][t][i] = f2bf(s4[2 * t][qt][i]);
-            pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
-          }
-      l_run[0] = l_run[1] = 1.f;
-#else
       const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
       bf16x8 pf[2][2];  // [qt][page t]
 #pragma unroll
@@ -270,7 +253,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
             pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
           }
       }
-#endif
       // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
 #pragma unroll
       for (int t = 0; t < 2; ++t)

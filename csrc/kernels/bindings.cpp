@@ -14,8 +14,9 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
-#include <mutex>
+#include <atomic>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 
 #include "api.h"
@@ -40,16 +41,22 @@ void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
 }
 
-// Tuning knobs (DSSE_* environment variables) are read once and cached: no getenv on the launch path.
-// refresh_env() (op dsse::refresh_env) re-reads them, for the tuning tools that change them in-process.
-std::mutex g_env_mu;
-std::unordered_map<std::string, int> g_env;
+// Tuning knobs (DSSE_* environment variables) are read once per thread and cached in a thread-local map: no
+// getenv and no lock on the launch path.  refresh_env() (op dsse::refresh_env, for the tuning tools that change
+// them in-process) bumps a generation that makes every thread re-read on its next lookup.
+std::atomic<uint64_t> g_env_gen{1};
 int env_int(const char* name, int dflt) {
-  std::lock_guard<std::mutex> lk(g_env_mu);
-  auto it = g_env.find(name);
-  if (it == g_env.end()) {
+  thread_local std::unordered_map<std::string, int> cache;
+  thread_local uint64_t gen = 0;
+  const uint64_t g = g_env_gen.load(std::memory_order_acquire);
+  if (gen != g) {
+    cache.clear();
+    gen = g;
+  }
+  auto it = cache.find(name);
+  if (it == cache.end()) {
     const char* v = std::getenv(name);
-    it = g_env.emplace(name, v ? std::atoi(v) : INT32_MIN).first;
+    it = cache.emplace(name, v ? std::atoi(v) : INT32_MIN).first;
   }
   return it->second == INT32_MIN ? dflt : it->second;
 }
@@ -69,10 +76,7 @@ const bool g_fpe_trap = [] {
   return true;
 }();
 
-void refresh_env() {
-  std::lock_guard<std::mutex> lk(g_env_mu);
-  g_env.clear();
-}
+void refresh_env() { g_env_gen.fetch_add(1, std::memory_order_acq_rel); }
 
 
 
@@ -96,6 +100,7 @@ void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
 struct SCfg {
   int mt, nt, nw, rd, S;
   bool ok;
+  int ring_nw = 0;  // waves per workgroup of the LDS-DMA ring form (0 = stream_launch's default rule)
 };
 // 64 < M <= 256: one workgroup holds all rows (mt 8 / 16, X slices of 256 / 128 columns); M > 256: row
 // blocks of 64 (mt 4, L2-shared weights).
@@ -153,6 +158,8 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
                          (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4 && env_int("DSSE_RING128", 1));
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
     int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
+    if (c.ring_nw > 0 && (N / 16) % c.ring_nw == 0 && M <= 64)
+      return dsse_gemm_ring(mode, c.ring_nw, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
     // QKV at 33-64 rows: 3 waves (384 tiles -> 128 x S 2 = 256 workgroups instead of 192; 64-stream step
     // 4.38-4.40 vs 4.41-4.42 ms, profiles/r2/qkv_ring3_ab.log; DSSE_QKV_RING3=0 = 4 waves)
     if (mode == dsse::kQkvRope && c.mt == 4 && env_int("DSSE_QKV_RING3", 1) && (N / 16) % 3 == 0) nw = 3;
@@ -373,7 +380,14 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
       return c.S;
     }
   } else if (impl == 2) {
-    const SCfg c = pick_stream(M, N, K);
+    SCfg c = pick_stream(M, N, K);
+    // 17-64 rows on the ring: DSSE_RESID_NW / DSSE_RESID_SPLIT = waves per workgroup and K split of the O / down
+    // projections (more K slices: fewer X bytes per workgroup, more slab bytes for the norm)
+    const int rnw = env_int("DSSE_RESID_NW", 0), rsp = env_int("DSSE_RESID_SPLIT", 0);
+    if (M > 16 && M <= 64 && rnw > 0 && rsp > 1 && (N / 16) % rnw == 0 && K % (128 * rsp) == 0) {
+      c.ring_nw = rnw;
+      c.S = rsp;
+    }
     if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
       check_dtype(x, at::kBFloat16, "x");
       check_dtype(w, at::kBFloat16, "w");
@@ -431,9 +445,12 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
   run_gemm(dsse::kQkvRope, x, w, ep);
 }
 
+// sync: optional int32 workspace of the row-split norm (elementwise.hip rmsnorm_split_kernel), 9 words per row
+// (four 8-byte granules + one generation word), owned by ONE caller (a model runner): two launches sharing it
+// must never run concurrently.  Zero-initialised once; never reset.
 void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
              const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids,
-             const c10::optional<Tensor>& part, int64_t nsplit) {
+             const c10::optional<Tensor>& part, int64_t nsplit, const c10::optional<Tensor>& sync) {
   check_gpu(resid, "resid");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -473,8 +490,16 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     mode = 3;
     pptr = part->data_ptr<float>();
   }
+  void* sptr = nullptr;
+  int sync_rows = 0;
+  if (sync.has_value() && env_int("DSSE_NORM_SPLIT", 1)) {
+    check_gpu(*sync, "sync");
+    check_dtype(*sync, at::kInt, "sync");
+    sync_rows = (int)(sync->numel() / 9);
+    if (sync_rows >= M) sptr = sync->data_ptr();
+  }
   DSSE_CHECK_HIP(dsse_rmsnorm(mode, M, resid.data_ptr<float>(), H, dptr, eptr, iptr, w.data_ptr(),
-                              y.data_ptr(), (float)eps, pptr, (int)nsplit, vocab, cur_stream()));
+                              y.data_ptr(), (float)eps, pptr, (int)nsplit, vocab, sptr, sync_rows, cur_stream()));
 }
 
 void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& rope,
@@ -662,7 +687,9 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
     const WCfg c = pick_wide(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
   } else {
-    const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
+    SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
+    const int qnw = env_int("DSSE_QKV_NW", 0);  // ring waves per workgroup (with DSSE_QKV_SPLIT)
+    if (qnw > 0 && M > 16 && M <= 64 && (N / 16) % qnw == 0) c.ring_nw = qnw;
     DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, S, 1, X, M, w.data_ptr(), K, N, &ep, sl));
   }
   p.qkv_part = sl;
@@ -760,7 +787,53 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 8; }
+// ---- TP all-reduce over IPC peer buffers (allreduce.hip) ------------------------------------------------------
+// ar_alloc: this rank's zeroed buffer for `rows` decode rows of width H -> (64-byte IPC handle as uint8 [64],
+// device pointer, uncached flag).  ar_open: a peer's handle -> its pointer in this process.  The buffers live
+// until ar_close (process lifetime in the engine).
+std::tuple<Tensor, int64_t, int64_t> ar_alloc(int64_t rows, int64_t H) {
+  TORCH_CHECK(rows > 0 && H > 0 && H % 512 == 0 && H <= 8192, "ar_alloc: bad shape");
+  Tensor h = at::zeros({64}, at::kByte);
+  void* p = nullptr;
+  int uncached = 0;
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+  DSSE_CHECK_HIP(dsse_ar_alloc(dsse_ar_buffer_bytes((int)rows, (int)H), &p, h.data_ptr(), &uncached));
+  return {h, (int64_t)reinterpret_cast<uintptr_t>(p), (int64_t)uncached};
+}
+int64_t ar_open(const Tensor& handle) {
+  TORCH_CHECK(handle.numel() == 64 && handle.scalar_type() == at::kByte && !handle.is_cuda(), "ar_open: 64-byte CPU handle");
+  void* p = nullptr;
+  DSSE_CHECK_HIP(dsse_ar_open(handle.contiguous().data_ptr(), &p));
+  return (int64_t)reinterpret_cast<uintptr_t>(p);
+}
+void ar_close(int64_t ptr, bool opened) { DSSE_CHECK_HIP(dsse_ar_close(reinterpret_cast<void*>(ptr), opened ? 1 : 0)); }
+
+// resid[b] += sum over ranks of tmp[b] (every rank's partial, read from the peers' buffers), y = rmsnorm(resid) * w.
+// peers: int64 device tensor [world] of buffer pointers in THIS process (own at index rank); epoch: int32 [rows],
+// zero-initialised, owned by this all-reduce context; err: int32 [1] (set on a timed-out peer wait).
+void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, double eps, const Tensor& peers,
+                int64_t rank, int64_t rows, Tensor& epoch, Tensor& err) {
+  for (const Tensor* t : {&tmp, (const Tensor*)&resid, &w, (const Tensor*)&y, &peers, (const Tensor*)&epoch,
+                          (const Tensor*)&err})
+    check_gpu(*t, "ar_rmsnorm tensor");
+  check_dtype(tmp, at::kBFloat16, "tmp");
+  check_dtype(resid, at::kFloat, "resid");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(y, at::kBFloat16, "y");
+  check_dtype(peers, at::kLong, "peers");
+  check_dtype(epoch, at::kInt, "epoch");
+  check_dtype(err, at::kInt, "err");
+  const int M = (int)tmp.size(0), H = (int)tmp.size(1);
+  TORCH_CHECK(tmp.dim() == 2 && resid.size(0) >= M && resid.size(1) == H && y.size(0) >= M && y.size(1) == H &&
+                  w.numel() == H, "ar_rmsnorm: shape mismatch");
+  TORCH_CHECK(M <= rows && epoch.numel() >= rows, "ar_rmsnorm: more rows than the buffers hold");
+  DSSE_CHECK_HIP(dsse_ar_rmsnorm(M, tmp.data_ptr(), resid.data_ptr<float>(), w.data_ptr(), y.data_ptr(), H, (float)eps,
+                                 reinterpret_cast<const unsigned long long*>(peers.data_ptr<int64_t>()), (int)rank,
+                                 (int)peers.numel(), (int)rows, reinterpret_cast<unsigned int*>(epoch.data_ptr<int>()),
+                                 reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
+}
+
+int64_t kernels_abi_version() { return 10; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -798,7 +871,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
-        "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
+        "Tensor? ids=None, Tensor? part=None, int nsplit=0, Tensor(c!)? sync=None) -> ()");
   m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
   m.def("refresh_env() -> ()", &refresh_env);
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
@@ -818,6 +891,11 @@ TORCH_LIBRARY(dsse, m) {
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
         "Tensor? ring_counter=None, Tensor(c!)? positions_inc=None, int vocab=2147483647) -> ()");
+  m.def("ar_alloc(int rows, int H) -> (Tensor, int, int)", &ar_alloc);
+  m.def("ar_open(Tensor handle) -> int", &ar_open);
+  m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
+  m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
+        "Tensor(c!) epoch, Tensor(d!) err) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
@@ -839,4 +917,5 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
+  m.impl("ar_rmsnorm", &ar_rmsnorm);
 }

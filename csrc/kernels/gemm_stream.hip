@@ -437,7 +437,7 @@ static hipError_t launch_r(const bf16* X, int ldx, int M, const bf16* W, int K, 
 // Ring depth per (rows, waves): as many 128-column chunks as the LDS holds (slot = 16 MT rows x 256 B of X +
 // NW x 4 KiB of weights, <= 160 KiB in all).
 constexpr int ring_depth(int mt, int nw) {
-  return mt == 8 ? 3 : (mt == 4 ? (nw == 3 ? 5 : (nw == 4 ? 4 : 3)) : (nw == 4 ? 6 : 4));
+  return mt == 8 ? 3 : (mt == 4 ? (nw == 3 ? 5 : (nw <= 6 ? 4 : 3)) : (nw == 4 ? 6 : 4));
 }
 
 template <int MODE>
@@ -448,7 +448,7 @@ static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf1
     return launch_r<MT_, NW_, ring_depth(MT_, NW_), MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   DSSE_R_CASE(8, 4)
-  DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
+  DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 5) DSSE_R_CASE(4, 6) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
   DSSE_R_CASE(2, 4) DSSE_R_CASE(2, 7) DSSE_R_CASE(2, 8)
 #undef DSSE_R_CASE
   return hipErrorInvalidValue;

@@ -84,12 +84,19 @@ void Bus::set_gate(std::shared_ptr<FrameGate> g) {
 }
 
 // Duplicate / post-terminal frame of conversation `c` (shard lock held).  A terminal conversation that sees
-// sequence 1 again starts a new stream (e.g. the next turn of a conversation id a client reuses).
+// sequence 1 again starts a new stream (e.g. the next turn of a conversation id a client reuses) -- but only
+// when that frame is NEWER than the terminal one (producer timestamp; without timestamps: the dedupe window
+// has passed since the terminal frame).  A redelivered first token of the finished stream is a duplicate: it
+// must not wipe the replay ring that Last-Event-ID reconnects read.
 bool Bus::duplicate_locked(Conv& c, const Frame& f, int64_t now) {
   if (f.seq <= 0) return false;
   if (c.done) {
-    if (f.seq == 1 && !f.done && c.done_seq > 1) {  // a new stream under the same conversation id
-      c.done = false;
+    if (f.seq == 1 && !f.done && c.done_seq > 1) {
+      const bool newer = (f.timestamp > 0 && c.done_ts > 0)
+                             ? f.timestamp > c.done_ts
+                             : (cfg_.dedupe_window_s <= 0 || now - c.done_mono > cfg_.dedupe_window_s * 1000000000LL);
+      if (!newer) return true;
+      c.done = false;  // a new stream under the same conversation id
       c.ring.clear();
       c.last_seq = 0;
       return false;
@@ -124,6 +131,8 @@ int Bus::deliver(const FramePtr& f, std::vector<SinkPtr>* flush_list) {
       c.done = true;
       c.done_seq = f->seq;
       c.done_ns = now_ns();
+      c.done_ts = f->timestamp;
+      c.done_mono = f->created_mono;
     }
     subs = c.subs;  // a reference to the current (immutable) list; pushes happen outside the shard lock
   }

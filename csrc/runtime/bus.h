@@ -121,6 +121,8 @@ class Bus {
     bool done = false;
     int64_t done_seq = 0;
     int64_t done_ns = 0;
+    int64_t done_ts = 0;    // producer timestamp of the terminal frame
+    int64_t done_mono = 0;  // its created_mono
   };
   struct Shard {
     std::mutex mu;

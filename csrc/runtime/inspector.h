@@ -10,6 +10,7 @@
 //                        verdict kills the conversation (publishes on chat.<id>.control)
 //   hybrid             - tokens are held for INSPECTION_BUFFER_MS while inspected, then released
 #pragma once
+#include <cstdint>
 #include <string>
 #include <string_view>
 
@@ -36,6 +37,9 @@ const char* inspection_mode_name(InspectionMode m);
 // {"subject","data","sequence","timestamp"} to the endpoint URL (the Spin function's POST /inspect,
 // src/spin-functions/nats-subscriber/src/lib.rs:34-54) and parses {"action","reason","redacted_content"}.
 // Blocking HTTP/1.1 over one keep-alive connection (reconnected on error); one client per calling thread.
+// Every wait is bounded by timeout_ms (connect included: non-blocking connect + poll), and a failure opens a
+// circuit: for the next 1 s (doubling per consecutive failure, up to 30 s) inspect() fails at once, so the
+// caller fails open instead of paying the timeout per token while the endpoint is down.
 class RemoteInspector {
  public:
   explicit RemoteInspector(const std::string& url, int timeout_ms = 250);
@@ -50,9 +54,13 @@ class RemoteInspector {
  private:
   bool connect_();
   bool roundtrip(const std::string& req, std::string* body);
+  void trip();
+  static constexpr int64_t kMinBackoffMs = 1000, kMaxBackoffMs = 30000;
   std::string host_, port_, path_;
   int timeout_ms_;
   int fd_ = -1;
+  int64_t open_until_ns_ = 0;
+  int64_t backoff_ms_ = kMinBackoffMs;
 };
 
 }  // namespace dsse

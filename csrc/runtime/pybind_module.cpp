@@ -17,6 +17,7 @@
 #include "json.h"
 #include "metrics.h"
 #include "server.h"
+#include "shm_ring.h"
 #include "util.h"
 
 namespace py = pybind11;
@@ -272,6 +273,72 @@ class DpWorkerPy {
   bool shutdown_ = false;
 };
 
+// One direction of a same-node control channel (bytes messages) over a POSIX shm SPSC ring: the TP leader's
+// per-step plan to each follower (serving/tp.py ShmPlanChannel).  The creator owns (and unlinks) the ring.
+class ShmChannelPy {
+ public:
+  ShmChannelPy(const std::string& name, bool create, size_t capacity, int open_timeout_ms) {
+    std::string err;
+    {
+      py::gil_scoped_release nogil;
+      r_ = create ? ShmRing::create(name, capacity, true, &err) : ShmRing::open(name, open_timeout_ms, &err);
+    }
+    if (!r_) throw std::runtime_error("shm channel: " + err);
+  }
+  bool push(const py::bytes& b, int timeout_ms) {
+    std::string s = b;
+    py::gil_scoped_release nogil;
+    return timeout_ms > 0 ? r_->push_wait(s.data(), (uint32_t)s.size(), timeout_ms) : r_->push(s.data(), (uint32_t)s.size());
+  }
+  py::object pop(int timeout_ms, int spin_us) {
+    std::string out;
+    bool got;
+    {
+      py::gil_scoped_release nogil;
+      got = timeout_ms > 0 || spin_us > 0 ? r_->pop_wait(&out, timeout_ms, spin_us) : r_->pop(&out);
+    }
+    if (!got) return py::none();
+    return py::bytes(out);
+  }
+  void close() { r_->close(); }
+  bool closed() const { return r_->closed(); }
+  const std::string& name() const { return r_->name(); }
+
+ private:
+  std::unique_ptr<ShmRing> r_;
+};
+
+// The TP leader's side of the plan channel: one ring per follower, every message pushed to all of them in one
+// call without the GIL.
+class ShmFanoutPy {
+ public:
+  ShmFanoutPy(const std::vector<std::string>& names, size_t capacity) {
+    std::string err;
+    py::gil_scoped_release nogil;
+    for (const auto& n : names) {
+      auto r = ShmRing::create(n, capacity, true, &err);
+      if (!r) throw std::runtime_error("shm fanout: " + err);
+      rings_.push_back(std::move(r));
+    }
+  }
+  bool push(const py::bytes& b, int timeout_ms) {
+    char* data = nullptr;
+    Py_ssize_t len = 0;
+    PyBytes_AsStringAndSize(b.ptr(), &data, &len);
+    py::gil_scoped_release nogil;
+    for (auto& r : rings_)
+      if (!(r->push(data, (uint32_t)len) || (timeout_ms > 0 && r->push_wait(data, (uint32_t)len, timeout_ms))))
+        return false;
+    return true;
+  }
+  void close() {
+    for (auto& r : rings_) r->close();
+  }
+
+ private:
+  std::vector<std::unique_ptr<ShmRing>> rings_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_dsse_runtime, m) {
@@ -319,6 +386,19 @@ PYBIND11_MODULE(_dsse_runtime, m) {
            py::arg("ttft"), py::arg("itl"), py::arg("host") = std::vector<double>{})
       .def("set_vocab", &DpWorkerPy::set_vocab);
   m.def("dp_ring_name", &dp_ring_name);
+
+  py::class_<ShmChannelPy>(m, "ShmChannel")
+      .def(py::init<const std::string&, bool, size_t, int>(), py::arg("name"), py::arg("create"),
+           py::arg("capacity") = 1 << 20, py::arg("open_timeout_ms") = 60000)
+      .def("push", &ShmChannelPy::push, py::arg("data"), py::arg("timeout_ms") = 5000)
+      .def("pop", &ShmChannelPy::pop, py::arg("timeout_ms") = 0, py::arg("spin_us") = 0)
+      .def("close", &ShmChannelPy::close)
+      .def("closed", &ShmChannelPy::closed)
+      .def_property_readonly("name", &ShmChannelPy::name);
+  py::class_<ShmFanoutPy>(m, "ShmFanout")
+      .def(py::init<const std::vector<std::string>&, size_t>(), py::arg("names"), py::arg("capacity") = 1 << 20)
+      .def("push", &ShmFanoutPy::push, py::arg("data"), py::arg("timeout_ms") = 5000)
+      .def("close", &ShmFanoutPy::close);
 
   m.def("encode_token_message", [](const std::string& cid, const std::string& tok, int64_t seq, bool done, int64_t ts) {
     return encode_token_message(TokenMessage{cid, tok, seq, done, ts});

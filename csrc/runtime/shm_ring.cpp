@@ -42,6 +42,10 @@ struct ShmRing::Header {
   std::atomic<uint32_t> space_seq;              // bumped on pop (producer futex)
   std::atomic<uint32_t> closed;
   std::atomic<uint32_t> ready;                  // set last by the creator
+  // sleepers on data_seq / space_seq: a push or pop only pays the futex_wake syscall when the other side is
+  // actually asleep (seq_cst on both sides: the sleeper registers, re-checks, sleeps; the waker bumps, then looks)
+  alignas(64) std::atomic<uint32_t> data_waiters;
+  std::atomic<uint32_t> space_waiters;
 };
 
 std::unique_ptr<ShmRing> ShmRing::create(const std::string& name, size_t capacity, bool replace, std::string* err) {
@@ -76,6 +80,8 @@ std::unique_ptr<ShmRing> ShmRing::create(const std::string& name, size_t capacit
   r->h_->data_seq.store(0);
   r->h_->space_seq.store(0);
   r->h_->closed.store(0);
+  r->h_->data_waiters.store(0);
+  r->h_->space_waiters.store(0);
   r->data_ = static_cast<uint8_t*>(p) + sizeof(Header);
   r->map_bytes_ = bytes;
   r->owner_ = true;
@@ -144,8 +150,8 @@ bool ShmRing::push(const void* data, uint32_t len) {
   std::memcpy(data_ + off, &len, 4);
   std::memcpy(data_ + off + 4, data, len);
   h_->head.store(head + need, std::memory_order_release);
-  h_->data_seq.fetch_add(1, std::memory_order_release);
-  futex_wake(&h_->data_seq);
+  h_->data_seq.fetch_add(1, std::memory_order_seq_cst);
+  if (h_->data_waiters.load(std::memory_order_seq_cst) != 0) futex_wake(&h_->data_seq);
   return true;
 }
 
@@ -157,7 +163,10 @@ bool ShmRing::push_wait(const void* data, uint32_t len, int timeout_ms) {
     if (closed()) return false;
     const int64_t left = t_end - mono_ms();
     if (left <= 0) return false;
-    futex_wait(&h_->space_seq, seq, (int)std::min<int64_t>(left, 50));
+    h_->space_waiters.fetch_add(1, std::memory_order_seq_cst);
+    if (h_->space_seq.load(std::memory_order_seq_cst) == seq)
+      futex_wait(&h_->space_seq, seq, (int)std::min<int64_t>(left, 50));
+    h_->space_waiters.fetch_sub(1, std::memory_order_seq_cst);
   }
 }
 
@@ -176,12 +185,20 @@ bool ShmRing::pop(std::string* out) {
   }
   out->assign(reinterpret_cast<const char*>(data_ + off + 4), len);
   h_->tail.store(tail + pad8(4 + (size_t)len), std::memory_order_release);
-  h_->space_seq.fetch_add(1, std::memory_order_release);
-  futex_wake(&h_->space_seq);
+  h_->space_seq.fetch_add(1, std::memory_order_seq_cst);
+  if (h_->space_waiters.load(std::memory_order_seq_cst) != 0) futex_wake(&h_->space_seq);
   return true;
 }
 
-bool ShmRing::pop_wait(std::string* out, int timeout_ms) {
+bool ShmRing::pop_wait(std::string* out, int timeout_ms, int spin_us) {
+  if (spin_us > 0) {  // a consumer expecting the next message within microseconds polls before it sleeps
+    const auto t_spin = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+    do {
+      if (pop(out)) return true;
+      if (closed()) return false;
+      __builtin_ia32_pause();
+    } while (std::chrono::steady_clock::now() < t_spin);
+  }
   const int64_t t_end = mono_ms() + timeout_ms;
   while (true) {
     const uint32_t seq = h_->data_seq.load(std::memory_order_acquire);
@@ -189,7 +206,10 @@ bool ShmRing::pop_wait(std::string* out, int timeout_ms) {
     if (closed()) return false;
     const int64_t left = t_end - mono_ms();
     if (left <= 0) return false;
-    futex_wait(&h_->data_seq, seq, (int)std::min<int64_t>(left, 50));
+    h_->data_waiters.fetch_add(1, std::memory_order_seq_cst);
+    if (h_->data_seq.load(std::memory_order_seq_cst) == seq)
+      futex_wait(&h_->data_seq, seq, (int)std::min<int64_t>(left, 50));
+    h_->data_waiters.fetch_sub(1, std::memory_order_seq_cst);
   }
 }
 

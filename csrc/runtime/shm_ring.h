@@ -30,7 +30,9 @@ class ShmRing {
   bool push_wait(const void* data, uint32_t len, int timeout_ms);
   // Consumer side.  pop() is non-blocking; pop_wait() sleeps until a message arrives or timeout.
   bool pop(std::string* out);
-  bool pop_wait(std::string* out, int timeout_ms);
+  // spin_us > 0: poll for that long before sleeping on the futex (a latency-critical consumer, e.g. a TP
+  // follower waiting for the leader's next step plan, skips the sleep/wake round trip).
+  bool pop_wait(std::string* out, int timeout_ms, int spin_us = 0);
 
   // Either side may close; the other side sees closed() (pending messages can still be popped).
   void close();

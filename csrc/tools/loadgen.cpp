@@ -10,6 +10,10 @@
 // RESP connection pool, per-token arrival records (-arrivals FILE: int32 stream, int32 sequence,
 // int64 recv_ns, int64 msg_timestamp_ns), and a JSON summary (-json) with latency and inter-token
 // percentiles.  Chat extras: -message, -max-tokens, -ignore-eos, -id-prefix.
+// Serving under continuous arrivals (tools/bench_serving.py): -rate R starts the chat streams as a Poisson
+// process of R requests/s (seeded by -seed) instead of all at once, and records each request's send time as an
+// arrival with sequence 0 (TTFT = first token - that); -long-every K -long-words W makes every K-th request a
+// W-word prompt (one synthetic token per word: an 8k-token prompt is -long-words 8000).
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -60,6 +64,10 @@ struct Args {
   int pool = 16;
   std::string arrivals;
   bool json = false;
+  double rate = 0;         // chat: Poisson request arrivals per second (0 = all at once)
+  int long_every = 0;      // chat: every K-th request gets the long prompt
+  int long_words = 0;
+  uint64_t seed = 42;
   int connect_batch = 512;  // connections started per thread per loop iteration
 };
 
@@ -161,8 +169,10 @@ struct Consumer {
 class ConsumerThread {
  public:
   ConsumerThread(const Args& a, const sockaddr_in& addr, const std::string& host, std::vector<std::string> ids,
-                 std::vector<int> idx, Stats* st, int64_t deadline_ns)
-      : a_(a), addr_(addr), host_(host), ids_(std::move(ids)), idx_(std::move(idx)), st_(st), deadline_(deadline_ns) {}
+                 std::vector<int> idx, Stats* st, int64_t deadline_ns, std::vector<int64_t> start_at = {},
+                 const std::string* long_msg = nullptr)
+      : a_(a), addr_(addr), host_(host), ids_(std::move(ids)), idx_(std::move(idx)), st_(st), deadline_(deadline_ns),
+        start_at_(std::move(start_at)), long_msg_(long_msg) {}
 
   void run() {
     ep_ = epoll_create1(EPOLL_CLOEXEC);
@@ -170,12 +180,15 @@ class ConsumerThread {
     size_t next = 0, live = 0;
     epoll_event evs[256];
     while (true) {
-      // open connections in batches so a 10k-connection run does not flood the listen backlog
+      // open connections in batches so a 10k-connection run does not flood the listen backlog; with -rate, each at
+      // its Poisson arrival time
+      const int64_t t_now = now_ns();
       for (int k = 0; k < a_.connect_batch && next < ids_.size(); ++k, ++next) {
+        if (!start_at_.empty() && start_at_[next] > t_now) break;
         if (start(next)) ++live;
       }
       if (live == 0 && next >= ids_.size()) break;
-      if (now_ns() > deadline_ + 5'000'000'000LL) break;
+      if (t_now > deadline_ + 5'000'000'000LL) break;
       int n = epoll_wait(ep_, evs, 256, next < ids_.size() ? 1 : 100);
       for (int i = 0; i < n; ++i) {
         Consumer& c = conns_[evs[i].data.u32];
@@ -208,7 +221,9 @@ class ConsumerThread {
     }
     const std::string& id = ids_[i];
     if (a_.chat) {
-      std::string body = "{\"message\":\"" + jesc(a_.message) + "\",\"conversation_id\":\"" + jesc(id) + "\"";
+      const bool is_long = long_msg_ && a_.long_every > 0 && c.idx % a_.long_every == a_.long_every - 1;
+      std::string body = "{\"message\":\"" + jesc(is_long ? *long_msg_ : a_.message) + "\",\"conversation_id\":\"" +
+                         jesc(id) + "\"";
       if (a_.max_tokens > 0) body += ",\"max_tokens\":" + std::to_string(a_.max_tokens);
       if (a_.ignore_eos) body += ",\"ignore_eos\":true";
       body += "}";
@@ -222,6 +237,7 @@ class ConsumerThread {
     ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
     ev.data.u32 = (uint32_t)i;
     epoll_ctl(ep_, EPOLL_CTL_ADD, c.fd, &ev);
+    if (!start_at_.empty()) c.local.push_back({c.idx, 0, now_ns(), 0});  // request sent (TTFT origin)
     return true;
   }
 
@@ -369,6 +385,8 @@ class ConsumerThread {
   std::vector<int> idx_;
   Stats* st_;
   int64_t deadline_;
+  std::vector<int64_t> start_at_;
+  const std::string* long_msg_;
   int ep_ = -1;
   std::vector<Consumer> conns_;
 };
@@ -501,7 +519,8 @@ void usage() {
   fprintf(stderr,
           "usage: dsse-loadgen [-mode producer|consumer|both] [-chat] [-redis host:port] [-sse http://host:port]\n"
           "  [-conversations N] [-tokens T] [-token-delay MS] [-duration 30s] [-threads T] [-pool P]\n"
-          "  [-message TEXT] [-max-tokens N] [-ignore-eos] [-id-prefix P] [-arrivals FILE] [-json]\n");
+          "  [-message TEXT] [-max-tokens N] [-ignore-eos] [-id-prefix P] [-arrivals FILE] [-json]\n"
+          "  [-rate REQ_PER_S] [-long-every K -long-words W] [-seed S]\n");
 }
 
 }  // namespace
@@ -535,6 +554,10 @@ int main(int argc, char** argv) {
     else if (k == "-pool") a.pool = std::max(1, std::atoi(val().c_str()));
     else if (k == "-arrivals") a.arrivals = val();
     else if (k == "-json") a.json = true;
+    else if (k == "-rate") a.rate = std::atof(val().c_str());
+    else if (k == "-long-every") a.long_every = std::atoi(val().c_str());
+    else if (k == "-long-words") a.long_words = std::atoi(val().c_str());
+    else if (k == "-seed") a.seed = (uint64_t)std::strtoull(val().c_str(), nullptr, 10);
     else if (k == "-h" || k == "-help") { usage(); return 0; }
     else { fprintf(stderr, "unknown flag %s\n", argv[i]); usage(); return 2; }
   }
@@ -562,15 +585,32 @@ int main(int argc, char** argv) {
   Stats st;
   std::vector<std::thread> threads;
   std::vector<std::unique_ptr<ConsumerThread>> cons;
+  // -rate: one global Poisson arrival process (exponential gaps), dealt round-robin to the threads in order
+  std::vector<int64_t> start_at;
+  if (a.chat && a.rate > 0) {
+    std::mt19937_64 rng(a.seed);
+    std::exponential_distribution<double> gap(a.rate);
+    double t = 0;
+    const int64_t t0 = now_ns() + 100'000'000LL;
+    for (int i = 0; i < a.conversations; ++i) {
+      start_at.push_back(t0 + (int64_t)(t * 1e9));
+      t += gap(rng);
+    }
+  }
+  std::string long_msg;
+  for (int i = 0; i < a.long_words; ++i) long_msg += (i ? " w" : "w") + std::to_string(i % 9973);
   if (consume) {
     for (int t = 0; t < a.threads; ++t) {
       std::vector<std::string> part;
       std::vector<int> idx;
+      std::vector<int64_t> at;
       for (int i = t; i < a.conversations; i += a.threads) {
         part.push_back(ids[(size_t)i]);
         idx.push_back(i);
+        if (!start_at.empty()) at.push_back(start_at[(size_t)i]);
       }
-      cons.emplace_back(new ConsumerThread(a, sse_addr, hp, part, idx, &st, deadline));
+      cons.emplace_back(new ConsumerThread(a, sse_addr, hp, part, idx, &st, deadline, at,
+                                           a.long_words > 0 ? &long_msg : nullptr));
     }
     for (auto& c : cons) threads.emplace_back([&c] { c->run(); });
     if (produce) std::this_thread::sleep_for(std::chrono::milliseconds(500));  // main.go:162
@@ -600,8 +640,10 @@ int main(int argc, char** argv) {
     return x.stream != y.stream ? x.stream < y.stream : x.recv_ns < y.recv_ns;
   });
   for (size_t i = 0; i < arr.size(); ++i) {
+    if (arr[i].seq == 0) continue;  // a request's send record (-rate)
     if (arr[i].ts_ns > 1'000'000'000'000'000LL) lat.push_back((double)(arr[i].recv_ns - arr[i].ts_ns) / 1e6);
-    if (i > 0 && arr[i].stream == arr[i - 1].stream) gaps.push_back((double)(arr[i].recv_ns - arr[i - 1].recv_ns) / 1e6);
+    if (i > 0 && arr[i].stream == arr[i - 1].stream && arr[i - 1].seq > 0)
+      gaps.push_back((double)(arr[i].recv_ns - arr[i - 1].recv_ns) / 1e6);
   }
   if (!a.arrivals.empty()) {
     FILE* f = std::fopen(a.arrivals.c_str(), "wb");

@@ -71,8 +71,7 @@ def _parallel(jobs, verbose):
 KERNEL_VARIANTS = {
     "checked": ["-DDSSE_KERNEL_CHECKS=1"],
     "noxcd": ["-DDSSE_XCD_SPLITK=0"],  # experiment build (split-K workgroups in plain dispatch order)
-    "pfnosm": ["-DDSSE_PREFILL_NOSOFTMAX=1"],
-    "pfregs": ["-DDSSE_PREFILL_GLDS=0"],  # experiment build: flash-prefill K/V staged through registers (round 1)  # timing experiment only: flash prefill without the softmax (wrong output)
+    "pfregs": ["-DDSSE_PREFILL_GLDS=0"],  # experiment build: flash-prefill K/V staged through registers (round 1)
     "wdef": ["-DDSSE_W_DEFAULT=1"],     # experiment build (default cache policy on gemm_stream weights)
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 

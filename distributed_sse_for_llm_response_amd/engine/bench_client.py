@@ -1,7 +1,8 @@
 """SSE client process for bench.py --delivery sse.
 
-Started BEFORE the parent touches the GPU (plain subprocess).  Reads one JSON config line from stdin
-({"host", "port", "streams", "message", "max_tokens", "prefix"}), opens `streams` concurrent POST /chat
+Started BEFORE the parent touches the GPU (plain subprocess).  Reads JSON config lines from stdin, one run each
+({"host", "port", "streams", "message", "max_tokens", "prefix"}, optional "rate" / "seed" / "long_every" /
+"long_words" for Poisson arrivals), opens `streams` POST /chat
 SSE streams and records the arrival time of every token event, then prints one JSON object
 {"arrivals": [[stream, sequence, recv_ns, msg_timestamp_ns], ...], "errors": [...]}.
 
@@ -39,6 +40,10 @@ def _native(cfg):
                "-message", cfg["message"], "-max-tokens", str(cfg["max_tokens"]), "-ignore-eos",
                "-id-prefix", cfg.get("prefix", "bench-"), "-duration", str(cfg.get("duration_s", 900)) + "s",
                "-threads", str(threads), "-arrivals", arr, "-json"]
+        if cfg.get("rate"):  # serving under continuous arrivals (tools/bench_serving.py): Poisson starts, send records
+            cmd += ["-rate", str(cfg["rate"]), "-seed", str(cfg.get("seed", 42))]
+        if cfg.get("long_every") and cfg.get("long_words"):
+            cmd += ["-long-every", str(cfg["long_every"]), "-long-words", str(cfg["long_words"])]
         out = subprocess.run(cmd, capture_output=True, text=True)
         summary = json.loads(out.stdout.strip().splitlines()[-1]) if out.stdout.strip() else {}
         rec = np.fromfile(arr, dtype=_REC) if os.path.exists(arr) else np.zeros(0, dtype=_REC)
@@ -68,15 +73,16 @@ async def _asyncio_main(cfg):
 
 
 def main():
-    line = sys.stdin.readline()
-    if not line.strip():
-        return 0
-    cfg = json.loads(line)
-    result = None if cfg.get("python_client") else _native(cfg)
-    if result is None:
-        result = asyncio.run(_asyncio_main(cfg))
-    sys.stdout.write(json.dumps(result) + "\n")
-    sys.stdout.flush()
+    # one JSON config line per run, until stdin closes (tools/bench_serving.py sends several rate points)
+    for line in sys.stdin:
+        if not line.strip():
+            break
+        cfg = json.loads(line)
+        result = None if cfg.get("python_client") else _native(cfg)
+        if result is None:
+            result = asyncio.run(_asyncio_main(cfg))
+        sys.stdout.write(json.dumps(result) + "\n")
+        sys.stdout.flush()
     return 0
 
 

@@ -231,7 +231,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
     from ..models.tokenizer import SyntheticTokenizer, prompt_for_request
     from .engine import LLMEngine, SamplingParams
 
-    from ..serving.tp import PlanChannel, TPLeader, follower_loop, make_tp_groups
+    from ..serving.tp import TPLeader, follower_loop, make_plan_channel, make_tp_groups
 
     device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
     if world % tp:
@@ -243,7 +243,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
 
         tp_group, plan_group, group, leader = make_tp_groups(world, tp, dist.get_backend())
         comm = TPComm(rank=rank - leader, size=tp, group=tp_group)
-        plan_ch = PlanChannel(plan_group, leader)
+        plan_ch = make_plan_channel(plan_group, leader, group, tp)
     # Admission prefills ~max_prefill_tokens of prompts per engine step while the already admitted streams
     # decode, so the first streams run ahead by up to `skew` steps.  Every stream must stay live through
     # the whole timed window (full batch on every timed step): budget the tokens and the KV for it.
@@ -291,6 +291,7 @@ def run_serving_bench(client, model="mistral-7b-v0.3", device=None, streams=64, 
                                         "streams": streams * replicas, "message": " ".join(words),
                                         "max_tokens": total + 2, "prefix": "bench-"}) + "\n")
         client.stdin.flush()
+        client.stdin.close()  # one run: the client exits after it
 
     def publish(events):
         if events:

@@ -8,7 +8,7 @@ Decode step for a batch bucket of B slots (all device-resident, no host round tr
       qkv GEMM           x·Wqkvᵀ as fp32 split-K slabs
       paged_attention    sums the slabs, RoPE, writes this token's K/V into the paged cache, then
                          flash-decoding over the pages (+ partition combine)
-      gemm_resid         resid += attn·Woᵀ          (TP>1: gemm_out + RCCL all-reduce + add)
+      gemm_resid         resid += attn·Woᵀ          (TP>1: gemm_out + one fused IPC all-reduce + add + norm kernel)
       rmsnorm            x = norm(resid)
       gemm_silu          h = silu(x·Wgᵀ)·(x·Wuᵀ)
       gemm_resid         resid += h·Wdᵀ             (TP>1: gemm_out + all-reduce + add)
@@ -131,6 +131,14 @@ class ModelRunner:
         ws = max(decode_partitioning(b, nkv, max_model_len)[1] * b for b in batch_buckets(Bm))
         self.part_o = torch.zeros(max(1, ws) * nkv * 16 * 128, device=dev, dtype=torch.float32)
         self.part_ml = torch.zeros(max(1, ws) * nkv * 16 * 2, device=dev, dtype=torch.float32)
+        # row-split RMSNorm rendezvous workspace (decode rows; ops.rmsnorm sync=): owned by this runner, whose
+        # launches are all on one stream
+        self.norm_sync = ops.norm_sync_workspace(Bm, dev) if dev.type == "cuda" else None
+        # TP decode: the residual all-reduces on the fused IPC kernel (parallel/comm.py IpcAllReduce), RCCL otherwise
+        self.fast_ar_reason = self.comm.enable_ipc_allreduce(dev, Bm, H) if self.comm.size > 1 else "tp=1"
+        if self.comm.size > 1 and self.comm.rank == 0:
+            print(f"[engine] TP={self.comm.size} decode all-reduce: "
+                  f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
         self.graphs = {}
         self.graph_pool = None
 
@@ -154,20 +162,18 @@ class ModelRunner:
             self._qkv_attention(li, L, B, x, part, nparts)
             if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
                 ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
-                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
+                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
             else:
                 ops.gemm_out(self.attn[r], L.wo_t, self.tmp[r])
-                comm.all_reduce(self.tmp[r])
-                ops.rmsnorm(resid, L.ffn_norm, x, eps, delta=self.tmp[r])
+                comm.all_reduce_rmsnorm(self.tmp[r], resid, L.ffn_norm, x, eps, sync=self.norm_sync)
             ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             if comm.size == 1:
                 ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
-                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
+                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
             else:
                 ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
-                comm.all_reduce(self.tmp[r])
-                ops.rmsnorm(resid, w_next, x, eps, delta=self.tmp[r])
+                comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps, sync=self.norm_sync)
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
@@ -216,11 +222,10 @@ class ModelRunner:
         eps = self.cfg.rms_eps
         if self.comm.size == 1:
             ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
-            ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns)
+            ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
         else:
             ops.gemm_out(a, wt, tmp)
-            self.comm.all_reduce(tmp)
-            ops.rmsnorm(resid, norm_w, x, eps, delta=tmp)
+            self.comm.all_reduce_rmsnorm(tmp, resid, norm_w, x, eps, sync=self.norm_sync)
 
     def _sample_commit(self, B: int) -> None:
         """Candidates per (row, vocab chunk) on each rank -> (TP: all-gather, 8 B per candidate) -> pick."""
@@ -317,8 +322,10 @@ class ModelRunner:
     def move_slots(self, src: list, dst: list) -> None:
         """Slot compaction: decode state (last token, position) of slot src[i] -> dst[i], gathered before it
         is scattered so swaps work; stream-ordered after every decode step already enqueued."""
-        si = torch.tensor(src, dtype=torch.long).to(self.device)
-        di = torch.tensor(dst, dtype=torch.long).to(self.device)
+        idx = torch.tensor([src, dst], dtype=torch.long)
+        if self.device.type == "cuda":  # pinned + non_blocking: no host wait for the decode steps already queued
+            idx = idx.pin_memory().to(self.device, non_blocking=True)
+        si, di = idx[0], idx[1]
         for t in (self.ids, self.positions):
             t.index_copy_(0, di, t.index_select(0, si))
 

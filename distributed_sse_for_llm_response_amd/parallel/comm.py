@@ -7,6 +7,12 @@ the vocab-sized logits).  All of them are issued on torch's current stream, so t
 into the decode hipGraph together with the kernels.
 
 The same code runs on CPU tensors with the ``gloo`` backend for the multi-process tests.
+
+Decode all-reduces on GPUs go through ``IpcAllReduce`` when it is available: one hand-written kernel per
+all-reduce (``csrc/kernels/allreduce.hip``) that exchanges the rows of the O / down partial products through
+IPC-mapped peer buffers over xGMI and folds the residual add + RMSNorm in.  It is set up once per TP group
+(handles exchanged over the group, a self-test against ``dist.all_reduce`` decided by all ranks together) and
+RCCL stays the fallback (``DSSE_CUSTOM_AR=0`` forces it).
 """
 from __future__ import annotations
 
@@ -59,6 +65,126 @@ class TPComm:
     def barrier(self) -> None:
         if self.size > 1:
             dist.barrier(group=self.group)
+
+    # ---- fused all-reduce + residual + RMSNorm (decode) ------------------------------------------------------
+    fast_ar: object = None  # IpcAllReduce once enable_ipc_allreduce succeeded on every rank
+
+    def enable_ipc_allreduce(self, device, rows: int, hidden: int) -> str:
+        """Set up the IPC all-reduce for up to `rows` rows of width `hidden` (collective over the TP group).
+        Returns "" when enabled, else the reason RCCL stays in use (identical on every rank)."""
+        if self.size <= 1:
+            return "tp=1"
+        why = ""
+        if os.environ.get("DSSE_CUSTOM_AR", "1") == "0":
+            why = "DSSE_CUSTOM_AR=0"
+        elif torch.device(device).type != "cuda":
+            why = "not on a GPU"
+        elif self.size > IpcAllReduce.MAX_RANKS:
+            why = f"more than {IpcAllReduce.MAX_RANKS} ranks"
+        # every rank takes the same branch: the reasons above depend only on the environment and the TP size
+        if why:
+            return why
+        ar, why = IpcAllReduce.create(self, torch.device(device), rows, hidden)
+        self.fast_ar = ar
+        return why
+
+    def all_reduce_rmsnorm(self, tmp, resid, norm_w, y, eps: float, sync=None) -> None:
+        """resid += all_reduce(tmp); y = rmsnorm(resid) * norm_w (the TP decode residual step)."""
+        from .. import ops
+
+        if self.fast_ar is not None and tmp.shape[0] <= self.fast_ar.rows:
+            self.fast_ar(tmp, resid, norm_w, y, eps)
+            return
+        self.all_reduce(tmp)
+        ops.rmsnorm(resid, norm_w, y, eps, delta=tmp, sync=sync)
+
+
+class IpcAllReduce:
+    """Per-rank context of the fused IPC all-reduce (allreduce.hip ar_rmsnorm_kernel).
+
+    Every rank allocates one buffer (flags + two parities of [rows, H] bf16), exports its IPC handle, and opens
+    the handles of the other ranks of its TP group; ``peers`` holds the T buffer pointers as this process sees
+    them.  ``epoch`` counts calls per row (the kernel's flag values) and must advance identically on every rank,
+    which it does because every rank runs the same decode steps.  ``err`` is set by a timed-out peer wait."""
+
+    MAX_RANKS = 8
+
+    def __init__(self, comm, device, rows, hidden, own_ptr, peer_ptrs, uncached):
+        self.comm, self.device, self.rows, self.hidden = comm, device, rows, hidden
+        self.own_ptr, self.peer_ptrs, self.uncached = own_ptr, peer_ptrs, uncached
+        self.peers = torch.tensor(peer_ptrs, dtype=torch.int64, device=device)
+        self.epoch = torch.zeros(rows, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+
+    @classmethod
+    def create(cls, comm, device, rows: int, hidden: int):
+        """(context or None, reason).  Collective: handle exchange + self-test + a MIN vote over the group."""
+        from .. import ops
+
+        ok, why, ctx = True, "", None
+        try:
+            ops.load_library(required=True)
+            handle, ptr, uncached = torch.ops.dsse.ar_alloc(rows, hidden)
+            payload = [bytes(handle.tolist())]
+        except Exception as e:  # noqa: BLE001 - the vote below makes every rank fall back together
+            ok, why, payload, ptr, uncached = False, f"alloc: {type(e).__name__}: {e}", [b""], 0, 0
+        handles = [None] * comm.size
+        dist.all_gather_object(handles, payload[0], group=comm.group)
+        if ok and all(handles):
+            try:
+                ptrs = []
+                for q, h in enumerate(handles):
+                    if q == comm.rank:
+                        ptrs.append(ptr)
+                    else:
+                        ptrs.append(int(torch.ops.dsse.ar_open(torch.tensor(list(h), dtype=torch.uint8))))
+                ctx = cls(comm, device, rows, hidden, ptr, ptrs, bool(uncached))
+            except Exception as e:  # noqa: BLE001
+                ok, why = False, f"open: {type(e).__name__}: {e}"
+        elif ok:
+            ok, why = False, "a peer could not allocate its buffer"
+        if ok:
+            why = ctx.self_test()
+            ok = not why
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        if dist.get_backend(comm.group) == "gloo":
+            flag = flag.cpu()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
+        if int(flag.item()) == 0:
+            return None, why or "another rank of the TP group failed the IPC all-reduce self-test"
+        return ctx, ""
+
+    def __call__(self, tmp, resid, norm_w, y, eps: float) -> None:
+        torch.ops.dsse.ar_rmsnorm(tmp, resid, norm_w, y, eps, self.peers, self.comm.rank, self.rows, self.epoch,
+                                  self.err)
+
+    def self_test(self) -> str:
+        """Fused all-reduce of random partials vs RCCL/gloo sum + reference norm, at a few row counts; ""=ok."""
+        from ..ops import reference as R
+
+        gen = torch.Generator().manual_seed(1234 + self.comm.rank)
+        H = self.hidden
+        for M in sorted({1, min(7, self.rows), self.rows}):
+            for _ in range(3):  # both buffer parities, twice
+                tmp = (torch.randn(M, H, generator=gen) * 0.5).bfloat16().to(self.device)
+                resid0 = torch.randn(M, H, generator=torch.Generator().manual_seed(M)).to(self.device)
+                w = (1 + 0.1 * torch.randn(H, generator=torch.Generator().manual_seed(7))).bfloat16().to(self.device)
+                r = resid0.clone()
+                y = torch.zeros(M, H, dtype=torch.bfloat16, device=self.device)
+                self(tmp, r, w, y, 1e-5)
+                ref = tmp.float().clone()
+                self.comm.all_reduce(ref)
+                r_ref = resid0.cpu() + ref.cpu()
+                y_ref = torch.zeros(M, H, dtype=torch.bfloat16)
+                R.rmsnorm(r_ref.clone(), w.cpu(), y_ref, 1e-5)
+                torch.cuda.synchronize(self.device)
+                if int(self.err.item()) != 0:
+                    return "self-test: a peer wait timed out"
+                err_r = float((r.cpu() - r_ref).abs().max())
+                err_y = float((y.cpu().float() - y_ref.float()).abs().max())
+                if err_r > 1e-3 or err_y > 5e-2:
+                    return f"self-test: M={M} max |resid err| {err_r:.3g}, |y err| {err_y:.3g}"
+        return ""
 
 
 def env_rank_info():

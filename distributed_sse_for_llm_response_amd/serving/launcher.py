@@ -22,13 +22,13 @@ from ..parallel.comm import TPComm, init_distributed
 from .app import EngineLoop, ServingApp, build_engine
 from .config import ServeConfig
 from .faults import Watchdog
-from .tp import PlanChannel, TPLeader, follower_loop, make_tp_groups
+from .tp import TPLeader, follower_loop, make_plan_channel, make_tp_groups
 
 
 class TPLeaderLoop(EngineLoop):
     """The first rank of a TP group: the normal engine loop, every step preceded by a plan broadcast."""
 
-    def __init__(self, runtime, engine, tokenizer, cfg, channel: PlanChannel):
+    def __init__(self, runtime, engine, tokenizer, cfg, channel):
         super().__init__(runtime, engine, tokenizer, cfg)
         self.drv = TPLeader(engine, channel)
 
@@ -75,7 +75,7 @@ def serve_tp(cfg: ServeConfig, rank: int, local: int, world: int, tp: int, devic
     backend = dist.get_backend()
     tp_group, plan_group, g, leader = make_tp_groups(world, tp, backend)
     comm = TPComm(rank=rank - leader, size=tp, group=tp_group)
-    channel = PlanChannel(plan_group, leader)
+    channel = make_plan_channel(plan_group, leader, g, tp)
     dp = world // tp
     if rank != leader:
         engine, _ = build_engine(cfg, device=device, comm=comm)

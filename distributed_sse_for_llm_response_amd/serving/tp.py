@@ -9,16 +9,21 @@ the followers, which apply it to their own engine and step too.  Every schedulin
 from identical inputs on every rank: the engine runs with ``deterministic=True`` (drained steps are
 consumed by count, never by whether an event happens to have completed on this rank).
 
-The plan is a fixed-size int32 message broadcast over a CPU (gloo) group of the TP ranks -- no pickling,
-no GPU sync -- split over several broadcasts when a step admits more prompt tokens than one holds.
-Followers know sequences by the leader's request id (``Sequence.rid``, which also seeds their sampling),
-so no conversation-id strings cross ranks.
+The plan is a small int32 message (a 6-word header plus only the words the step needs -- an empty step is 24
+bytes).  Between ranks of one node it travels through POSIX shared-memory rings (``ShmPlanChannel``: one SPSC
+ring per follower, the follower polls for 2 ms -- longer than a TP decode step -- before it sleeps, so the per-step host cost is a few
+microseconds -- ``tools/bench_plan_channel.py``, ``profiles/r3/plan_channel.md``); ``GlooPlanChannel`` (header
+broadcast, then the payload only when there is one) is the fallback when the ranks do not share a node.  The
+leader applies the DECODED plan, exactly what the followers apply, so every rank admits the same parameters
+(seed, float32 temperature / top-p).  Followers know sequences by the leader's request id (``Sequence.rid``,
+which also seeds their sampling), so no conversation-id strings cross ranks.
 
 Reference: the reference configures TP only as a vLLM flag (kubernetes/base/llm/deployment.yaml:88-89).
 """
 from __future__ import annotations
 
 import struct
+from array import array
 from dataclasses import dataclass, field
 
 import torch
@@ -54,8 +59,15 @@ class Plan:
     def encode(self) -> list:
         w = []
         for rid, prompt, p, arrival in self.adds:
-            seed = -1 if p.seed is None else int(p.seed) & 0x7FFFFFFF
-            w += [rid, arrival & 0x7FFFFFFF, (arrival >> 31) & 0x7FFFFFFF, int(p.max_tokens), int(p.top_k), seed,
+            # seeds travel whole: two 31-bit words (the server accepts seeds up to 2^53 - 1); -1 = no seed
+            if p.seed is None:
+                s_lo, s_hi = -1, -1
+            else:
+                sd = int(p.seed)
+                if not 0 <= sd < (1 << 62):
+                    raise ValueError(f"TP plan: seed {sd} outside [0, 2^62)")
+                s_lo, s_hi = sd & 0x7FFFFFFF, (sd >> 31) & 0x7FFFFFFF
+            w += [rid, arrival & 0x7FFFFFFF, (arrival >> 31) & 0x7FFFFFFF, int(p.max_tokens), int(p.top_k), s_lo, s_hi,
                   int(bool(p.ignore_eos)), _f2i(p.temperature), _f2i(p.top_p), len(prompt)]
             w += [int(t) for t in prompt]
         for rid in self.aborts:
@@ -69,12 +81,12 @@ class Plan:
         p = Plan(step=bool(flags & F_STEP), stop=bool(flags & F_STOP), sync=bool(flags & F_SYNC))
         o = 0
         for _ in range(n_add):
-            rid, a_lo, a_hi, mt, tk, seed, ie, temp, top_p, n = w[o:o + 10]
-            o += 10
+            rid, a_lo, a_hi, mt, tk, s_lo, s_hi, ie, temp, top_p, n = w[o:o + 11]
+            o += 11
             prompt = w[o:o + n]
             o += n
             sp = SamplingParams(temperature=_i2f(temp), top_p=_i2f(top_p), top_k=tk, max_tokens=mt,
-                                seed=None if seed < 0 else seed, ignore_eos=bool(ie))
+                                seed=None if s_lo < 0 else s_lo | (s_hi << 31), ignore_eos=bool(ie))
             p.adds.append((rid, prompt, sp, a_lo | (a_hi << 31)))
         for _ in range(n_abort):
             p.aborts.append(w[o])
@@ -84,40 +96,144 @@ class Plan:
             o += 2
         return p
 
+    def flags(self) -> int:
+        return (F_STEP if self.step else 0) | (F_STOP if self.stop else 0) | (F_SYNC if self.sync else 0)
 
-class PlanChannel:
-    """Leader -> followers plan broadcast over a gloo group of one TP group (``src`` = leader's global rank)."""
+    def roundtrip(self) -> "Plan":
+        """The plan exactly as a follower decodes it (the leader applies this, so every rank agrees bit for bit)."""
+        if not (self.adds or self.aborts or self.flow):
+            return self
+        return Plan.decode(self.flags(), len(self.adds), len(self.aborts), len(self.flow), self.encode())
 
-    HEADER = 6  # magic, flags, n_add, n_abort, n_flow, payload words in this message
 
-    def __init__(self, group, src: int, capacity: int = 1 << 16):
-        self.group, self.src, self.cap = group, src, capacity
-        self.buf = torch.zeros(capacity, dtype=torch.int32)
+def _messages(plan: Plan, room: int):
+    """The plan's wire messages: [header(6) + payload chunk] int32 arrays, F_MORE on all but the last."""
+    words = plan.encode()
+    chunks = [words[i:i + room] for i in range(0, len(words), room)] or [[]]
+    out = []
+    for k, chunk in enumerate(chunks):
+        flags = plan.flags() | (0 if k == len(chunks) - 1 else F_MORE)
+        out.append(array("i", [MAGIC, flags, len(plan.adds), len(plan.aborts), len(plan.flow), len(chunk)] + chunk))
+    return out
+
+
+class _Reassembly:
+    def __init__(self):
+        self.words = []
+
+    def feed(self, msg) -> "Plan | None":
+        magic, flags, n_add, n_abort, n_flow, n = msg[:6]
+        if magic != MAGIC:
+            raise RuntimeError(f"TP plan channel: bad message (magic {magic:#x})")
+        self.words += list(msg[6:6 + n])
+        if flags & F_MORE:
+            return None
+        words, self.words = self.words, []
+        return Plan.decode(flags, n_add, n_abort, n_flow, words)
+
+
+class ShmPlanChannel:
+    """Leader -> followers plans through one shared-memory SPSC ring per follower (same node).
+
+    The leader creates the rings (``/dsse-tp-<pid>-<group>-<k>``) and sends their prefix over the gloo plan group
+    once; a follower polls its ring for ``spin_us`` before it sleeps on the ring's futex, so a step plan arriving
+    right after the previous step is picked up without a wake-up syscall."""
+
+    ROOM = 1 << 18  # payload words per message (1 MiB: a ring holds at least two)
+
+    def __init__(self, group, src: int, rank: int, group_ranks: list, tag: str = "", spin_us: int | None = None):
+        import os
+
+        from .. import runtime
+
+        self.src, self.rank = src, rank
+        self.spin_us = int(os.environ.get("DSSE_TP_PLAN_SPIN_US", "2000")) if spin_us is None else spin_us
+        rt = runtime.load()
+        obj = [None]
+        if rank == src:
+            prefix = f"/dsse-tp-{os.getpid()}-{tag or src}"
+            self.out = rt.ShmFanout([f"{prefix}-{k}" for k in range(1, len(group_ranks))], 4 << 20)
+            obj[0] = prefix
+        dist.broadcast_object_list(obj, src=src, group=group)
+        if rank != src:
+            k = group_ranks.index(rank)
+            self.inp = rt.ShmChannel(f"{obj[0]}-{k}", False, 0, 60000)
+        dist.barrier(group=group)  # every follower attached before the leader may close anything
+        self._re = _Reassembly()
+        self._hdr = {}
 
     def send(self, plan: Plan) -> None:
-        words = plan.encode()
-        room = self.cap - self.HEADER
-        chunks = [words[i:i + room] for i in range(0, len(words), room)] or [[]]
-        for k, chunk in enumerate(chunks):
-            last = k == len(chunks) - 1
-            flags = ((F_STEP if plan.step else 0) | (F_STOP if plan.stop else 0) | (F_SYNC if plan.sync else 0) |
-                     (0 if last else F_MORE))
-            self.buf[: self.HEADER] = torch.tensor([MAGIC, flags, len(plan.adds), len(plan.aborts), len(plan.flow),
-                                                    len(chunk)], dtype=torch.int32)
-            if chunk:
-                self.buf[self.HEADER:self.HEADER + len(chunk)] = torch.tensor(chunk, dtype=torch.int32)
-            dist.broadcast(self.buf, src=self.src, group=self.group)
+        if plan.empty() or not (plan.adds or plan.aborts or plan.flow):  # the steady decode step: cached bytes
+            b = self._hdr.get(plan.flags())
+            if b is None:
+                b = self._hdr[plan.flags()] = _messages(plan, self.ROOM)[0].tobytes()
+            msgs = (b,)
+        else:
+            msgs = [m.tobytes() for m in _messages(plan, self.ROOM)]
+        for b in msgs:
+            if not self.out.push(b, 60000):
+                raise RuntimeError("TP plan channel: follower ring full or closed")
 
     def recv(self) -> Plan:
-        words = []
         while True:
-            dist.broadcast(self.buf, src=self.src, group=self.group)
-            magic, flags, n_add, n_abort, n_flow, n = self.buf[: self.HEADER].tolist()
-            if magic != MAGIC:
-                raise RuntimeError(f"TP plan channel: bad message (magic {magic:#x})")
-            words += self.buf[self.HEADER:self.HEADER + n].tolist()
-            if not flags & F_MORE:
-                return Plan.decode(flags, n_add, n_abort, n_flow, words)
+            b = self.inp.pop(60000, self.spin_us)
+            if b is None:
+                if self.inp.closed():
+                    raise RuntimeError("TP plan channel closed by the leader")
+                continue
+            plan = self._re.feed(array("i", b))
+            if plan is not None:
+                return plan
+
+
+class GlooPlanChannel:
+    """Leader -> followers plans over a gloo group (ranks on different nodes): a 6-word header broadcast, then the
+    payload words only when the message has any (an empty step plan is one 24-byte broadcast)."""
+
+    HEADER = 6
+    ROOM = 1 << 16
+
+    def __init__(self, group, src: int):
+        self.group, self.src = group, src
+        self.hdr = torch.zeros(self.HEADER, dtype=torch.int32)
+        self._re = _Reassembly()
+
+    def send(self, plan: Plan) -> None:
+        for msg in _messages(plan, self.ROOM):
+            t = torch.frombuffer(bytearray(msg.tobytes()), dtype=torch.int32)
+            self.hdr.copy_(t[: self.HEADER])
+            dist.broadcast(self.hdr, src=self.src, group=self.group)
+            if len(msg) > self.HEADER:
+                dist.broadcast(t[self.HEADER:].clone(), src=self.src, group=self.group)
+
+    def recv(self) -> Plan:
+        while True:
+            dist.broadcast(self.hdr, src=self.src, group=self.group)
+            hdr = self.hdr.tolist()
+            payload = []
+            if hdr[5] > 0:
+                buf = torch.zeros(hdr[5], dtype=torch.int32)
+                dist.broadcast(buf, src=self.src, group=self.group)
+                payload = buf.tolist()
+            plan = self._re.feed(hdr + payload)
+            if plan is not None:
+                return plan
+
+
+def make_plan_channel(plan_group, leader: int, group_index: int, tp: int):
+    """Shared-memory plan rings when the TP group is on this node (always, for the single-node launcher), gloo
+    otherwise (``DSSE_TP_PLAN=gloo`` forces it)."""
+    import os
+
+    rank = dist.get_rank()
+    ranks = list(range(leader, leader + tp))
+    if os.environ.get("DSSE_TP_PLAN", "shm") != "gloo":
+        return ShmPlanChannel(plan_group, leader, rank, ranks, tag=f"{os.environ.get('MASTER_PORT', '0')}-{group_index}")
+    return GlooPlanChannel(plan_group, leader)
+
+
+class PlanChannel(GlooPlanChannel):
+    """Backwards-compatible name of the gloo channel."""
 
 
 def follower_conv(rid: int) -> str:
@@ -137,7 +253,7 @@ def apply_plan(engine, plan: Plan, conv_of=follower_conv) -> None:
 class TPLeader:
     """The leader's side: collects the step's inputs, broadcasts them, applies them locally and steps."""
 
-    def __init__(self, engine, channel: PlanChannel | None):
+    def __init__(self, engine, channel):
         self.engine, self.ch = engine, channel
         self.plan = Plan()
         self._conv = {}   # rid -> conversation id (leader's real ids)
@@ -164,7 +280,7 @@ class TPLeader:
         plan.step = run
         if self.ch is not None:
             self.ch.send(plan)
-        apply_plan(self.engine, plan, self._conv.__getitem__)
+        apply_plan(self.engine, plan.roundtrip(), self._conv.__getitem__)
         events = self.engine.step() if run else []
         for e in events:  # forget finished conversations
             if e.done:
@@ -183,7 +299,7 @@ class TPLeader:
             self.ch.send(Plan(stop=True))
 
 
-def follower_loop(engine, channel: PlanChannel, on_sync=None) -> None:
+def follower_loop(engine, channel, on_sync=None) -> None:
     """A follower rank: mirror the leader's plans until it sends stop."""
     while True:
         plan = channel.recv()

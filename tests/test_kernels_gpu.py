@@ -110,6 +110,33 @@ def test_gemm_resid_split_then_fused_norm(gpu, M, K):
     _close(y, yr, 2e-2, 1e-2, "y")
 
 
+@pytest.mark.parametrize("nw,S", [(8, 8), (6, 4), (5, 4), (4, 16), (8, 4)])
+@pytest.mark.parametrize("M,K", [(64, 4096), (33, 14336), (64, 14336)])
+def test_resid_split_ring_shapes(gpu, monkeypatch, nw, S, M, K):
+    """O / down projection on the ring with DSSE_RESID_NW / DSSE_RESID_SPLIT (wider workgroups, deeper K split):
+    the slabs reduced by the norm equal resid += x·wᵀ followed by the norm."""
+    N = {5: 5120, 6: 3072}.get(nw, 4096)  # N / 16 tiles divisible by nw; N a multiple of 1024 for the norm
+    monkeypatch.setenv("DSSE_RESID_NW", str(nw))
+    monkeypatch.setenv("DSSE_RESID_SPLIT", str(S))
+    ops.refresh_env()
+    g = torch.Generator().manual_seed(nw * 1000 + S * 10 + M + K)
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
+    nwt = (1 + 0.1 * torch.randn(N, generator=g)).bfloat16()
+    r0 = torch.randn(M, N, generator=g)
+    r = r0.clone().to(gpu)
+    part = torch.zeros(32 * 64 * N, device=gpu)
+    y = torch.zeros(M, N, device=gpu, dtype=torch.bfloat16)
+    ns = ops.gemm_resid_split(x, w, r, part)
+    assert ns == S
+    ops.rmsnorm(r, nwt.to(gpu), y, 1e-5, part=part, nsplit=ns, sync=ops.norm_sync_workspace(64, gpu))
+    yr = torch.zeros(M, N, dtype=torch.bfloat16)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    R.rmsnorm(r0, nwt, yr, 1e-5)
+    _close(r, r0, 1e-3, 1e-3, "resid")
+    _close(y, yr, 2e-2, 1e-2, "y")
+
+
 @pytest.mark.parametrize("M", [1, 20, 64, 150])
 def test_gemm_silu(gpu, tiles, M):
     g = torch.Generator().manual_seed(M + 100)
@@ -233,6 +260,45 @@ def test_rmsnorm(gpu, mode, M, H):
     R.rmsnorm(resid0, w, yr, 1e-5, delta, embed, ids)
     _close(r_gpu, resid0, 1e-5, 1e-5, "resid")
     _close(y, yr, 2e-2, 1e-2, "y")
+
+
+def test_rmsnorm_row_split_rendezvous(gpu):
+    """Row-split RMSNorm (4 workgroups per row exchanging {ss, tag} granules): 60 back-to-back launches on ONE
+    sync workspace with varying row counts, modes 0 / 1 / 3 and slab counts, every call against the fp32
+    reference -- a granule of a previous call read as current would show as a wrong norm of that row."""
+    g = torch.Generator().manual_seed(11)
+    H, cap = 4096, 256
+    sync = ops.norm_sync_workspace(cap, gpu)
+    w = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16()
+    wg = w.to(gpu)
+    part = torch.zeros(4 * cap * H, device=gpu)
+    for it in range(60):
+        M = [64, 1, 256, 37, 128, 200][it % 6]
+        mode = [3, 0, 1][it % 3]
+        resid0 = torch.randn(M, H, generator=g) * (1 + it % 5)
+        r_gpu = resid0.clone().to(gpu)
+        y = torch.zeros(M, H, device=gpu, dtype=torch.bfloat16)
+        yr = torch.zeros(M, H, dtype=torch.bfloat16)
+        if mode == 3:
+            ns = 1 + it % 4
+            slabs = torch.randn(ns, M, H, generator=g)
+            part[: ns * M * H] = slabs.reshape(-1).to(gpu)
+            ops.rmsnorm(r_gpu, wg, y, 1e-5, part=part, nsplit=ns, sync=sync)
+            resid0 += slabs.sum(0)
+            R.rmsnorm(resid0, w, yr, 1e-5)
+        elif mode == 1:
+            delta = torch.randn(M, H, generator=g).bfloat16()
+            ops.rmsnorm(r_gpu, wg, y, 1e-5, delta=delta.to(gpu), sync=sync)
+            R.rmsnorm(resid0, w, yr, 1e-5, delta)
+        else:
+            ops.rmsnorm(r_gpu, wg, y, 1e-5, sync=sync)
+            R.rmsnorm(resid0, w, yr, 1e-5)
+        _close(r_gpu, resid0, 1e-4, 1e-5, f"resid it={it} M={M} mode={mode}")
+        _close(y, yr, 2e-2, 1e-2, f"y it={it} M={M} mode={mode}")
+    # each row's generation advanced once per call that covered it (quarter 0 bumps it after the rendezvous)
+    gen = sync[8 * cap:].cpu()
+    calls = [sum(1 for it in range(60) if [64, 1, 256, 37, 128, 200][it % 6] > m) for m in range(cap)]
+    assert gen.tolist() == calls
 
 
 def test_rope_kv_write_and_silu_mul(gpu):

@@ -1,6 +1,7 @@
 """Whole-model numerics at the real Mistral-7B dimensions (H 4096, F 14336, 32 / 8 heads, vocab 32768; two
 layers to keep the fp32 oracle fast): the full fp32 logits of the graph-captured decode step, at every decode
-path the engine picks by batch bucket (skinny 1, X-streaming 64, wide 128, hipBLASLt + wide 192 / 256), after
+path the engine picks by batch bucket (register-streaming skinny at 1, LDS-DMA ring at 64 and 128, the wide-bucket
+projections at 192 / 256 -- no library GEMM anywhere), after
 plain and chunked prefill, against ``models/mistral.py:reference_forward`` of the same weights.
 
 The criterion is on whole logits rows (cosine similarity and max-abs error relative to the row's scale), not on

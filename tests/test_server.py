@@ -585,3 +585,70 @@ def test_inspection_endpoint_failure_fails_open_and_async_uses_it():
     finally:
         r.stop()
         insp.close()
+
+
+def test_redelivered_first_token_after_done_is_a_duplicate(bare_rt):
+    """a redelivered seq-1 frame of a finished stream (its old timestamp, inside the dedupe window) must
+    not reopen the conversation: it is dropped and the replay ring survives for Last-Event-ID reconnects."""
+    conv = "redeliver-1"
+    c = RespClient(H, bare_rt.bound_port("resp"))
+    ts0 = time.time_ns()
+    msgs = [(1, "a", False, ts0), (2, "b", False, ts0 + 1), (3, "[DONE]", True, ts0 + 2)]
+    for seq, tok, done, ts in msgs + [(1, "a", False, ts0)]:  # the last one is an at-least-once redelivery
+        c.cmd("PUBLISH", f"llm:tokens:{conv}", json.dumps({"conversation_id": conv, "token": tok, "sequence": seq,
+                                                           "done": done, "timestamp": ts}))
+    c.close()
+    time.sleep(0.1)
+    resp = request(H, bare_rt.bound_port("edge"), "GET", f"/stream/{conv}", headers={"Last-Event-ID": "1"}, timeout=5)
+    assert [(t["token"], t["sequence"]) for t in tokens_of(resp)] == [("b", 2), ("[DONE]", 3)]
+    assert bare_rt.last_sequence(conv) == 3
+
+
+def test_black_holed_inspection_endpoint_fails_open_quickly():
+    """an INSPECTION_ENDPOINT that accepts TCP but never answers must not stall every token for the
+    timeout: the first failure opens the circuit and the stream is delivered (uninspected) at once."""
+    hole = socket.socket()
+    hole.bind((H, 0))
+    hole.listen(1)  # the kernel completes the handshake; nobody ever reads or answers
+    r = make_rt(inspection_mode="inline", inspection_endpoint=f"http://{H}:{hole.getsockname()[1]}/inspect",
+                inspection_timeout_ms=300)
+    try:
+        th, got = _stream_in_thread(r, "hole")
+        t0 = time.monotonic()
+        for i in range(40):
+            r.publish("hole", f"t{i}", i + 1, False, 0)
+        r.publish("hole", "[DONE]", 41, True, 0)
+        th.join(10)
+        assert [t["token"] for t in tokens_of(got[0])] == [f"t{i}" for i in range(40)] + ["[DONE]"]
+        assert time.monotonic() - t0 < 3.0  # 40 tokens x 2 attempts x 300 ms without the circuit breaker
+    finally:
+        r.stop()
+        hole.close()
+
+
+@pytest.mark.parametrize("role", ["edge", "origin"])
+@pytest.mark.parametrize("body, err", [
+    ({"max_tokens": 1e20}, b"max_tokens must be an integer in [1, 1048576]\n"),
+    ({"max_tokens": 0}, b"max_tokens must be an integer in [1, 1048576]\n"),
+    ({"top_k": 2.5}, b"top_k must be an integer in [-1, 1048576]\n"),
+    ({"seed": -5}, b"seed must be an integer in [0, 9007199254740991]\n"),
+    ({"seed": 2 ** 60}, b"seed must be an integer in [0, 9007199254740991]\n"),
+    (b'{"message":"hi","temperature":1e400}', b"temperature and top_p must be finite\n"),
+])
+def test_chat_rejects_bad_sampling_fields(bare_rt, role, body, err):
+    """/chat's optional integer fields are range- and integrality-checked before any cast (a
+    400 before the SSE response starts), on the edge and on the origin API alike."""
+    bare_rt.set_local_engine(True)
+    raw = body if isinstance(body, bytes) else json.dumps({"message": "hi", **body}).encode()
+    r = request(H, bare_rt.bound_port(role), "POST", "/chat", raw)
+    assert r.status == 400 and r.body == err
+    assert bare_rt.poll_requests(10, 0) == []
+
+
+def test_chat_accepts_valid_sampling_fields(bare_rt):
+    bare_rt.set_local_engine(True)
+    r = request(H, bare_rt.bound_port("origin"), "POST", "/chat",
+                {"message": "hi", "max_tokens": 7, "top_k": 3, "seed": 2 ** 40, "temperature": 0.5, "top_p": 0.9})
+    assert r.status == 200
+    (q,) = bare_rt.poll_requests(10, 0)
+    assert (q["max_tokens"], q["top_k"], q["seed"]) == (7, 3, 2 ** 40)

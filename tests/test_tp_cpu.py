@@ -208,6 +208,7 @@ REQS = [{"message": "same prompt", "conversation_id": "g0"},
         {"message": "a different prompt here", "conversation_id": "g1"},
         {"message": "sampled one", "conversation_id": "s0", "temperature": 1.0, "seed": 7},
         {"message": "sampled two", "conversation_id": "s1", "temperature": 0.8, "seed": 11},  # unfiltered: TP-invariant
+        {"message": "sampled three", "conversation_id": "s2", "temperature": 1.0, "seed": 2 ** 40 + 3},  # > 31 bits
         {"message": "same prompt", "conversation_id": "g2"}]
 
 

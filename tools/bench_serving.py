@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Serving under continuous arrivals: TTFT and in-flight inter-token latency while new prompts are prefilled.
+
+The steady-state bench (bench.py) times decode once every stream is admitted.  Here requests arrive as a
+Poisson process (the reference's producers start staggered and stream continuously: demo/load-generator/
+main.go:166-184,204-240; its chat UI reports per-request TTFT: demo/chat-ui/index.html:580-588) through the
+full path -- POST /chat on the native server -> engine (decode-priority chunked prefill, PREFILL_BUDGET prompt
+tokens per step while streams decode) -> bus -> SSE sockets of the native load generator (-rate).
+
+Per rate point: TTFT = first token received - request sent (short and long prompts separately), in-flight ITL
+= gaps between consecutive tokens of a stream (its first token excluded), both p50 / p99, plus the mean number
+of concurrent streams and the delivered token rate in the measurement window (the first `--skip-s` seconds,
+while the system fills, are excluded from ITL).
+
+    python tools/bench_serving.py --rates 40,70 --requests 600 --max-tokens 200 --prefill-budget 512,2048
+    python tools/bench_serving.py --rates 70 --long-every 50 --long-words 8000   # some 8k-token prompts
+
+Random-init Mistral-7B weights, synthetic prompts (one token per word).  Prints one JSON line per point.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def analyse(arrivals, n_req, long_every, skip_s, max_tokens):
+    import numpy as np
+
+    by = {}
+    for s, seq, recv, _ts in arrivals:
+        by.setdefault(int(s), []).append((int(seq), int(recv)))
+    if not by:
+        return {"error": "no arrivals"}
+    t_first_send = min(min(r for q, r in v if q == 0) for v in by.values() if any(q == 0 for q, _ in v))
+    w0 = t_first_send + int(skip_s * 1e9)
+    ttft_s, ttft_l, gaps, spans, done, toks = [], [], [], [], 0, 0
+    t_end = 0
+    for s, v in by.items():
+        v.sort(key=lambda x: x[1])
+        send = [r for q, r in v if q == 0]
+        tk = [r for q, r in v if q > 0]
+        if not send or not tk:
+            continue
+        is_long = long_every > 0 and s % long_every == long_every - 1
+        (ttft_l if is_long else ttft_s).append((tk[0] - send[0]) / 1e6)
+        gaps += [(b - a) / 1e6 for a, b in zip(tk, tk[1:]) if a >= w0]
+        spans.append((send[0], tk[-1]))
+        toks += sum(1 for r in tk if r >= w0)
+        t_end = max(t_end, tk[-1])
+        done += 1
+    q = lambda a, p: round(float(np.percentile(a, p)), 3) if len(a) else None  # noqa: E731
+    win = max(1e-9, (t_end - w0) / 1e9)
+    conc = sum(max(0, min(e, t_end) - max(b, w0)) for b, e in spans) / 1e9 / win
+    return {"requests": n_req, "completed": done,
+            "ttft_ms": {"p50": q(ttft_s, 50), "p99": q(ttft_s, 99), "n": len(ttft_s)},
+            "ttft_long_ms": {"p50": q(ttft_l, 50), "p99": q(ttft_l, 99), "n": len(ttft_l)},
+            "itl_ms": {"p50": q(gaps, 50), "p90": q(gaps, 90), "p99": q(gaps, 99), "max": q(gaps, 100)},
+            "mean_concurrent_streams": round(conc, 1), "tokens_per_s": round(toks / win, 1), "window_s": round(win, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="mistral-7b-v0.3")
+    ap.add_argument("--rates", default="70", help="comma list of request rates (req/s)")
+    ap.add_argument("--requests", type=int, default=600)
+    ap.add_argument("--max-tokens", type=int, default=200)
+    ap.add_argument("--prompt-words", type=int, default=500, help="short prompt length (~1 token per word)")
+    ap.add_argument("--long-every", type=int, default=0)
+    ap.add_argument("--long-words", type=int, default=8000)
+    ap.add_argument("--prefill-budget", default="2048", help="comma list of PREFILL_BUDGET values")
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=8448)
+    ap.add_argument("--skip-s", type=float, default=2.0)
+    ap.add_argument("--warmup-requests", type=int, default=48)
+    ap.add_argument("--engine", default="gpu", help="gpu | cpu (the tiny CPU model: a functional check of the tool)")
+    a = ap.parse_args()
+
+    from distributed_sse_for_llm_response_amd.engine import bench_harness
+
+    client = bench_harness.spawn_client()  # before this process touches the GPU
+
+    import torch  # noqa: F401
+
+    from distributed_sse_for_llm_response_amd.serving.app import ServingApp
+    from distributed_sse_for_llm_response_amd.serving.config import ServeConfig
+
+    cfg = ServeConfig(host="127.0.0.1", sse_port=0, origin_port=-1, metrics_port=-1, engine=a.engine, model=a.model,
+                      max_batch=a.max_batch, max_model_len=a.max_model_len, max_tokens=a.max_tokens,
+                      temperature=1.0, first_token_timeout_ms=300000)
+    t0 = time.time()
+    app = ServingApp(cfg).start()
+    print(f"[bench_serving] engine up in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    port = app.port("edge")
+    message = " ".join(f"w{i % 997}" for i in range(a.prompt_words))
+    try:
+        runs = 0
+        for budget in [int(b) for b in a.prefill_budget.split(",")]:
+            app.engine.prefill_budget = budget
+            for rate in [float(r) for r in a.rates.split(",")]:
+                for warm, n in ((True, a.warmup_requests), (False, a.requests)):
+                    if warm and runs > 0:
+                        continue
+                    runs += 1
+                    req = {"host": "127.0.0.1", "port": port, "streams": n, "message": message,
+                           "max_tokens": a.max_tokens, "prefix": f"srv{runs}-", "rate": rate, "seed": runs,
+                           "duration_s": 1200}
+                    if a.long_every and not warm:
+                        req.update(long_every=a.long_every, long_words=a.long_words)
+                    client.stdin.write(json.dumps(req) + "\n")
+                    client.stdin.flush()
+                    res = json.loads(client.stdout.readline())
+                    if warm:
+                        continue
+                    out = {"metric": "serving under Poisson arrivals", "rate_req_s": rate, "prefill_budget": budget,
+                           "max_tokens": a.max_tokens, "prompt_tokens": a.prompt_words + 6,
+                           "long_prompt_every": a.long_every, "long_prompt_tokens": a.long_words + 6 if a.long_every else 0,
+                           **analyse(res["arrivals"], n, a.long_every, a.skip_s, a.max_tokens),
+                           "client_errors": res.get("errors", [])[:3], "engine_stats_cumulative": {
+                               k: app.engine.stats.get(k) for k in ("prefill_tokens", "decode_steps", "steps",
+                                                                    "preemptions", "compactions")}}
+                    print(json.dumps(out), flush=True)
+    finally:
+        client.stdin.close()
+        app.stop()
+
+
+if __name__ == "__main__":
+    main()
