@@ -384,7 +384,7 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
     // 17-64 rows on the ring: DSSE_RESID_NW / DSSE_RESID_SPLIT = waves per workgroup and K split of the O / down
     // projections (more K slices: fewer X bytes per workgroup, more slab bytes for the norm)
     const int rnw = env_int("DSSE_RESID_NW", 0), rsp = env_int("DSSE_RESID_SPLIT", 0);
-    if (M > 16 && M <= 64 && rnw > 0 && rsp > 1 && (N / 16) % rnw == 0 && K % (128 * rsp) == 0) {
+    if (M > 32 && M <= 64 && rnw > 0 && rsp > 1 && (N / 16) % rnw == 0 && K % (128 * rsp) == 0) {
       c.ring_nw = rnw;
       c.S = rsp;
     }
@@ -689,7 +689,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   } else {
     SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
     const int qnw = env_int("DSSE_QKV_NW", 0);  // ring waves per workgroup (with DSSE_QKV_SPLIT)
-    if (qnw > 0 && M > 16 && M <= 64 && (N / 16) % qnw == 0) c.ring_nw = qnw;
+    if (qnw > 0 && M > 32 && M <= 64 && (N / 16) % qnw == 0) c.ring_nw = qnw;  // 33-64 rows: the MT = 4 ring
     DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, S, 1, X, M, w.data_ptr(), K, N, &ep, sl));
   }
   p.qkv_part = sl;

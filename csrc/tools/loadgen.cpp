@@ -613,7 +613,16 @@ int main(int argc, char** argv) {
                                            a.long_words > 0 ? &long_msg : nullptr));
     }
     for (auto& c : cons) threads.emplace_back([&c] { c->run(); });
-    if (produce) std::this_thread::sleep_for(std::chrono::milliseconds(500));  // main.go:162
+    if (produce) {
+      // main.go:162 waits a fixed 500 ms; at 10k connections that is not enough for every subscription to exist
+      // before its producer starts (tokens published earlier are not delivered live: round-2 runs received
+      // 416k-476k of 500k).  Wait for every consumer's response headers (the server subscribes first), at least
+      // 500 ms and at most 60 s.
+      std::this_thread::sleep_for(std::chrono::milliseconds(500));
+      const int64_t until = now_ns() + 60'000'000'000LL;
+      while (st.opened.load() + st.errors.load() < a.conversations && now_ns() < until)
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
   }
   bool prod_ok = true;
   if (produce) {

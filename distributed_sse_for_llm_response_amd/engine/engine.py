@@ -18,7 +18,11 @@ Per ``step()`` (host, a few hundred microseconds of Python):
 3. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
    non-blocking copies on the compute stream;
 4. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
-   streams keep their inter-token latency while new prompts are absorbed);
+   streams keep their inter-token latency while new prompts are absorbed).  While streams decode, the chunk
+   rides in the decode step itself (``ModelRunner.mixed``: one forward over the B decode rows + the chunk's
+   rows, every weight byte streamed once) with a budget that keeps the step near the next row bucket
+   (``DSSE_MIXED_ROWS`` - B tokens, at least 64); a prompt queued for more than ``DSSE_MIXED_BOOST_STEPS``
+   steps raises the budget to PREFILL_BUDGET (the TTFT guard; counted in steps, so TP ranks agree);
 5. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
    next step; token ring row ``t`` receives every token produced in step ``t``);
 6. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
@@ -95,6 +99,7 @@ class Sequence:
     orig_len: int = 0           # prompt length as submitted (after a preemption `prompt` also holds out_ids)
     out_ids: list = field(default_factory=list)  # tokens published so far (re-prefilled after a preemption)
     base: int = 0               # tokens published before the latest (re-)admission
+    enq_step: int = 0           # engine step at which it was queued (the mixed-step TTFT boost counts steps)
 
 
 class _Drain:
@@ -153,14 +158,19 @@ class LLMEngine:
         self._rid = itertools.count(1)
         self._dirty_slots: set = set()
         self.ring_head = int(runner.ring_counter.item()) if runner.device.type == "cuda" else int(runner.ring_counter[0])
-        self.stats = {"steps": 0, "decode_steps": 0, "prefill_tokens": 0, "tokens": 0, "last_step_s": 0.0,
-                      "pauses": 0, "preemptions": 0, "compactions": 0, "host_s": 0.0, "wait_s": 0.0}
+        self.stats = {"steps": 0, "decode_steps": 0, "mixed_steps": 0, "prefill_tokens": 0, "tokens": 0,
+                      "last_step_s": 0.0, "pauses": 0, "preemptions": 0, "compactions": 0, "host_s": 0.0, "wait_s": 0.0}
         # admission keeps this many pages free for running sequences to grow into (vLLM's 1% watermark)
         self.watermark = max(1, runner.kv.num_blocks // 100)
         self._bt_new: list = []  # (sequence, page index, block) appended since the last upload
         self._pending: list = []  # events raised between steps (aborts of queued requests), returned by the next
         self.on_ttft = None
         self.on_itl = None
+        # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
+        self.mixed = os.environ.get("DSSE_MIXED", "1") == "1" and hasattr(runner, "mixed")
+        self.mixed_rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
+        self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
+        self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
 
     # ------------------------------------------------------------------ requests
     def next_rid(self) -> int:
@@ -175,7 +185,8 @@ class LLMEngine:
         if len(prompt) > max_prompt:
             prompt = prompt[-max_prompt:]  # keep the tail (most recent context)
         s = Sequence(rid=next(self._rid) if rid is None else rid, conversation_id=conversation_id,
-                     prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns(), orig_len=len(prompt))
+                     prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns(), orig_len=len(prompt),
+                     enq_step=self.step_no)
         self.waiting.append(s)
         self.by_conv[conversation_id] = s
         return s
@@ -390,6 +401,17 @@ class LLMEngine:
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
         budget = self.prefill_budget if running_decode else self.idle_prefill_budget
+        if running_decode and self.mixed:
+            # the chunk rides in the decode step: keep B + chunk near the next row bucket, unless a prompt has
+            # waited too long (counted in steps: identical on every TP rank)
+            hi = max((s.slot for s in self.slots if s is not None and s.state == "decode"), default=-1) + 1
+            B = next(b for b in batch_buckets(self.r.max_batch) if b >= hi)
+            oldest = min((s.enq_step for s in self.slots if s is not None and s.state == "prefill"),
+                         default=self.step_no)
+            if self.waiting:
+                oldest = min(oldest, self.waiting[0].enq_step)
+            if self.step_no - oldest <= self.mixed_boost_steps:
+                budget = min(budget, max(self.mixed_min_tokens, self.mixed_rows - B))
         chunks, finished = [], []
         for s in self.slots:
             if s is None or s.state != "prefill" or s.aborted or budget <= 0:
@@ -444,17 +466,23 @@ class LLMEngine:
         self._upload()
         producers = []
         ran = False
+        dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
+               and not s.stop_after_enqueue and not s.paused]
+        mixed = bool(chunks) and bool(dec) and self.mixed
         if chunks:
-            r.prefill(chunks, ring_row=row)
+            if not mixed:
+                r.prefill(chunks, ring_row=row)
             self.stats["prefill_tokens"] += sum(len(c.tokens) for c in chunks)
             producers += [(s.slot, s) for s in prefill_done]
             ran = True
-        dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
-               and not s.stop_after_enqueue and not s.paused]
         if dec:
             hi = max(s.slot for s in dec) + 1
             B = next(b for b in batch_buckets(r.max_batch) if b >= hi)
-            r.decode(B)
+            if mixed:
+                r.mixed(B, chunks, ring_row=row)
+                self.stats["mixed_steps"] += 1
+            else:
+                r.decode(B)
             for s in dec:
                 s.decode_enqueued += 1
                 producers.append((s.slot, s))

@@ -345,20 +345,16 @@ class ModelRunner:
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 
-    def prefill(self, seqs: list, ring_row: int) -> None:
-        """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
-        first token into ids[slot] and ring[ring_row, slot] and get positions[slot] set on device."""
-        if not seqs:
-            return
-        w, cfg, comm, dev = self.w, self.cfg, self.comm, self.device
-        nh, nkv, F = w.nh, w.nkv, w.ffn
-        H, eps = cfg.hidden_size, cfg.rms_eps
+    def _prefill_meta(self, seqs: list, row0: int = 0):
+        """Packed metadata of prefill chunks whose rows start at `row0` of the activations (0 for a prefill-only
+        batch, B for the prefill rows of a mixed step): host lists + device tensors (one pinned upload)."""
+        dev = self.device
         n = len(seqs)
         ids, pos, slots = [], [], []
         q_start, q_len, ctx_len, work_seq, work_tile = [], [], [], [], []
         bt = torch.zeros(n, self.max_blocks, dtype=torch.int32)
         for i, s in enumerate(seqs):
-            q_start.append(len(ids))
+            q_start.append(row0 + len(ids))
             for j, t in enumerate(s.tokens):
                 p = s.start_pos + j
                 ids.append(t)
@@ -380,45 +376,21 @@ class ModelRunner:
         if dev.type == "cuda":
             meta = meta.pin_memory().to(dev, non_blocking=True)
             bt = bt.pin_memory().to(dev, non_blocking=True)
-        o = 0
-        d_ids, o = meta[o:o + T], o + T
-        d_pos, o = meta[o:o + T], o + T
-        d_slots, o = meta[o:o + T], o + T
-        d_qs, o = meta[o:o + n], o + n
-        d_ql, o = meta[o:o + n], o + n
-        d_ctx, o = meta[o:o + n], o + n
-        nw = len(work_seq)
-        d_ws, o = meta[o:o + nw], o + nw
-        d_wt, o = meta[o:o + nw], o + nw
-        f32 = dict(device=dev, dtype=torch.float32)
-        bf = dict(device=dev, dtype=torch.bfloat16)
-        resid = torch.empty(T, H, **f32)
-        x = torch.empty(T, H, **bf)
-        q = torch.empty(T, nh, 128, **bf)
-        attn = torch.empty(T, nh, 128, **bf)
-        h = torch.empty(T, F, **bf)
-        max_ctx = max(ctx_len)
-        part = math.ceil(max_ctx / 32) * 32
-        ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d_ids)
-        nl = len(w.layers)
-        # every projection on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows);
-        # gate_up with its fused SiLU·mul epilogue (no [T, 2F] intermediate)
-        tmp = torch.empty(T, H, **bf)
-        qkv = torch.empty(T, (nh + 2 * nkv) * 128, **bf)
-        for li, L in enumerate(w.layers):
-            # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
-            # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
-            ops.gemm_out(x, L.wqkv_t, qkv)
-            ops.rope_kv_write(qkv, d_pos, d_slots, self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
-            ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], bt, d_qs, d_ql, d_ctx, d_ws, d_wt, attn,
-                                self.part_o, self.part_ml, part, 1)
-            self._prefill_resid(attn.view(T, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
-            ops.gemm_silu(x, L.wgu_t, h)
-            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
+        d, o = {}, 0
+        for name, k in (("ids", T), ("pos", T), ("slots", T), ("qs", n), ("ql", n), ("ctx", n),
+                        ("ws", len(work_seq)), ("wt", len(work_seq))):
+            d[name], o = meta[o:o + k], o + k
+        d["bt"] = bt
+        return T, q_start, q_len, ctx_len, d
+
+    def _prefill_sample(self, seqs: list, x, q_start: list, q_len: list, ring_row: int) -> None:
+        """Sequences whose last chunk this is sample their first token (rows q_start + q_len - 1 of `x`) into
+        ids[slot] and ring[ring_row, slot]; positions[slot] is set on the device."""
+        w, cfg, comm, dev = self.w, self.cfg, self.comm, self.device
         last = [i for i, s in enumerate(seqs) if s.last_chunk]
         if not last:
             return
+        f32 = dict(device=dev, dtype=torch.float32)
         rows = torch.tensor([q_start[i] + q_len[i] - 1 for i in last], dtype=torch.long, device=dev)
         xl = x.index_select(0, rows)
         logits = torch.empty(len(last), w.vocab_local, **f32)
@@ -444,3 +416,92 @@ class ModelRunner:
         self.ids.index_copy_(0, slot_idx, new_ids)
         self.ring[ring_row].index_copy_(0, slot_idx, new_ids)
         self.positions.index_copy_(0, slot_idx, last_pos + 1)
+
+    def prefill(self, seqs: list, ring_row: int) -> None:
+        """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
+        first token into ids[slot] and ring[ring_row, slot] and get positions[slot] set on device."""
+        if not seqs:
+            return
+        w, cfg, dev = self.w, self.cfg, self.device
+        nh, nkv, F = w.nh, w.nkv, w.ffn
+        H, eps = cfg.hidden_size, cfg.rms_eps
+        T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs)
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        resid = torch.empty(T, H, **f32)
+        x = torch.empty(T, H, **bf)
+        q = torch.empty(T, nh, 128, **bf)
+        attn = torch.empty(T, nh, 128, **bf)
+        h = torch.empty(T, F, **bf)
+        part = math.ceil(max(ctx_len) / 32) * 32
+        ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d["ids"])
+        nl = len(w.layers)
+        # every projection on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows);
+        # gate_up with its fused SiLU·mul epilogue (no [T, 2F] intermediate)
+        tmp = torch.empty(T, H, **bf)
+        qkv = torch.empty(T, (nh + 2 * nkv) * 128, **bf)
+        for li, L in enumerate(w.layers):
+            # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
+            # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
+            ops.gemm_out(x, L.wqkv_t, qkv)
+            ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
+            ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
+                                d["wt"], attn, self.part_o, self.part_ml, part, 1)
+            self._prefill_resid(attn.view(T, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
+            ops.gemm_silu(x, L.wgu_t, h)
+            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
+        self._prefill_sample(seqs, x, q_start, q_len, ring_row)
+
+    # ------------------------------------------------------------------ mixed prefill + decode
+    def mixed(self, B: int, seqs: list, ring_row: int) -> None:
+        """ONE forward over the decode slots [0, B) and the prefill chunks `seqs` (rows B .. B+T-1): every weight
+        byte streams once for both, so prompt tokens absorbed while streams decode cost the in-flight streams a
+        bigger GEMM (M = B + T rows) instead of a whole extra prefill pass (decode-priority
+        chunked prefill).  Eager (the row count varies step to step).  Decode rows: QKV as a bf16 tile ->
+        vectorised RoPE + K/V write for all B + T rows -> decode attention (partitioned flash-decoding) for the B
+        decode rows and flash prefill for the chunk rows -> shared o / gate_up / down / norms -> the B decode
+        rows sample and commit exactly as the captured decode step does (ids, ring row, positions), the chunks
+        that finish a prompt sample their first token as prefill() does.  Same tokens as prefill() + decode()
+        (greedy: tests/test_mixed_step.py)."""
+        w, cfg, comm, dev = self.w, self.cfg, self.comm, self.device
+        nh, nkv, F = w.nh, w.nkv, w.ffn
+        H, eps = cfg.hidden_size, cfg.rms_eps
+        r = slice(0, B)
+        T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs, row0=B)
+        M = B + T
+        ops.decode_prep(self.active[r], self.positions[r], self.block_tables[r], self.slots[r], self.ctx_len[r],
+                        self.q_len[r], self.kv.num_blocks)
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        resid = torch.empty(M, H, **f32)
+        x = torch.empty(M, H, **bf)
+        q = torch.empty(M, nh, 128, **bf)
+        attn = torch.empty(M, nh, 128, **bf)
+        h = torch.empty(M, F, **bf)
+        tmp = torch.empty(M, H, **bf)
+        qkv = torch.empty(M, (nh + 2 * nkv) * 128, **bf)
+        ids = torch.cat([self.ids[r], d["ids"]])
+        pos = torch.cat([self.positions[r], d["pos"]])
+        slots = torch.cat([self.slots[r], d["slots"]])
+        ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=ids)
+        dpart, dnparts = decode_partitioning(B, nkv, self.max_model_len)
+        ppart = math.ceil(max(ctx_len) / 32) * 32
+        nl = len(w.layers)
+        for li, L in enumerate(w.layers):
+            kc, vc = self.kv.k[li], self.kv.v[li]
+            ops.gemm_out(x, L.wqkv_t, qkv)
+            ops.rope_kv_write(qkv, pos, slots, self.rope, q, kc, vc, nh, nkv)
+            ops.paged_attention(0, q[r], kc, vc, self.block_tables[r], self.q_start[r], self.q_len[r],
+                                self.ctx_len[r], self.work_seq[r], self.work_tile[r], attn[r], self.part_o,
+                                self.part_ml, dpart, dnparts)
+            ops.paged_attention(2, q, kc, vc, d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"], d["wt"], attn,
+                                self.part_o, self.part_ml, ppart, 1)
+            self._resid_proj(attn.view(M, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
+            ops.gemm_silu(x, L.wgu_t, h)
+            w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+            self._resid_proj(h, L.wd_t, resid, w_next, x, tmp)
+        ops.gemm_out(x[r], w.lm_head_t, self.logits[r])
+        self._sample_commit(B)
+        self._prefill_sample(seqs, x, q_start, q_len, ring_row)
+        ops.ring_advance(self.ring_counter)

@@ -90,3 +90,49 @@ def test_full_dims_decode_logits_match_reference(model, gpu, B):
             worst_cos, worst_rel = min(worst_cos, c), max(worst_rel, e)
     print(f"bucket {B}: worst cosine {worst_cos:.6f}, worst max-abs / max {worst_rel:.4f}")
     assert not math.isnan(worst_cos)
+
+
+@pytest.mark.parametrize("B", [64, 128])
+def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B):
+    """ModelRunner.mixed (the engine's prefill-in-decode step): B decode rows + two new prompts' rows in one
+    forward; the decode rows' logits and the new prompts' first tokens against the fp32 reference, then the new
+    sequences decode in the next bucket."""
+    std, r = model
+    g = torch.Generator().manual_seed(1000 + B)
+    n_new = 2
+    prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
+               for _ in range(B + n_new)]
+    tables = [list(range(i * PAGES_PER_SEQ, (i + 1) * PAGES_PER_SEQ)) for i in range(B + n_new)]
+    r.block_tables.zero_()
+    for i, bt in enumerate(tables):
+        r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    seqs = [PrefillSeq(i, p, 0, tables[i], True) for i, p in enumerate(prompts[:B])]
+    for k in range(0, B, 64):
+        r.prefill(seqs[k:k + 64], ring_row=0)
+    r.active.zero_()
+    r.active[:B] = 1
+    r.temperature.zero_()
+    gen = [[int(t)] for t in r.ids[:B].cpu()]
+    new = [PrefillSeq(B + j, prompts[B + j], 0, tables[B + j], True) for j in range(n_new)]
+    r.mixed(B, new, ring_row=int(r.ring_counter.item()))
+    torch.cuda.synchronize()
+    mixed_logits = r.logits[:B].clone()
+    for i, t in enumerate(r.ids[:B].cpu()):
+        gen[i].append(int(t))
+    for i in range(0, B, 7):
+        ref, _ = reference_forward(CFG, std, torch.tensor(prompts[i] + gen[i][:1], device=gpu))
+        _compare(ref[len(prompts[i])], mixed_logits[i], f"mixed step, decode row {i}")
+    for j in range(n_new):
+        p = prompts[B + j]
+        ref, _ = reference_forward(CFG, std, torch.tensor(p, device=gpu))
+        tok = int(r.ids[B + j])
+        assert float(ref[-1].max() - ref[-1, tok]) < 0.02 * float(ref[-1].abs().max()), f"new prompt {j}"
+    # the new sequences join the batch (bucket 2B) and decode like everyone else
+    r.active[B:B + n_new] = 1
+    r.decode(2 * B if 2 * B in BUCKETS else 256)
+    torch.cuda.synchronize()
+    for j in range(n_new):
+        p = prompts[B + j]
+        first = int(r.ring[(int(r.ring_counter.item()) - 2) % r.ring.shape[0], B + j])
+        ref, _ = reference_forward(CFG, std, torch.tensor(p + [first], device=gpu))
+        _compare(ref[-1], r.logits[B + j], f"new sequence {j} first decode step")
