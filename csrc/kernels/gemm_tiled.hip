@@ -127,12 +127,15 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
   }
 
   constexpr int INS = G::A_INS + G::B_INS;
-  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+  static_assert(NS >= 2 && NS <= 4, "2-4 LDS stages");
   issue(0, 0);
-  if (NS == 3 && nk > 1) issue(1, 1);
+  if (NS >= 3 && nk > 1) issue(1, 1);
+  if (NS == 4 && nk > 2) issue(2, 2);
   for (int t = 0; t < nk; ++t) {
-    // step t's DMA done on this wave (NS = 3: step t+1's may stay in flight), then everyone's: publish step t
-    if (NS == 3 && t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INS) : "memory");
+    // step t's DMA done on this wave (steps t+1 .. t+NS-2 may stay in flight), then everyone's: publish step t
+    const int younger = min(NS - 2, nk - 1 - t);
+    if (NS == 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * INS) : "memory");
+    else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     // the stage step t+NS-1 overwrites was last read in step t-1, which every wave finished before this barrier
     if (t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
@@ -395,6 +398,8 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
     case 2: return launch_t<4, 1, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 waves
     case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
     case 4: return launch_phased<MODE>(X, ldx, M, W, K, N, S, ep, part, st);              // 256 x 256, phased
+    case 5: return launch_t<2, 2, 4, 4, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 128, 4 stages
+    case 6: return launch_t<4, 1, 4, 4, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 stages
   }
   return hipErrorInvalidValue;
 }
@@ -402,7 +407,8 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
 }  // namespace dsse
 
 // cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves),
-// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel).
+// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel),
+// 5 / 6 = cfg 1 / 2 with 4 LDS stages (two steps' DMA in flight across each barrier).
 // Shape contract (checked by the caller): N % BN == 0, K % (64 S) == 0, the tiled weight layout (api.h).
 // S > 1: fp32 slabs [S, M, N] into `part`, reduced by launch_splitk_reduce unless partial_only.
 extern "C" hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M,

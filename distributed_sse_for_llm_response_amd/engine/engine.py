@@ -18,11 +18,12 @@ Per ``step()`` (host, a few hundred microseconds of Python):
 3. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
    non-blocking copies on the compute stream;
 4. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
-   streams keep their inter-token latency while new prompts are absorbed).  While streams decode, the chunk
-   rides in the decode step itself (``ModelRunner.mixed``: one forward over the B decode rows + the chunk's
-   rows, every weight byte streamed once) with a budget that keeps the step near the next row bucket
+   streams keep their inter-token latency while new prompts are absorbed).  With ``DSSE_MIXED=1`` the chunk
+   rides in the decode step itself instead (``ModelRunner.mixed``: one forward over the B decode rows + the
+   chunk's rows, every weight byte streamed once) with a budget that keeps the step near the next row bucket
    (``DSSE_MIXED_ROWS`` - B tokens, at least 64); a prompt queued for more than ``DSSE_MIXED_BOOST_STEPS``
-   steps raises the budget to PREFILL_BUDGET (the TTFT guard; counted in steps, so TP ranks agree);
+   steps raises the budget to PREFILL_BUDGET (the TTFT guard; counted in steps, so TP ranks agree).  Off by
+   default: run eagerly it measured slower than separate passes (``profiles/r3/serving_arrivals.md``);
 5. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
    next step; token ring row ``t`` receives every token produced in step ``t``);
 6. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
@@ -167,7 +168,7 @@ class LLMEngine:
         self.on_ttft = None
         self.on_itl = None
         # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
-        self.mixed = os.environ.get("DSSE_MIXED", "1") == "1" and hasattr(runner, "mixed")
+        self.mixed = os.environ.get("DSSE_MIXED", "0") == "1" and hasattr(runner, "mixed")
         self.mixed_rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
         self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
         self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
