@@ -209,7 +209,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 6) {
+  if (cfg < 0 || cfg > 9) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
     // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
     // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
@@ -220,14 +220,16 @@ TCfg pick_tiled(int M, int N, int K) {
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
     const int narrow = env_int("DSSE_T_NARROW_CFG", 1);
-    if (narrow >= 0 && narrow <= 6 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
+    if (narrow >= 0 && narrow <= 9 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
     // wide projections of those buckets (gate_up, LM head): DSSE_T_WIDE_CFG (default by the rule above)
     const int wide = env_int("DSSE_T_WIDE_CFG", -1);
-    if (wide >= 0 && wide <= 6 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
+    if (wide >= 0 && wide <= 9 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
   }
   const int min_wgs = env_int("DSSE_T_MIN_WGS", 160);  // split K until this many workgroups (M <= 512)
-  // tile shapes of gemm_tiled.hip launch_t_mode: BM 128 for cfg 1, else 256; BN 64 for cfg 2, 256 for cfg 3 / 4
-  const int BM = (cfg == 1 || cfg == 5) ? 128 : 256, BN = (cfg == 2 || cfg == 6) ? 64 : ((cfg == 3 || cfg == 4) ? 256 : 128);
+  // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
+  static constexpr int kBM[10] = {256, 128, 256, 256, 256, 128, 256, 128, 256, 256};
+  static constexpr int kBN[10] = {128, 128, 64, 256, 256, 128, 64, 128, 128, 64};
+  const int BM = kBM[cfg], BN = kBN[cfg];
   c.cfg = cfg;
   c.S = 1;
   c.ok = N % BN == 0 && K % 64 == 0;
@@ -495,7 +497,7 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
   }
   void* sptr = nullptr;
   int sync_rows = 0;
-  if (sync.has_value() && env_int("DSSE_NORM_SPLIT", 1)) {
+  if (sync.has_value() && env_int("DSSE_NORM_SPLIT", 0)) {
     check_gpu(*sync, "sync");
     check_dtype(*sync, at::kInt, "sync");
     sync_rows = (int)(sync->numel() / 9);

@@ -20,6 +20,9 @@
 // stored (MFMA output rows depend only on the same A row).
 #include "gemm_epilogue.h"
 
+#include <cstdlib>
+#include <type_traits>
+
 #ifndef DSSE_X_TOUCH
 #define DSSE_X_TOUCH 1  // L2 warm-up loads of the next X slice (see the kernel)
 #endif
@@ -454,6 +457,183 @@ static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf1
   return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// gemm_ring2: the ring GEMM with the weight look-ahead decoupled from X (round 3, profiles/r3/fillbench.md).
+//
+// An HBM weight stream is latency-bound (~2.3 us loaded): a CU moves weight bytes in flight / 2.3 us, up to
+// ~28 GB/s (7.2 TB/s chip-wide) at 32-64 KiB in flight.  gemm_ring_kernel stages X and W through ONE ring (one
+// slot = X chunk + every wave's W chunk, one vmcnt for both), so X's 16 KiB per slot limits W to 1-3 chunks in
+// flight (12-28 KiB at 64 rows: 3.6-4.4 TB/s on qkv / o / down).  Here:
+//   * NW compute waves, each with its OWN ring of DW weight slots (4 KiB: its 16-column tile x 128-deep chunk)
+//     in LDS, filled by its own buffer_load ... lds DW - 1 chunks ahead and waited for by its own counted vmcnt
+//     (its own loads only: no barrier needed for W, the wave both fills and reads its slots);
+//   * XL loader waves that only stage X (16 MT rows x 128 columns per chunk, L2-resident: 86 GB/s per CU) into
+//     a short ring of DX slots, DX - 1 chunks ahead;
+//   * one s_barrier per chunk: the loaders' vmcnt retired X(c) before it, and every compute wave finished chunk
+//     c - 1 before it, so X(c + DX - 1) may overwrite X(c - 1)'s slot right after it.
+// W-slot reuse needs no barrier: a compute wave refills the slot of chunk c - 1 after its MFMAs of chunk c,
+// which consumed chunk c - 1's fragments (their ds_reads completed) one iteration earlier.  Look-ahead past the
+// last chunk: weights fail the buffer range check (no traffic; zeros land in a slot nobody reads), X re-reads
+// the last chunk into a slot nobody reads, so every wave's per-chunk load count -- the vmcnt literals -- is
+// uniform.  Same epilogues and split-K contract as gemm_ring_kernel.
+template <int MT, int NW, int XL, int DX, int DW>
+struct Ring2Geom {
+  static constexpr int SLOTX = 16 * MT * 256;       // X chunk image (16 MT rows x 256 B)
+  static constexpr int XOFF = 0, WOFF = DX * SLOTX;  // X ring, then NW x DW weight slots of 4 KiB
+  static constexpr size_t LDS = (size_t)DX * SLOTX + (size_t)NW * DW * 4096;
+};
+
+template <int MT, int NW, int XL, int DX, int DW, int MODE>
+__global__ void __launch_bounds__(64 * (NW + XL))
+gemm_ring2_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
+                  GemmEpi ep, float* __restrict__ part) {
+  using G = Ring2Geom<MT, NW, XL, DX, DW>;
+  constexpr int MP = 16 * MT;
+  constexpr int XN = MP / 4;              // 1 KiB X DMA instructions per chunk (4 rows each)
+  static_assert(XN % XL == 0, "X instructions split evenly over the loader waves");
+  constexpr int XI = XN / XL;             // per loader wave per chunk
+  static_assert(DX >= 3 && DW >= 3 && G::LDS <= 160 * 1024, "rings of >= 3 slots within the CU's LDS");
+  constexpr int WAUX = DSSE_W_DEFAULT ? 0 : kAuxNT;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  int wg = blockIdx.x, ks = blockIdx.y;
+  if (DSSE_XCD_SPLITK && gridDim.y > 1 && 8 % gridDim.y == 0 && (gridDim.x * gridDim.y) % 8 == 0) {
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x, xcd = lin % 8, slot = lin / 8, per = 8 / gridDim.y;
+    ks = xcd / per;
+    wg = slot * per + xcd % per;
+  }
+  const int k0 = ks * Kr;
+  const int nch = Kr >> 7;
+  const int KC = K >> 7;
+
+  if (w >= NW) {  // ---------------- X loader wave
+    const int lw = w - NW;
+    const bf16* xsrc[XI];
+    int xdst[XI];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      xdst[i] = lw * XI + i;  // instruction index within the chunk: rows 4 xdst .. 4 xdst + 3
+      const int row = 4 * xdst[i] + g;
+      xsrc[i] = X + (size_t)min(row, M - 1) * ldx + k0 + 8 * (r ^ swz(row & 15));
+    }
+    auto issue_x = [&](int c, int slot) {
+      const int cc = min(c, nch - 1);
+      char* base = smem + G::XOFF + slot * G::SLOTX;
+#pragma unroll
+      for (int i = 0; i < XI; ++i) glds16_s(xsrc[i] + cc * 128, base + xdst[i] * 1024);
+    };
+#pragma unroll
+    for (int d = 0; d < DX - 1; ++d) issue_x(d, d);
+    for (int c0 = 0; c0 < nch; c0 += DX) {
+#pragma unroll
+      for (int u = 0; u < DX; ++u) {
+        if (u > 0 && c0 + u >= nch) break;
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((DX - 2) * XI) : "memory");
+        issue_x(c0 + u + DX - 1, (u + DX - 1) % DX);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---------------- compute wave: its own 16-column tile and weight ring
+  const int tgi = wg * NW + w;
+  const int tgu = __builtin_amdgcn_readfirstlane(tgi), k0u = __builtin_amdgcn_readfirstlane(k0);
+  const __amdgpu_buffer_rsrc_t wrs =
+      make_rsrc(W + ((size_t)tgu * KC + (k0u >> 7)) * kTileChunk, (uint32_t)nch * kTileChunk * 2);
+  char* wring = smem + G::WOFF + w * (DW * 4096);
+  auto issue_w = [&](int c, int slot) {
+    char* wb = wring + slot * 4096;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(wb + 1024 * s)),
+          16, (uint32_t)c * (kTileChunk * 2) + 1024 * s + lane * 16, 0, 0, WAUX);
+  };
+#pragma unroll
+  for (int d = 0; d < DW - 1; ++d) issue_w(d, d);
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DX and DW chunks per unrolled group: slot indices are compile-time constants in both rings
+  constexpr int UN = DX * DW;
+  for (int c0 = 0; c0 < nch; c0 += UN) {
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      if (u > 0 && c0 + u >= nch) break;
+      // own W(c) landed (W(c+1) .. W(c+DW-2) may stay in flight), then X(c) published by the loaders
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((DW - 2) * 4) : "memory");
+      const char* xb = smem + G::XOFF + (u % DX) * G::SLOTX;
+      const char* wb = wring + (u % DW) * 4096 + lane * 16;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 xf[MT];
+        const int ch = ((4 * g + s) ^ swz(r)) << 4;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * 256 + ch);
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wb + 1024 * s);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16x16x32(xf[mt], wf, acc[mt]);
+      }
+      issue_w(c0 + u + DW - 1, (u + DW - 1) % DW);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
+  if constexpr (MODE == kSiluMul) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) silu_epilogue4(ep, M, 16 * mt + 4 * g, tgi, r, acc[mt]);
+    return;
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = acc[mt][i];
+      const float partner = MODE == kQkvRope ? __shfl_xor(v, 8) : 0.f;
+      epilogue<MODE>(ep, part_ks, M, N, 16 * mt + 4 * g + i, tgi, r, v, partner);
+    }
+}
+
+template <int MT, int NW, int XL, int DX, int DW, int MODE>
+static hipError_t launch_r2(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
+                            float* part, hipStream_t st) {
+  const size_t lds = Ring2Geom<MT, NW, XL, DX, DW>::LDS;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring2_kernel<MT, NW, XL, DX, DW, MODE>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  dim3 grid(N / 16 / NW, S), block(64 * (NW + XL));
+  hipLaunchKernelGGL((gemm_ring2_kernel<MT, NW, XL, DX, DW, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S,
+                     ep, part);
+  return hipGetLastError();
+}
+
+// (rows tile MT, compute waves NW) -> loader waves, X slots, W slots per wave (LDS <= 160 KiB)
+template <int MODE>
+static hipError_t launch_r2_mode(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
+                                 const GemmEpi& ep, float* part, hipStream_t st) {
+  const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
+#define DSSE_R2_CASE(MT_, NW_, XL_, DX_, DW_) \
+  if (mt == MT_ && nw == NW_) return launch_r2<MT_, NW_, XL_, DX_, DW_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
+  // 33-64 rows: X slot 16 KiB x 3
+  DSSE_R2_CASE(4, 3, 1, 3, 8) DSSE_R2_CASE(4, 4, 1, 3, 7) DSSE_R2_CASE(4, 5, 1, 3, 5) DSSE_R2_CASE(4, 6, 1, 3, 4)
+  DSSE_R2_CASE(4, 7, 1, 3, 4) DSSE_R2_CASE(4, 8, 1, 3, 3)
+  // 17-32 rows: X slot 8 KiB x 3
+  DSSE_R2_CASE(2, 3, 1, 3, 10) DSSE_R2_CASE(2, 4, 1, 3, 8) DSSE_R2_CASE(2, 7, 1, 3, 4) DSSE_R2_CASE(2, 8, 1, 3, 4)
+  // 65-128 rows: X slot 32 KiB x 3, two loader waves
+  DSSE_R2_CASE(8, 4, 2, 3, 4)
+#undef DSSE_R2_CASE
+  return hipErrorInvalidValue;
+}
+
 }  // namespace dsse
 
 // rd: weight-ring depth in LDS slices (mt <= 4: 1 = 4 chunks = 16 KiB per wave in flight, 2 = 8 chunks;
@@ -493,17 +673,32 @@ extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, 
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
   if (M > 128 || M < 17 || (M > 64 && nw != 4) || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
+  // ring2 (decoupled weight look-ahead): DSSE_RING2=1 (default), 0 = the single-ring kernel (also the fallback
+  // for a shape ring2 is not instantiated for)
+  static const bool r2 = [] {
+    const char* v = std::getenv("DSSE_RING2");
+    return !(v && v[0] == '0');
+  }();
+  auto run = [&](auto mode_tag, int s_, const GemmEpi* e_, float* p_) -> hipError_t {
+    constexpr int MODE = decltype(mode_tag)::value;
+    if (r2) {
+      const hipError_t e2 = launch_r2_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
+      if (e2 != hipErrorInvalidValue) return e2;
+      (void)hipGetLastError();
+    }
+    return launch_r_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
+  };
   if (S == 1 && !partial_only) {
     switch (mode) {
-      case kStoreBf16: return launch_r_mode<kStoreBf16>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kStoreF32: return launch_r_mode<kStoreF32>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kResidAdd: return launch_r_mode<kResidAdd>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kSiluMul: return launch_r_mode<kSiluMul>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kQkvRope: return launch_r_mode<kQkvRope>(nw, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreBf16: return run(std::integral_constant<int, kStoreBf16>{}, 1, ep, nullptr);
+      case kStoreF32: return run(std::integral_constant<int, kStoreF32>{}, 1, ep, nullptr);
+      case kResidAdd: return run(std::integral_constant<int, kResidAdd>{}, 1, ep, nullptr);
+      case kSiluMul: return run(std::integral_constant<int, kSiluMul>{}, 1, ep, nullptr);
+      case kQkvRope: return run(std::integral_constant<int, kQkvRope>{}, 1, ep, nullptr);
     }
     return hipErrorInvalidValue;
   }
-  hipError_t e = launch_r_mode<kPartial>(nw, x, ldx, M, w, K, N, S, *ep, part, st);
+  hipError_t e = run(std::integral_constant<int, kPartial>{}, S, ep, part);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

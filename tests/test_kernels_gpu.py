@@ -40,6 +40,9 @@ GEMM_CONFIGS = {
     "tiled-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "3"},
     "tiled-128-ns4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "5", "DSSE_T_SPLIT": "2"},
     "tiled-256x64-ns4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "6"},
+    "tiled2-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "7", "DSSE_T_SPLIT": "2"},
+    "tiled2-256x128": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "8"},
+    "tiled2-256x64-split4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "9", "DSSE_T_SPLIT": "4"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
@@ -245,6 +248,65 @@ def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     _close(vc, vr, 3e-2, 2e-2, "v cache")
 
 
+@pytest.mark.parametrize("cfg", ["auto", "tiled2-128-split2", "tiled2-256x128", "tiled2-256x64-split4"])
+@pytest.mark.parametrize("M", [129, 192, 200, 256])
+def test_decode_bucket_epilogues(gpu, monkeypatch, cfg, M):
+    """Every epilogue of the 129-256-row decode buckets (bf16 / fp32 store, residual add, SiLU*mul, QKV + RoPE +
+    K/V write, split-K slabs reduced by the norm) on the separate-X/W-ring tiled kernels, at row counts that are
+    not multiples of the tile height, against the fp32 reference."""
+    for k, v in GEMM_CONFIGS[cfg].items():
+        monkeypatch.setenv(k, v)
+    ops.refresh_env()
+    g = torch.Generator().manual_seed(M * 7 + len(cfg))
+    K = 2048
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(1024, K, dev=gpu, scale=1 / 45, gen=g))
+    for dt in (torch.bfloat16, torch.float32):
+        out = torch.zeros(M, 1024, device=gpu, dtype=dt)
+        ref = torch.zeros(M, 1024, dtype=dt)
+        ops.gemm_out(x, w, out)
+        R.gemm_out(x.cpu(), w.cpu(), ref)
+        _close(out, ref, 2e-2 if dt == torch.bfloat16 else 1e-3, 1e-2, f"gemm_out {dt}")
+    r0 = torch.randn(M, 1024, generator=g)
+    r = r0.clone().to(gpu)
+    ops.gemm_resid(x, w, r)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    _close(r, r0, 1e-3, 1e-3, "gemm_resid")
+    h = torch.zeros(M, 512, device=gpu, dtype=torch.bfloat16)
+    hr = torch.zeros(M, 512, dtype=torch.bfloat16)
+    ops.gemm_silu(x, w, h)
+    R.gemm_silu(x.cpu(), w.cpu(), hr)
+    _close(h, hr, 2e-2, 2e-2, "gemm_silu")
+    nh, nkv = 4, 2
+    wq = R.tile_weight(_rand((nh + 2 * nkv) * 128, K, dev=gpu, scale=1 / 45, gen=g))
+    rope = R.rope_table(4096, 1e6, gpu)
+    positions = torch.randint(0, 4000, (M,), generator=g, dtype=torch.int32)
+    slots = torch.randperm(16 * 32, generator=g)[:M].to(torch.int32)
+    slots[-1] = -1
+    q = torch.zeros(M, nh * 128, device=gpu, dtype=torch.bfloat16)
+    kc = torch.zeros(16, nkv, 32, 128, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros(16, nkv, 128, 32, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_qkv_rope(x, wq, positions.to(gpu), slots.to(gpu), rope, q, kc, vc, nh, nkv)
+    qr, kr, vr = torch.zeros(M, nh * 128, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    R.gemm_qkv_rope(x.cpu(), wq.cpu(), positions, slots, rope.cpu(), qr, kr, vr, nh, nkv)
+    _close(q, qr, 3e-2, 2e-2, "q")
+    _close(kc, kr, 3e-2, 2e-2, "k cache")
+    _close(vc, vr, 3e-2, 2e-2, "v cache")
+    # split-K slabs reduced inside the RMSNorm (the o / down projections of the wide buckets)
+    nwt = (1 + 0.1 * torch.randn(1024, generator=g)).bfloat16()
+    r0 = torch.randn(M, 1024, generator=g)
+    r = r0.clone().to(gpu)
+    part = torch.zeros(32 * M * 1024, device=gpu)
+    y = torch.zeros(M, 1024, device=gpu, dtype=torch.bfloat16)
+    ns = ops.gemm_resid_split(x, w, r, part)
+    ops.rmsnorm(r, nwt.to(gpu), y, 1e-5, part=part, nsplit=ns)
+    yr = torch.zeros(M, 1024, dtype=torch.bfloat16)
+    R.gemm_resid(x.cpu(), w.cpu(), r0)
+    R.rmsnorm(r0, nwt, yr, 1e-5)
+    _close(r, r0, 1e-3, 1e-3, "split resid")
+    _close(y, yr, 2e-2, 1e-2, "split norm")
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("M,H", [(1, 4096), (37, 4096), (5, 1024), (3, 8192)])
 def test_rmsnorm(gpu, mode, M, H):
@@ -264,10 +326,12 @@ def test_rmsnorm(gpu, mode, M, H):
     _close(y, yr, 2e-2, 1e-2, "y")
 
 
-def test_rmsnorm_row_split_rendezvous(gpu):
+def test_rmsnorm_row_split_rendezvous(gpu, monkeypatch):
     """Row-split RMSNorm (4 workgroups per row exchanging {ss, tag} granules): 60 back-to-back launches on ONE
     sync workspace with varying row counts, modes 0 / 1 / 3 and slab counts, every call against the fp32
     reference -- a granule of a previous call read as current would show as a wrong norm of that row."""
+    monkeypatch.setenv("DSSE_NORM_SPLIT", "1")  # off by default (measured slower in the decode step)
+    ops.refresh_env()
     g = torch.Generator().manual_seed(11)
     H, cap = 4096, 256
     sync = ops.norm_sync_workspace(cap, gpu)
