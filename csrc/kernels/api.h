@@ -113,6 +113,7 @@ hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
 hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
                             int max_blocks, int num_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
 hipError_t dsse_ring_advance(int* counter, hipStream_t st);
+hipError_t dsse_prefetch(const void* src, int64_t bytes, int wgs, unsigned* sink, hipStream_t st);
 // TP all-reduce + residual + RMSNorm over IPC peer buffers (allreduce.hip)
 size_t dsse_ar_buffer_bytes(int rows, int H);
 hipError_t dsse_ar_alloc(size_t bytes, void** ptr, void* handle64, int* uncached);

@@ -546,6 +546,20 @@ void decode_prep(const Tensor& active, const Tensor& positions, const Tensor& bl
                                   cur_stream()));
 }
 
+// Warm the Infinity Cache with the first `bytes` of `t` (all of it when bytes < 0) on `wgs` workgroups; `sink`:
+// an int32 tensor of >= 1024 words the kernel never writes in practice (it keeps the loads alive).
+void prefetch(const Tensor& t, Tensor& sink, int64_t bytes, int64_t wgs) {
+  check_gpu(t, "t");
+  check_gpu(sink, "sink");
+  check_dtype(sink, at::kInt, "sink");
+  TORCH_CHECK(t.is_contiguous(), "prefetch needs a contiguous tensor");
+  TORCH_CHECK(sink.numel() >= 1024, "sink must hold 1024 words");
+  const int64_t total = t.numel() * t.element_size();
+  const int64_t n = bytes < 0 ? total : std::min(bytes, total);
+  DSSE_CHECK_HIP(dsse_prefetch(t.data_ptr(), n, (int)std::max<int64_t>(1, std::min<int64_t>(wgs, 1024)),
+                               reinterpret_cast<unsigned*>(sink.data_ptr<int>()), cur_stream()));
+}
+
 void ring_advance(Tensor& counter) {
   check_gpu(counter, "counter");
   check_dtype(counter, at::kInt, "counter");
@@ -885,6 +899,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("decode_prep(Tensor active, Tensor positions, Tensor block_tables, Tensor(a!) slots, "
         "Tensor(b!) ctx_len, Tensor(c!) q_len, int num_blocks=2147483647) -> ()");
   m.def("ring_advance(Tensor(a!) counter) -> ()");
+  m.def("prefetch(Tensor t, Tensor(a!) sink, int bytes, int wgs) -> ()");
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
         "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
@@ -918,6 +933,7 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("decode_prep", &decode_prep);
   m.impl("ring_advance", &ring_advance);
+  m.impl("prefetch", &prefetch);
   m.impl("paged_attention", &paged_attention);
   m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);

@@ -28,6 +28,7 @@ import math
 import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -39,6 +40,10 @@ from .weights import EngineWeights
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
+# Prefill batches of up to 2048 tokens replay a captured graph per row bucket (padded rows: slot -1, no K/V write,
+# no attention work); larger batches (long prompts at an idle budget) run eagerly.  DSSE_PREFILL_GRAPHS=0 disables.
+PREFILL_GRAPH_BUCKETS = (128, 256, 512, 1024, 2048)
+PREFILL_GRAPH_SEQS = 16  # sequences per captured prefill batch (more: eager)
 # Largest decode bucket on the fused-norm decode step (gemm_skinny / gemm_stream, split-K slabs reduced in the
 # norms); larger buckets take the wide path (_decode_layers_wide), whose projections the kernel library routes to
 # gemm_wide / gemm_tiled by row count (bindings.cpp gemm_impl).  Round 1 measured the split at 128 rows
@@ -141,6 +146,8 @@ class ModelRunner:
                   f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
         self.graphs = {}
         self.graph_pool = None
+        self.pf_graphs = {}   # row bucket -> captured prefill graph
+        self.pf = None        # static prefill buffers (allocated by capture)
 
     # ------------------------------------------------------------------ decode
     def decode_forward(self, B: int) -> None:
@@ -311,6 +318,34 @@ class ModelRunner:
             self.graphs[B] = g
         torch.cuda.synchronize(self.device)
         self._restore_state(saved)
+        self._capture_prefill()
+
+    def _capture_prefill(self) -> None:
+        """One graph per prefill row bucket over static buffers (_PrefillStatic); the metadata of a batch is
+        uploaded into them before the replay.  Captured with all-padding metadata (every row slot -1: no K/V
+        write; every work item on the empty sequence)."""
+        if os.environ.get("DSSE_PREFILL_GRAPHS", "1") == "0":
+            return
+        buckets = [t for t in PREFILL_GRAPH_BUCKETS if t <= self.max_prefill_tokens]
+        if not buckets:
+            return
+        self.pf = _PrefillStatic(self, max(buckets))
+        self.pf.upload_padding()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for tb in buckets:
+                self._prefill_layers(tb, self.pf.views(tb))
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for tb in sorted(buckets, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._prefill_layers(tb, self.pf.views(tb))
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.pf_graphs[tb] = g
+        torch.cuda.synchronize(self.device)
 
     def _snapshot_state(self):
         return [t.clone() for t in (self.ids, self.positions, self.ring, self.ring_counter)]
@@ -418,40 +453,49 @@ class ModelRunner:
         self.positions.index_copy_(0, slot_idx, last_pos + 1)
 
     def prefill(self, seqs: list, ring_row: int) -> None:
-        """Run one packed prefill batch (eager).  Sequences whose last chunk this is sample their
+        """Run one packed prefill batch: a captured graph of the smallest row bucket that holds it (metadata
+        uploaded into the static buffers first), else eagerly.  Sequences whose last chunk this is sample their
         first token into ids[slot] and ring[ring_row, slot] and get positions[slot] set on device."""
         if not seqs:
             return
-        w, cfg, dev = self.w, self.cfg, self.device
-        nh, nkv, F = w.nh, w.nkv, w.ffn
-        H, eps = cfg.hidden_size, cfg.rms_eps
+        T = sum(len(s.tokens) for s in seqs)
+        tb = next((t for t in sorted(self.pf_graphs) if t >= T), None) if len(seqs) <= PREFILL_GRAPH_SEQS else None
+        if tb is not None:
+            q_start, q_len = self.pf.upload(seqs, tb)
+            self.pf_graphs[tb].replay()
+            self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)
+            return
+        w, dev = self.w, self.device
+        nh, nkv, F, H = w.nh, w.nkv, w.ffn, self.cfg.hidden_size
         T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs)
         f32 = dict(device=dev, dtype=torch.float32)
         bf = dict(device=dev, dtype=torch.bfloat16)
-        resid = torch.empty(T, H, **f32)
-        x = torch.empty(T, H, **bf)
-        q = torch.empty(T, nh, 128, **bf)
-        attn = torch.empty(T, nh, 128, **bf)
-        h = torch.empty(T, F, **bf)
-        part = math.ceil(max(ctx_len) / 32) * 32
+        d.update(resid=torch.empty(T, H, **f32), x=torch.empty(T, H, **bf), q=torch.empty(T, nh, 128, **bf),
+                 attn=torch.empty(T, nh, 128, **bf), h=torch.empty(T, F, **bf), tmp=torch.empty(T, H, **bf),
+                 qkv=torch.empty(T, (nh + 2 * nkv) * 128, **bf), part=math.ceil(max(ctx_len) / 32) * 32)
+        self._prefill_layers(T, d)
+        self._prefill_sample(seqs, d["x"], q_start, q_len, ring_row)
+
+    def _prefill_layers(self, T: int, d: dict) -> None:
+        """Embedding + every layer over T packed prompt rows (buffers and metadata in `d`; graph-capturable)."""
+        w, eps = self.w, self.cfg.rms_eps
+        nh, nkv = w.nh, w.nkv
+        resid, x, q, attn, h, tmp, qkv = (d[k] for k in ("resid", "x", "q", "attn", "h", "tmp", "qkv"))
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d["ids"])
         nl = len(w.layers)
         # every projection on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows);
         # gate_up with its fused SiLU·mul epilogue (no [T, 2F] intermediate)
-        tmp = torch.empty(T, H, **bf)
-        qkv = torch.empty(T, (nh + 2 * nkv) * 128, **bf)
         for li, L in enumerate(w.layers):
             # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
             # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
             ops.gemm_out(x, L.wqkv_t, qkv)
             ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
-                                d["wt"], attn, self.part_o, self.part_ml, part, 1)
+                                d["wt"], attn, self.part_o, self.part_ml, d["part"], 1)
             self._prefill_resid(attn.view(T, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
             ops.gemm_silu(x, L.wgu_t, h)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
-        self._prefill_sample(seqs, x, q_start, q_len, ring_row)
 
     # ------------------------------------------------------------------ mixed prefill + decode
     def mixed(self, B: int, seqs: list, ring_row: int) -> None:
@@ -505,3 +549,103 @@ class ModelRunner:
         self._sample_commit(B)
         self._prefill_sample(seqs, x, q_start, q_len, ring_row)
         ops.ring_advance(self.ring_counter)
+
+
+class _PrefillStatic:
+    """Static buffers of the captured prefill graphs (sized for the largest bucket Tmax; a bucket's graph uses
+    the first tb rows) and their metadata upload: one int32 image [ids | pos | slots | q_start | q_len | ctx_len |
+    work_seq | work_tile | block tables] filled on the host (two pinned buffers, alternating; an event guards
+    reuse) and copied with one non-blocking H2D before the replay.  Padding: rows >= T have slot -1 (no K/V
+    write) and token 0; sequence index NS is the empty sequence (q_len 0) that padded work items point at."""
+
+    def __init__(self, runner: ModelRunner, tmax: int):
+        self.r, self.tmax = runner, tmax
+        w, cfg, dev = runner.w, runner.cfg, runner.device
+        nh, nkv, F, H = w.nh, w.nkv, w.ffn, cfg.hidden_size
+        self.ns = PREFILL_GRAPH_SEQS
+        self.nw = tmax // PREFILL_TILE + self.ns  # work items: sum of ceil(q_len / 64) <= T / 64 + seqs
+        self.mb = runner.max_blocks
+        n1 = self.ns + 1
+        self.off = {}
+        o = 0
+        for name, k in (("ids", tmax), ("pos", tmax), ("slots", tmax), ("qs", n1), ("ql", n1), ("ctx", n1),
+                        ("ws", self.nw), ("wt", self.nw), ("bt", n1 * self.mb)):
+            self.off[name] = (o, k)
+            o += k
+        self.words = o
+        self.dev_meta = torch.zeros(o, dtype=torch.int32, device=dev)
+        self.host = [torch.zeros(o, dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.events = [None, None]
+        self.flip = 0
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        self.resid = torch.zeros(tmax, H, **f32)
+        self.x = torch.zeros(tmax, H, **bf)
+        self.q = torch.zeros(tmax, nh, 128, **bf)
+        self.attn = torch.zeros(tmax, nh, 128, **bf)
+        self.h = torch.zeros(tmax, F, **bf)
+        self.tmp = torch.zeros(tmax, H, **bf)
+        self.qkv = torch.zeros(tmax, (nh + 2 * nkv) * 128, **bf)
+        self.part = math.ceil(runner.max_model_len / 32) * 32
+
+    def _meta(self, name):
+        o, k = self.off[name]
+        return self.dev_meta[o:o + k]
+
+    def views(self, tb: int) -> dict:
+        nwb = tb // PREFILL_TILE + self.ns
+        d = {"ids": self._meta("ids")[:tb], "pos": self._meta("pos")[:tb], "slots": self._meta("slots")[:tb],
+             "qs": self._meta("qs"), "ql": self._meta("ql"), "ctx": self._meta("ctx"),
+             "ws": self._meta("ws")[:nwb], "wt": self._meta("wt")[:nwb],
+             "bt": self._meta("bt").view(self.ns + 1, self.mb), "part": self.part}
+        d.update(resid=self.resid[:tb], x=self.x[:tb], q=self.q[:tb], attn=self.attn[:tb], h=self.h[:tb],
+                 tmp=self.tmp[:tb], qkv=self.qkv[:tb])
+        return d
+
+    def _fill(self, buf: torch.Tensor, seqs: list, tb: int):
+        a = buf.numpy()
+        a[:] = 0
+        o = self.off
+        ids, pos, slots = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("ids", "pos", "slots"))
+        qs, ql, ctx = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("qs", "ql", "ctx"))
+        ws, wt = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("ws", "wt"))
+        bt = a[o["bt"][0]:o["bt"][0] + o["bt"][1]].reshape(self.ns + 1, self.mb)
+        slots[:] = -1
+        q_start, q_len, items = [], [], []
+        row = 0
+        for i, s in enumerate(seqs):
+            n = len(s.tokens)
+            q_start.append(row)
+            q_len.append(n)
+            p = s.start_pos + np.arange(n)
+            ids[row:row + n] = s.tokens
+            pos[row:row + n] = p
+            table = np.asarray(s.block_table, dtype=np.int64)
+            slots[row:row + n] = table[p // PAGE] * PAGE + p % PAGE
+            bt[i, :len(s.block_table)] = s.block_table
+            qs[i], ql[i], ctx[i] = row, n, s.start_pos + n
+            # flash prefill: heaviest (most keys) 64-query tiles first (as _prefill_meta)
+            items += [(-(s.start_pos + min(n, (t + 1) * PREFILL_TILE)), i, t)
+                      for t in range(math.ceil(n / PREFILL_TILE))]
+            row += n
+        items.sort()
+        ws[:] = self.ns  # padded items -> the empty sequence
+        for k, (_key, i, t) in enumerate(items):
+            ws[k], wt[k] = i, t
+        return q_start, q_len
+
+    def upload(self, seqs: list, tb: int):
+        """Metadata of `seqs` into the static buffers (stream-ordered before the replay that follows)."""
+        k = self.flip
+        self.flip ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()  # that pinned buffer's previous copy has been consumed
+        q_start, q_len = self._fill(self.host[k], seqs, tb)
+        self.dev_meta.copy_(self.host[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return q_start, q_len
+
+    def upload_padding(self):
+        self.upload([], self.tmax)

@@ -145,6 +145,17 @@ def decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_bloc
         ref.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
 
 
+def prefetch(t, sink, nbytes: int = -1, wgs: int = 256):
+    """Pull the first `nbytes` of `t` into the GPU's Infinity Cache ahead of the kernel that streams it (HIP only;
+    a no-op elsewhere).  `sink`: int32 [1024] scratch (prefetch_sink())."""
+    if _hip(t):
+        torch.ops.dsse.prefetch(t, sink, nbytes, wgs)
+
+
+def prefetch_sink(device):
+    return torch.zeros(1024, dtype=torch.int32, device=device)
+
+
 def ring_advance(counter):
     if _hip(counter):
         torch.ops.dsse.ring_advance(counter)

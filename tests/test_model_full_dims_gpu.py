@@ -136,3 +136,39 @@ def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B):
         first = int(r.ring[(int(r.ring_counter.item()) - 2) % r.ring.shape[0], B + j])
         ref, _ = reference_forward(CFG, std, torch.tensor(p + [first], device=gpu))
         _compare(ref[-1], r.logits[B + j], f"new sequence {j} first decode step")
+
+
+def test_prefill_graph_matches_eager(model, gpu):
+    """Prefill batches of <= 16 sequences replay a captured graph of their row bucket (padded rows: slot -1, work
+    items on the empty sequence): the K/V pages it writes and the first tokens it samples equal the eager pass."""
+    std, r = model
+    assert r.pf_graphs, "prefill graphs were not captured"
+    g = torch.Generator().manual_seed(77)
+    lens = [7, 60, 33, 1, 45]
+    prompts = [torch.randint(3, CFG.vocab_size, (n,), generator=g).tolist() for n in lens]
+    tables = [list(range(i * PAGES_PER_SEQ, (i + 1) * PAGES_PER_SEQ)) for i in range(len(lens))]
+    batches = [[PrefillSeq(i, p, 0, tables[i], True) for i, p in enumerate(prompts) if i != 1],
+               [PrefillSeq(1, prompts[1][:20], 0, tables[1], False)],
+               [PrefillSeq(1, prompts[1][20:], 20, tables[1], True)]]
+    r.temperature.zero_()
+    blocks = torch.tensor([b for t in tables for b in t], device=gpu)
+    out = {}
+    saved = dict(r.pf_graphs)
+    for mode in ("graph", "eager"):
+        r.pf_graphs = saved if mode == "graph" else {}
+        for li in range(CFG.num_layers):
+            r.kv.k[li].index_fill_(0, blocks, 0)
+            r.kv.v[li].index_fill_(0, blocks, 0)
+        r.ids.zero_()
+        for b in batches:
+            r.prefill(b, ring_row=0)
+        torch.cuda.synchronize()
+        out[mode] = ([r.kv.k[li].index_select(0, blocks).float() for li in range(CFG.num_layers)],
+                     [r.kv.v[li].index_select(0, blocks).float() for li in range(CFG.num_layers)],
+                     r.ids[:len(lens)].cpu().tolist())
+    r.pf_graphs = saved
+    for li in range(CFG.num_layers):
+        for kind, a, b in (("k", out["graph"][0][li], out["eager"][0][li]), ("v", out["graph"][1][li], out["eager"][1][li])):
+            err = (a - b).abs().max().item()
+            assert err <= 0.02 * max(1.0, b.abs().max().item()), f"layer {li} {kind}: max err {err}"
+    assert out["graph"][2] == out["eager"][2]

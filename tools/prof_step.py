@@ -15,7 +15,8 @@ import re
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*", "", name)
+    grid = re.search(r" grid=\S+$", name)
+    name = re.sub(r"\(.*", "", name) + (grid.group(0) if grid and "(" in name else "")
     name = name.replace("void ", "").replace("dsse::", "")
     return name[:70]
 
@@ -25,13 +26,16 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--marker", default="sample_pick")
     ap.add_argument("--last", type=int, default=6)
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid): separates the projections")
     args = ap.parse_args()
     rows = []
     if args.trace.endswith(".db"):  # rocprofv3's default SQLite output (ROCm 7)
         import sqlite3
 
         con = sqlite3.connect(args.trace)
-        rows = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+        q = "select start, end, name, grid_x, grid_y, workgroup_x from kernels"
+        rows = [(int(s), int(e), f"{n} grid={gx // max(1, wx)}x{gy}" if args.by_grid else n)
+                for s, e, n, gx, gy, wx in con.execute(q)]
     else:
         with open(args.trace) as f:
             for r in csv.DictReader(f):
