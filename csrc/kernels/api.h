@@ -92,7 +92,7 @@ hipError_t dsse_skinny_gemm(int mode, int mt, int nt, int kw, const void* X, int
                             const void* W, int K, int N, const dsse::GemmEpi* ep, hipStream_t st);
 hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd, int S, int partial_only, const void* X, int ldx, int M,
                             const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
-hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, const void* X, int ldx, int M,
+hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, int ring2, const void* X, int ldx, int M,
                           const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_wide(int mode, int mb, int rd, int S, int partial_only, const void* X, int ldx, int M, const void* W,
                           int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);

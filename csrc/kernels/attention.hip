@@ -453,7 +453,10 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     // 109 us, 5.9 TB/s).  (A next-page register prefetch variant cost 2-10 % and was removed.)
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
+    const int pd = p->pd == 2 && kwv <= 2 ? 2 : 1;  // DSSE_ATTN_PD=2: 2-page register ring (1 / 2 waves)
     if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, 1>), grid, dim3(512), 0, st, *p);
+    else if (kwv == 1 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 2>), grid, dim3(64), 0, st, *p);
+    else if (kwv == 2 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 2>), grid, dim3(128), 0, st, *p);
     else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 1>), grid, dim3(64), 0, st, *p);
     else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 1>), grid, dim3(128), 0, st, *p);
     else hipLaunchKernelGGL((paged_attention_kernel<1, 4, 1>), grid, dim3(256), 0, st, *p);

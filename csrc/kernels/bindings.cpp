@@ -150,6 +150,14 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
 // tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 7 / 8 (the 7-8-wave shapes; LDS; gate_up on 7
 // waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8, DSSE_S_RING7=0).  DSSE_S_RING=0 turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
 // waves 4.55 / 4.66 (gate_up 45.8 -> 43.5 us, LM head 52.5 -> 48.3; profiles/r2/ring_*.log).
+// Ring GEMM variant: DSSE_RING2 unset = the decoupled-look-ahead kernel (gemm_ring2) for 65-128 rows only
+// (128-stream step 6.19-6.22 vs 6.32-6.34 ms; at 33-64 rows 4.44 vs 4.40 ms: profiles/r3/ring2_ab.log,
+// step_p64_r{0,2}.md), 1 = every shape it is instantiated for, 0 = never.
+int ring2_for(int M) {
+  const int v = env_int("DSSE_RING2", -1);
+  return v == 0 ? 0 : (v == 1 ? 1 : (M > 64 ? 1 : 0));
+}
+
 hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const void* X, int M, const void* W, int K,
                          int N, const dsse::GemmEpi* ep, float* part) {
   const int ring = env_int("DSSE_S_RING", 1);
@@ -159,11 +167,12 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
     int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
     if (c.ring_nw > 0 && (N / 16) % c.ring_nw == 0 && M <= 64)
-      return dsse_gemm_ring(mode, c.ring_nw, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
+      return dsse_gemm_ring(mode, c.ring_nw, S, partial_only, ring2_for(M), X, K, M, W, K, N, ep, part, cur_stream());
     // QKV at 33-64 rows: 3 waves (384 tiles -> 128 x S 2 = 256 workgroups instead of 192; 64-stream step
     // 4.38-4.40 vs 4.41-4.42 ms, profiles/r2/qkv_ring3_ab.log; DSSE_QKV_RING3=0 = 4 waves)
     if (mode == dsse::kQkvRope && c.mt == 4 && env_int("DSSE_QKV_RING3", 1) && (N / 16) % 3 == 0) nw = 3;
-    if ((N / 16) % nw == 0) return dsse_gemm_ring(mode, nw, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
+    if ((N / 16) % nw == 0)
+      return dsse_gemm_ring(mode, nw, S, partial_only, ring2_for(M), X, K, M, W, K, N, ep, part, cur_stream());
   }
   return dsse_gemm_stream(mode, c.mt, c.nt, c.nw, c.rd, S, partial_only, X, K, M, W, K, N, ep, part, cur_stream());
 }
@@ -209,7 +218,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 9) {
+  if (cfg < 0 || cfg > 4) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
     // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
     // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
@@ -220,15 +229,15 @@ TCfg pick_tiled(int M, int N, int K) {
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
     const int narrow = env_int("DSSE_T_NARROW_CFG", 1);
-    if (narrow >= 0 && narrow <= 9 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
+    if (narrow >= 0 && narrow <= 4 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
     // wide projections of those buckets (gate_up, LM head): DSSE_T_WIDE_CFG (default by the rule above)
     const int wide = env_int("DSSE_T_WIDE_CFG", -1);
-    if (wide >= 0 && wide <= 9 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
+    if (wide >= 0 && wide <= 4 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
   }
   const int min_wgs = env_int("DSSE_T_MIN_WGS", 160);  // split K until this many workgroups (M <= 512)
   // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
-  static constexpr int kBM[10] = {256, 128, 256, 256, 256, 128, 256, 128, 256, 256};
-  static constexpr int kBN[10] = {128, 128, 64, 256, 256, 128, 64, 128, 128, 64};
+  static constexpr int kBM[5] = {256, 128, 256, 256, 256};
+  static constexpr int kBN[5] = {128, 128, 64, 256, 256};
   const int BM = kBM[cfg], BN = kBN[cfg];
   c.cfg = cfg;
   c.S = 1;

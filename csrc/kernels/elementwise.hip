@@ -300,7 +300,9 @@ extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const v
     }
     return hipGetLastError();
   }
-  const int nt = std::min(1024, H / 4);  // host-checked: H % 256 == 0, H <= 8192
+  // nit float4s per thread, nt threads: H == 4 nt nit exactly (H = 5120: 640 threads x 2), nt whole waves
+  const int nit = (H / 4 + 1023) / 1024, nt = H / 4 / nit;
+  if (nit > 2 || 4 * nt * nit != H || nt % 64 != 0) return hipErrorInvalidValue;
   switch (mode) {
     case 0: hipLaunchKernelGGL(rmsnorm_kernel<0>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;
     case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(M), dim3(nt), 0, st, resid, H, d, e, ids, wp, yp, eps, part, nsplit, M, vocab); break;

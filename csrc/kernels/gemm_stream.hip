@@ -451,7 +451,8 @@ static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf1
     return launch_r<MT_, NW_, ring_depth(MT_, NW_), MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   DSSE_R_CASE(8, 4)
-  DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 5) DSSE_R_CASE(4, 6) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
+  // (4, 5) is served by gemm_ring2 only: this kernel's 5-wave form wrote one wave's columns wrong (round 3)
+  DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 6) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
   DSSE_R_CASE(2, 4) DSSE_R_CASE(2, 7) DSSE_R_CASE(2, 8)
 #undef DSSE_R_CASE
   return hipErrorInvalidValue;
@@ -666,27 +667,25 @@ extern "C" hipError_t dsse_gemm_stream(int mode, int mt, int nt, int nw, int rd,
 // Ring variant (gemm_ring_kernel): 17 <= M <= 64 rows (16 MT-row MFMA tiles, MT = 2 / 4 by M), nw in {3, 4, 7, 8};
 // 65-128 rows (MT 8) with nw = 4;
 // K % (128 S) == 0, (N / 16) % nw == 0.
-extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, const void* X, int ldx, int M,
-                                     const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
+extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, int ring2, const void* X, int ldx,
+                                     int M, const void* W, int K, int N, const dsse::GemmEpi* ep, float* part,
                                      hipStream_t st) {
   using namespace dsse;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
   if (M > 128 || M < 17 || (M > 64 && nw != 4) || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
-  // ring2 (decoupled weight look-ahead): DSSE_RING2=1 (default), 0 = the single-ring kernel (also the fallback
-  // for a shape ring2 is not instantiated for)
-  static const bool r2 = [] {
-    const char* v = std::getenv("DSSE_RING2");
-    return !(v && v[0] == '0');
-  }();
+  // ring2: the decoupled-weight-look-ahead kernel (the single-ring kernel is the fallback for shapes it is not
+  // instantiated for); chosen by the caller (bindings.cpp ring2_for)
+  const bool r2 = ring2 != 0;
   auto run = [&](auto mode_tag, int s_, const GemmEpi* e_, float* p_) -> hipError_t {
     constexpr int MODE = decltype(mode_tag)::value;
-    if (r2) {
-      const hipError_t e2 = launch_r2_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
-      if (e2 != hipErrorInvalidValue) return e2;
-      (void)hipGetLastError();
-    }
-    return launch_r_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
+    // the preferred kernel, else the other one (a shape only one of them is instantiated for)
+    hipError_t e = r2 ? launch_r2_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st)
+                      : launch_r_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
+    if (e != hipErrorInvalidValue) return e;
+    (void)hipGetLastError();
+    return r2 ? launch_r_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st)
+              : launch_r2_mode<MODE>(nw, x, ldx, M, w, K, N, s_, *e_, p_, st);
   };
   if (S == 1 && !partial_only) {
     switch (mode) {

@@ -193,177 +193,6 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
       }
 }
 
-// ---- decode buckets (129-512 rows): X and W on separate LDS rings with separate loader waves (round 3).
-// The weight stream is HBM-latency-bound (~2.3 us loaded: a CU moves weight bytes in flight / 2.3 us,
-// profiles/r3/fillbench.md); in gemm_tiled_kernel X and W share each stage, so at 256 rows X's 16-32 KiB per
-// stage leave W 1-2 stages (16-32 KiB) in flight: 2.2-3.0 TB/s.  Here waves [0, LA) stage only X (NSA stages,
-// from L2, short ring) and waves [LA, NW) only W (NSB stages, deep ring); each loader wave's counted vmcnt covers
-// only its own kind, then one barrier per K step publishes both.  Stage reuse: the slot a loader refills right
-// after barrier t held step t-1, which every wave finished before that barrier.
-template <int WM, int WN, int MT, int NT, int LA, int NSA, int NSB>
-struct Tiled2Geom {
-  static constexpr int BM = WM * MT * 16, BN = WN * NT * 16, NW = WM * WN, NTHR = 64 * NW;
-  static constexpr int A_BYTES = BM * 128, B_BYTES = (BN / 16) * 2048;
-  static constexpr int A_PW = A_BYTES / 1024 / LA, B_PW = B_BYTES / 1024 / (NW - LA);  // instructions per loader
-  static_assert(A_BYTES % (1024 * LA) == 0 && B_BYTES % (1024 * (NW - LA)) == 0, "stage not divisible");
-  static constexpr size_t B_OFF = (size_t)NSA * A_BYTES, LDS = B_OFF + (size_t)NSB * B_BYTES;
-};
-
-template <int N>
-DEV void vm_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-// wait until at most y steps of PW loads each are outstanding (y wave-uniform, 0 <= y <= Y), then barrier
-template <int PW, int Y>
-DEV void wait_younger(int y) {
-  if constexpr (Y <= 0) {
-    vm_wait_barrier<0>();
-  } else {
-    if (y >= Y) vm_wait_barrier<Y * PW>();
-    else wait_younger<PW, Y - 1>(y);
-  }
-}
-
-template <int WM, int WN, int MT, int NT, int LA, int NSA, int NSB, int MODE>
-__global__ void __launch_bounds__(64 * WM * WN)
-gemm_tiled2_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
-                   GemmEpi ep, float* __restrict__ part) {
-  using G = Tiled2Geom<WM, WN, MT, NT, LA, NSA, NSB>;
-  static_assert(NSA >= 2 && NSA <= 4 && NSB >= 2 && NSB <= 8 && G::LDS <= 160 * 1024, "rings within the LDS");
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = w / WN, wn = w % WN;
-  const bool a_loader = w < LA;
-
-  const int nbm = (M + G::BM - 1) / G::BM, nbn = N / G::BN, ntile = nbm * nbn;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
-  const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
-  const int ks = lid / ntile, tl = lid % ntile;
-  constexpr int GM = 8;
-  const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
-  const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
-  const int m0 = bm * G::BM, n0 = bn * G::BN;
-  const int k0 = ks * Kr, nk = Kr >> 6;
-  const int KC = K >> 7;
-
-  // loader sources: an X loader covers A instructions [lw A_PW, (lw+1) A_PW) of a stage, a W loader B instructions
-  constexpr int PW = G::A_PW > G::B_PW ? G::A_PW : G::B_PW;
-  const bf16* src[PW];
-  int koff[PW], dst[PW];
-  const int lw = a_loader ? w : w - LA;
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int j = lw * (a_loader ? G::A_PW : G::B_PW) + i;
-    dst[i] = j * 1024;
-    if (a_loader) {
-      const int row = j * 8 + (lane >> 3);
-      const int p = (lane & 7) ^ a_swz(row);
-      src[i] = X + (size_t)min(m0 + min(row, G::BM - 1), M - 1) * ldx;
-      koff[i] = 32 * (p >> 1) + 8 * (p & 1);
-    } else {
-      src[i] = W + ((size_t)(n0 / 16 + (j >> 1)) * KC) * kTileChunk + (j & 1) * 512 + lane * 8;
-      koff[i] = 0;
-    }
-  }
-  auto issue = [&](int t) {  // this wave's share of step t
-    const int kk = k0 + 64 * t, c = kk >> 7, h = (kk >> 6) & 1;
-    if (a_loader) {
-      char* base = smem + (t % NSA) * G::A_BYTES;
-#pragma unroll
-      for (int i = 0; i < G::A_PW; ++i) glds16(src[i] + c * 128 + 16 * h + koff[i], base + dst[i]);
-    } else {
-      char* base = smem + G::B_OFF + (t % NSB) * G::B_BYTES;
-#pragma unroll
-      for (int i = 0; i < G::B_PW; ++i) glds16(src[i] + (size_t)c * kTileChunk + h * 1024, base + dst[i]);
-    }
-  };
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int a_off[MT][2];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = wm * MT * 16 + 16 * mt + r;
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp) a_off[mt][sp] = row * 128 + (((2 * g + sp) ^ a_swz(row)) << 4);
-  }
-
-  const int ahead = a_loader ? NSA - 1 : NSB - 1;  // steps issued before the loop
-  for (int t = 0; t < ahead && t < nk; ++t) issue(t);
-  for (int t = 0; t < nk; ++t) {
-    // this wave's share of step t landed (its younger steps t+1 .. stay in flight), then everyone's
-    const int younger = min(ahead - 1, nk - 1 - t);
-    if (a_loader) wait_younger<G::A_PW, NSA - 2>(younger);
-    else wait_younger<G::B_PW, NSB - 2>(younger);
-    if (t + ahead < nk) issue(t + ahead);
-    const char* As = smem + (t % NSA) * G::A_BYTES;
-    const char* Bs = smem + G::B_OFF + (t % NSB) * G::B_BYTES;
-    bf16x8 a0[MT], b0[NT], a1[MT], b1[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      b0[nt] = *reinterpret_cast<const bf16x8*>(Bs + (wn * NT + nt) * 2048 + lane * 16);
-      b1[nt] = *reinterpret_cast<const bf16x8*>(Bs + (wn * NT + nt) * 2048 + 1024 + lane * 16);
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      a0[mt] = *reinterpret_cast<const bf16x8*>(As + a_off[mt][0]);
-      a1[mt] = *reinterpret_cast<const bf16x8*>(As + a_off[mt][1]);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(a0[mt], b0[nt], acc[mt][nt]);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(a1[mt], b1[nt], acc[mt][nt]);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is reassigned
-
-  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
-  const int row0 = m0 + wm * MT * 16, tile0 = n0 / 16 + wn * NT;
-  if constexpr (MODE == kSiluMul) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) silu_epilogue4(ep, M, row0 + 16 * mt + 4 * g, tile0 + nt, r, acc[mt][nt]);
-    return;
-  }
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = acc[mt][nt][i];
-        const float partner = (MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
-        epilogue<MODE>(ep, part_ks, M, N, row0 + 16 * mt + 4 * g + i, tile0 + nt, r, v, partner);
-      }
-}
-
-template <int WM, int WN, int MT, int NT, int LA, int NSA, int NSB, int MODE>
-static hipError_t launch_t2(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
-                            float* part, hipStream_t st) {
-  using G = Tiled2Geom<WM, WN, MT, NT, LA, NSA, NSB>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tiled2_kernel<WM, WN, MT, NT, LA, NSA, NSB, MODE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
-    attr_set = true;
-  }
-  const int nbm = (M + G::BM - 1) / G::BM, nbn = N / G::BN;
-  hipLaunchKernelGGL((gemm_tiled2_kernel<WM, WN, MT, NT, LA, NSA, NSB, MODE>), dim3(nbm * nbn * S), dim3(G::NTHR),
-                     G::LDS, st, X, ldx, M, W, K, N, K / S, ep, part);
-  return hipGetLastError();
-}
-
 template <int WM, int WN, int MT, int NT, int NS, int FB, int MODE>
 static hipError_t launch_t(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
@@ -569,12 +398,6 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
     case 2: return launch_t<4, 1, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 waves
     case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
     case 4: return launch_phased<MODE>(X, ldx, M, W, K, N, S, ep, part, st);              // 256 x 256, phased
-    case 5: return launch_t<2, 2, 4, 4, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 128, 4 stages
-    case 6: return launch_t<4, 1, 4, 4, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 stages
-    // separate X / W rings (gemm_tiled2_kernel): <WM, WN, MT, NT, X-loader waves, X stages, W stages>
-    case 7: return launch_t2<2, 2, 4, 4, 2, 3, 6, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 128, 144 KiB
-    case 8: return launch_t2<4, 2, 4, 4, 4, 2, 6, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 128, 160 KiB
-    case 9: return launch_t2<4, 1, 4, 4, 2, 3, 8, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 160 KiB
   }
   return hipErrorInvalidValue;
 }
@@ -582,9 +405,9 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
 }  // namespace dsse
 
 // cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves),
-// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel),
-// 5 / 6 = cfg 1 / 2 with 4 LDS stages (two steps' DMA in flight across each barrier), 7 / 8 / 9 = 128 x 128 /
-// 256 x 128 / 256 x 64 with separate X and W rings (decode buckets: 4 / 4 / 6 W steps in flight).
+// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel).
+// (Round 3 also tried 4-stage rings and separate X / W loader rings for the 129-512-row decode buckets: all
+// slower in the 256-stream step, removed; profiles/r3/experiments_r3.md.)
 // Shape contract (checked by the caller): N % BN == 0, K % (64 S) == 0, the tiled weight layout (api.h).
 // S > 1: fp32 slabs [S, M, N] into `part`, reduced by launch_splitk_reduce unless partial_only.
 extern "C" hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M,

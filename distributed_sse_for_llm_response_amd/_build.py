@@ -107,11 +107,13 @@ def build_kernels(verbose: bool = False, force: bool = False, variant: str | Non
         ])
     _parallel(jobs, verbose)
     if force or _stale(out_so, objs):
+        tmp = out_so.with_name(out_so.name + ".tmp")
         _run([
-            HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out_so,
+            HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
             "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
             f"-Wl,-rpath,{torch_lib}",
         ], verbose)
+        os.replace(tmp, out_so)  # atomic: a concurrent reader (or a tree snapshot) never sees a half-written library
     return out_so
 
 

@@ -63,7 +63,11 @@ def test_watchdog_drops_readiness_during_a_stall_and_tracer_writes_steps(tmp_pat
             time.sleep(0.05)
         t.join(30)
         assert 503 in seen, seen                      # stalled -> not ready
-        assert request(H, port, "GET", "/readyz").status == 200  # recovered
+        # recovered: ready again once the engine loop beats within the threshold (a loaded host can take a while)
+        ready_by = time.time() + 10
+        while request(H, port, "GET", "/readyz").status != 200 and time.time() < ready_by:
+            time.sleep(0.05)
+        assert request(H, port, "GET", "/readyz").status == 200
         toks = [e.json() for e in out["r"].events if e.event == "token"]
         assert toks[-1]["done"]
         # the injected 1.5 s stall trips it; a loaded CI host (parallel workers) can starve the engine thread past

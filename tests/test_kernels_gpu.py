@@ -32,17 +32,14 @@ GEMM_CONFIGS = {
     "ring": {"DSSE_GEMM_IMPL": "2"},
     "ring-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
     "ring-nw8": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "8"},
+    "ring2-all": {"DSSE_GEMM_IMPL": "2", "DSSE_RING2": "1"},
+    "ring1-all": {"DSSE_GEMM_IMPL": "2", "DSSE_RING2": "0"},
     "wide-default": {"DSSE_GEMM_IMPL": "3"},
     "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
     "tiled-default": {"DSSE_GEMM_IMPL": "4"},
     "tiled-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "1", "DSSE_T_SPLIT": "2"},
     "tiled-256x64": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "2"},
     "tiled-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "3"},
-    "tiled-128-ns4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "5", "DSSE_T_SPLIT": "2"},
-    "tiled-256x64-ns4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "6"},
-    "tiled2-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "7", "DSSE_T_SPLIT": "2"},
-    "tiled2-256x128": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "8"},
-    "tiled2-256x64-split4": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "9", "DSSE_T_SPLIT": "4"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
@@ -154,12 +151,14 @@ def test_gemm_silu(gpu, tiles, M):
     _close(out, ref, 2e-2, 2e-2, "gemm_silu")
 
 
+@pytest.mark.parametrize("r2", ["0", "1"])
 @pytest.mark.parametrize("ring,nw", [("1", "4"), ("1", "7"), ("1", "8")])
 @pytest.mark.parametrize("M,K,S", [(33, 14336, "1"), (64, 14336, "4"), (48, 1536, "3"), (64, 4096, "2"),
                                    (17, 4096, "2"), (32, 14336, "4"), (100, 4096, "2"), (128, 14336, "4")])
-def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S):
-    """LDS-DMA ring GEMM (gemm_ring_kernel): chunk counts per workgroup that are not multiples of the ring depth,
-    split-K slabs reduced by the library, every epilogue against the fp32 reference."""
+def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S, r2):
+    """LDS-DMA ring GEMMs (gemm_ring_kernel; r2 = 1: gemm_ring2_kernel, the decoupled weight look-ahead): chunk
+    counts per workgroup that are not multiples of the ring depth, split-K slabs reduced by the library, every
+    epilogue against the fp32 reference."""
     if M > 64 and nw != "4":
         pytest.skip("65-128 rows: the ring runs the 4-wave shapes only (N = 16 * nw * 5 has no kernel there)")
     g = torch.Generator().manual_seed(M * 7 + K + int(nw))
@@ -167,7 +166,7 @@ def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S):
     x = _rand(M, K, dev=gpu, gen=g)
     w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
     for k, v in {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": ring, "DSSE_S_NW": nw, "DSSE_S_SPLIT": S,
-                 "DSSE_RING128": "1"}.items():
+                 "DSSE_RING128": "1", "DSSE_RING2": r2}.items():
         monkeypatch.setenv(k, v)
     ops.refresh_env()
     out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
@@ -248,12 +247,12 @@ def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     _close(vc, vr, 3e-2, 2e-2, "v cache")
 
 
-@pytest.mark.parametrize("cfg", ["auto", "tiled2-128-split2", "tiled2-256x128", "tiled2-256x64-split4"])
+@pytest.mark.parametrize("cfg", ["auto", "tiled-default", "tiled-128-split2", "tiled-256x64"])
 @pytest.mark.parametrize("M", [129, 192, 200, 256])
 def test_decode_bucket_epilogues(gpu, monkeypatch, cfg, M):
     """Every epilogue of the 129-256-row decode buckets (bf16 / fp32 store, residual add, SiLU*mul, QKV + RoPE +
-    K/V write, split-K slabs reduced by the norm) on the separate-X/W-ring tiled kernels, at row counts that are
-    not multiples of the tile height, against the fp32 reference."""
+    K/V write, split-K slabs reduced by the norm) on the tiled kernels, at row counts that are not multiples of
+    the tile height, against the fp32 reference."""
     for k, v in GEMM_CONFIGS[cfg].items():
         monkeypatch.setenv(k, v)
     ops.refresh_env()

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--configs", default="KWV=4;KWV=1")
     ap.add_argument("--target-wgs", default="512", help="flash-decoding partition targets to sweep")
+    ap.add_argument("--seq-pages", action="store_true", help="pages in cache order instead of a random permutation")
     args = ap.parse_args()
     ops.load_library(required=True)
     dev = torch.device("cuda", 0)
@@ -39,7 +40,8 @@ def main():
             copies = max(2, (600 << 20) // max(1, kv_bytes) + 1)
             ks = [torch.randn(total, args.hkv, 32, 128, device=dev, dtype=torch.bfloat16) for _ in range(copies)]
             vs = [torch.randn(total, args.hkv, 128, 32, device=dev, dtype=torch.bfloat16) for _ in range(copies)]
-            bt = torch.randperm(total, device=dev, dtype=torch.int64).to(torch.int32).view(B, npg)
+            order = torch.arange(total, device=dev) if args.seq_pages else torch.randperm(total, device=dev)
+            bt = order.to(torch.int32).view(B, npg)
             bt = torch.cat([bt, torch.zeros(B, 1, device=dev, dtype=torch.int32)], 1).contiguous()
             q = torch.randn(B, args.hq, 128, device=dev, dtype=torch.bfloat16)
             out = torch.empty_like(q)
