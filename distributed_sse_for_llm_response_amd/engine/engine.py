@@ -50,7 +50,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .kv_cache import PAGE, BlockAllocator, blocks_needed
-from .model_runner import RING_SIZE, ModelRunner, PrefillSeq, batch_buckets
+from .model_runner import PREFILL_GRAPH_SEQS, RING_SIZE, ModelRunner, PrefillSeq, batch_buckets
 
 
 @dataclass
@@ -399,6 +399,13 @@ class LLMEngine:
             self.r.move_slots(src, dst)
             self.stats["compactions"] += 1
 
+    def _mixed_fits(self, B: int, chunks: list) -> bool:
+        graphs = getattr(self.r, "mx_graphs", None)
+        if not graphs:  # no captured mixed steps (CPU, or DSSE_MIXED_GRAPHS=0): the eager mixed step takes any size
+            return True
+        entry = graphs.get(B)
+        return entry is not None and sum(len(c.tokens) for c in chunks) <= entry[0] and len(chunks) <= PREFILL_GRAPH_SEQS
+
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
         budget = self.prefill_budget if running_decode else self.idle_prefill_budget
@@ -469,7 +476,9 @@ class LLMEngine:
         ran = False
         dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
                and not s.stop_after_enqueue and not s.paused]
-        mixed = bool(chunks) and bool(dec) and self.mixed
+        B = next(b for b in batch_buckets(r.max_batch) if b >= max(s.slot for s in dec) + 1) if dec else 0
+        # a mixed step only when the chunks fit its captured graph (a starved prompt's big budget: separate passes)
+        mixed = bool(chunks) and bool(dec) and self.mixed and self._mixed_fits(B, chunks)
         if chunks:
             if not mixed:
                 r.prefill(chunks, ring_row=row)
@@ -477,8 +486,6 @@ class LLMEngine:
             producers += [(s.slot, s) for s in prefill_done]
             ran = True
         if dec:
-            hi = max(s.slot for s in dec) + 1
-            B = next(b for b in batch_buckets(r.max_batch) if b >= hi)
             if mixed:
                 r.mixed(B, chunks, ring_row=row)
                 self.stats["mixed_steps"] += 1

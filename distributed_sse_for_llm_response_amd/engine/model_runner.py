@@ -148,6 +148,7 @@ class ModelRunner:
         self.graph_pool = None
         self.pf_graphs = {}   # row bucket -> captured prefill graph
         self.pf = None        # static prefill buffers (allocated by capture)
+        self.mx_graphs = {}   # decode bucket B -> (chunk rows C, captured mixed prefill + decode graph)
 
     # ------------------------------------------------------------------ decode
     def decode_forward(self, B: int) -> None:
@@ -318,9 +319,9 @@ class ModelRunner:
             self.graphs[B] = g
         torch.cuda.synchronize(self.device)
         self._restore_state(saved)
-        self._capture_prefill()
+        self._capture_prefill(buckets)
 
-    def _capture_prefill(self) -> None:
+    def _capture_prefill(self, decode_buckets) -> None:
         """One graph per prefill row bucket over static buffers (_PrefillStatic); the metadata of a batch is
         uploaded into them before the replay.  Captured with all-padding metadata (every row slot -1: no K/V
         write; every work item on the empty sequence)."""
@@ -346,6 +347,38 @@ class ModelRunner:
                 self.graph_pool = g.pool()
             self.pf_graphs[tb] = g
         torch.cuda.synchronize(self.device)
+        if os.environ.get("DSSE_MIXED", "0") == "1" and os.environ.get("DSSE_MIXED_GRAPHS", "1") != "0":
+            self._capture_mixed(decode_buckets)
+
+    def mixed_chunk(self, B: int) -> int:
+        """Prompt rows a mixed step carries beside B decode rows: the rest of DSSE_MIXED_ROWS (default 128), at
+        least 64, in whole 64-row flash-prefill tiles."""
+        rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
+        return max(PREFILL_TILE, -(-(rows - B) // PREFILL_TILE) * PREFILL_TILE)
+
+    def _capture_mixed(self, decode_buckets) -> None:
+        """One graph per decode bucket B for the mixed step with C = mixed_chunk(B) prompt rows (ModelRunner.mixed;
+        captured like the decode step: the decode state restored afterwards)."""
+        buckets = [b for b in decode_buckets if b + self.mixed_chunk(b) <= self.pf.tmax]
+        if not buckets:
+            return
+        saved = self._snapshot_state()
+        self.pf.upload_padding()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for B in buckets:
+                self._mixed_layers(B, self.mixed_chunk(B))
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for B in sorted(buckets, reverse=True):
+            C = self.mixed_chunk(B)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._mixed_layers(B, C)
+            self.mx_graphs[B] = (C, g)
+        torch.cuda.synchronize(self.device)
+        self._restore_state(saved)
 
     def _snapshot_state(self):
         return [t.clone() for t in (self.ids, self.positions, self.ring, self.ring_counter)]
@@ -502,35 +535,64 @@ class ModelRunner:
         """ONE forward over the decode slots [0, B) and the prefill chunks `seqs` (rows B .. B+T-1): every weight
         byte streams once for both, so prompt tokens absorbed while streams decode cost the in-flight streams a
         bigger GEMM (M = B + T rows) instead of a whole extra prefill pass (decode-priority
-        chunked prefill).  Eager (the row count varies step to step).  Decode rows: QKV as a bf16 tile ->
-        vectorised RoPE + K/V write for all B + T rows -> decode attention (partitioned flash-decoding) for the B
-        decode rows and flash prefill for the chunk rows -> shared o / gate_up / down / norms -> the B decode
-        rows sample and commit exactly as the captured decode step does (ids, ring row, positions), the chunks
-        that finish a prompt sample their first token as prefill() does.  Same tokens as prefill() + decode()
-        (greedy: tests/test_mixed_step.py)."""
-        w, cfg, comm, dev = self.w, self.cfg, self.comm, self.device
-        nh, nkv, F = w.nh, w.nkv, w.ffn
-        H, eps = cfg.hidden_size, cfg.rms_eps
-        r = slice(0, B)
+        chunked prefill).  A captured graph of bucket B when the chunks fit its C = mixed_chunk(B) rows (metadata
+        uploaded into the static prefill buffers first), else eagerly.  Decode rows: QKV as a bf16 tile ->
+        vectorised RoPE + K/V write for all rows -> decode attention (partitioned flash-decoding) for the B decode
+        rows and flash prefill for the chunk rows -> shared o / gate_up / down / norms -> the B decode rows sample
+        and commit exactly as the captured decode step does (ids, ring row, positions), the chunks that finish a
+        prompt sample their first token as prefill() does.  Same tokens as prefill() + decode() (greedy:
+        tests/test_mixed_step.py)."""
+        T = sum(len(s.tokens) for s in seqs)
+        entry = self.mx_graphs.get(B)
+        if entry is not None and T <= entry[0] and len(seqs) <= PREFILL_GRAPH_SEQS:
+            q_start, q_len = self.pf.upload(seqs, entry[0], row0=B)
+            entry[1].replay()
+            self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)
+            return
+        w, dev = self.w, self.device
+        nh, nkv, F, H = w.nh, w.nkv, w.ffn, self.cfg.hidden_size
         T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs, row0=B)
+        M = B + T
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        d.update(resid=torch.empty(M, H, **f32), x=torch.empty(M, H, **bf), q=torch.empty(M, nh, 128, **bf),
+                 attn=torch.empty(M, nh, 128, **bf), h=torch.empty(M, F, **bf), tmp=torch.empty(M, H, **bf),
+                 qkv=torch.empty(M, (nh + 2 * nkv) * 128, **bf), part=math.ceil(max(ctx_len) / 32) * 32,
+                 mx_ids=torch.empty(M, dtype=torch.int32, device=dev),
+                 mx_pos=torch.empty(M, dtype=torch.int32, device=dev),
+                 mx_slots=torch.empty(M, dtype=torch.int32, device=dev))
+        self._mixed_body(B, T, d)
+        self._prefill_sample(seqs, d["x"], q_start, q_len, ring_row)
+
+    def _mixed_layers(self, B: int, C: int) -> None:
+        """The graph body of a mixed step: bucket B decode rows + C static prompt rows (_PrefillStatic)."""
+        d = self.pf.views(C)
+        M = B + C
+        for k in ("resid", "x", "q", "attn", "h", "tmp", "qkv"):
+            d[k] = getattr(self.pf, k)[:M]
+        d.update(mx_ids=self.pf.mx_ids[:M], mx_pos=self.pf.mx_pos[:M], mx_slots=self.pf.mx_slots[:M])
+        self._mixed_body(B, C, d)
+
+    def _mixed_body(self, B: int, T: int, d: dict) -> None:
+        """Decode prep, the forward over B + T rows, the decode rows' sampling and the ring advance (graph-capturable
+        when `d` holds static buffers)."""
+        w, cfg = self.w, self.cfg
+        nh, nkv = w.nh, w.nkv
+        eps = cfg.rms_eps
+        r = slice(0, B)
         M = B + T
         ops.decode_prep(self.active[r], self.positions[r], self.block_tables[r], self.slots[r], self.ctx_len[r],
                         self.q_len[r], self.kv.num_blocks)
-        f32 = dict(device=dev, dtype=torch.float32)
-        bf = dict(device=dev, dtype=torch.bfloat16)
-        resid = torch.empty(M, H, **f32)
-        x = torch.empty(M, H, **bf)
-        q = torch.empty(M, nh, 128, **bf)
-        attn = torch.empty(M, nh, 128, **bf)
-        h = torch.empty(M, F, **bf)
-        tmp = torch.empty(M, H, **bf)
-        qkv = torch.empty(M, (nh + 2 * nkv) * 128, **bf)
-        ids = torch.cat([self.ids[r], d["ids"]])
-        pos = torch.cat([self.positions[r], d["pos"]])
-        slots = torch.cat([self.slots[r], d["slots"]])
+        ids, pos, slots = d["mx_ids"], d["mx_pos"], d["mx_slots"]
+        ids[:B].copy_(self.ids[r])
+        ids[B:].copy_(d["ids"][:T])
+        pos[:B].copy_(self.positions[r])
+        pos[B:].copy_(d["pos"][:T])
+        slots[:B].copy_(self.slots[r])
+        slots[B:].copy_(d["slots"][:T])
+        resid, x, q, attn, h, tmp, qkv = (d[k] for k in ("resid", "x", "q", "attn", "h", "tmp", "qkv"))
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=ids)
         dpart, dnparts = decode_partitioning(B, nkv, self.max_model_len)
-        ppart = math.ceil(max(ctx_len) / 32) * 32
         nl = len(w.layers)
         for li, L in enumerate(w.layers):
             kc, vc = self.kv.k[li], self.kv.v[li]
@@ -540,14 +602,13 @@ class ModelRunner:
                                 self.ctx_len[r], self.work_seq[r], self.work_tile[r], attn[r], self.part_o,
                                 self.part_ml, dpart, dnparts)
             ops.paged_attention(2, q, kc, vc, d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"], d["wt"], attn,
-                                self.part_o, self.part_ml, ppart, 1)
+                                self.part_o, self.part_ml, d["part"], 1)
             self._resid_proj(attn.view(M, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
             ops.gemm_silu(x, L.wgu_t, h)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             self._resid_proj(h, L.wd_t, resid, w_next, x, tmp)
         ops.gemm_out(x[r], w.lm_head_t, self.logits[r])
         self._sample_commit(B)
-        self._prefill_sample(seqs, x, q_start, q_len, ring_row)
         ops.ring_advance(self.ring_counter)
 
 
@@ -587,6 +648,9 @@ class _PrefillStatic:
         self.tmp = torch.zeros(tmax, H, **bf)
         self.qkv = torch.zeros(tmax, (nh + 2 * nkv) * 128, **bf)
         self.part = math.ceil(runner.max_model_len / 32) * 32
+        # mixed steps: ids / positions / slots of the B decode rows followed by the chunk rows
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.mx_ids, self.mx_pos, self.mx_slots = (torch.zeros(tmax, **i32) for _ in range(3))
 
     def _meta(self, name):
         o, k = self.off[name]
@@ -602,7 +666,7 @@ class _PrefillStatic:
                  tmp=self.tmp[:tb], qkv=self.qkv[:tb])
         return d
 
-    def _fill(self, buf: torch.Tensor, seqs: list, tb: int):
+    def _fill(self, buf: torch.Tensor, seqs: list, tb: int, row0: int = 0):
         a = buf.numpy()
         a[:] = 0
         o = self.off
@@ -615,7 +679,7 @@ class _PrefillStatic:
         row = 0
         for i, s in enumerate(seqs):
             n = len(s.tokens)
-            q_start.append(row)
+            q_start.append(row0 + row)
             q_len.append(n)
             p = s.start_pos + np.arange(n)
             ids[row:row + n] = s.tokens
@@ -623,7 +687,7 @@ class _PrefillStatic:
             table = np.asarray(s.block_table, dtype=np.int64)
             slots[row:row + n] = table[p // PAGE] * PAGE + p % PAGE
             bt[i, :len(s.block_table)] = s.block_table
-            qs[i], ql[i], ctx[i] = row, n, s.start_pos + n
+            qs[i], ql[i], ctx[i] = row0 + row, n, s.start_pos + n
             # flash prefill: heaviest (most keys) 64-query tiles first (as _prefill_meta)
             items += [(-(s.start_pos + min(n, (t + 1) * PREFILL_TILE)), i, t)
                       for t in range(math.ceil(n / PREFILL_TILE))]
@@ -634,13 +698,14 @@ class _PrefillStatic:
             ws[k], wt[k] = i, t
         return q_start, q_len
 
-    def upload(self, seqs: list, tb: int):
-        """Metadata of `seqs` into the static buffers (stream-ordered before the replay that follows)."""
+    def upload(self, seqs: list, tb: int, row0: int = 0):
+        """Metadata of `seqs` into the static buffers (stream-ordered before the replay that follows); the rows of
+        the chunks start at `row0` of the activations (a mixed step: after the B decode rows)."""
         k = self.flip
         self.flip ^= 1
         if self.events[k] is not None:
             self.events[k].synchronize()  # that pinned buffer's previous copy has been consumed
-        q_start, q_len = self._fill(self.host[k], seqs, tb)
+        q_start, q_len = self._fill(self.host[k], seqs, tb, row0)
         self.dev_meta.copy_(self.host[k], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()

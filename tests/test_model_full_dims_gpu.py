@@ -34,7 +34,12 @@ def model():
     std = init_standard_weights(CFG, seed=3, device=gpu)
     w = convert_standard(CFG, std, device=gpu)
     r = ModelRunner(w, num_blocks=256 * PAGES_PER_SEQ + 8, max_batch=256, max_model_len=512, device=gpu)
-    r.capture(BUCKETS)  # before any prefill: the warm-up pass writes no KV (every slot inactive)
+    import os
+    os.environ["DSSE_MIXED"] = "1"  # capture the mixed prefill + decode graphs too
+    try:
+        r.capture(BUCKETS)  # before any prefill: the warm-up pass writes no KV (every slot inactive)
+    finally:
+        del os.environ["DSSE_MIXED"]
     return std, r
 
 
@@ -92,16 +97,21 @@ def test_full_dims_decode_logits_match_reference(model, gpu, B):
     assert not math.isnan(worst_cos)
 
 
+@pytest.mark.parametrize("mode", ["graph", "eager"])
 @pytest.mark.parametrize("B", [64, 128])
-def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B):
+def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B, mode):
     """ModelRunner.mixed (the engine's prefill-in-decode step): B decode rows + two new prompts' rows in one
-    forward; the decode rows' logits and the new prompts' first tokens against the fp32 reference, then the new
-    sequences decode in the next bucket."""
+    forward -- the captured graph of bucket B (prompts within its C rows, padded) or the eager step; the decode
+    rows' logits and the new prompts' first tokens against the fp32 reference, then the new sequences decode in
+    the next bucket."""
     std, r = model
+    assert B in r.mx_graphs, "mixed graphs were not captured"
     g = torch.Generator().manual_seed(1000 + B)
     n_new = 2
     prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
-               for _ in range(B + n_new)]
+               for _ in range(B)]
+    C = r.mx_graphs[B][0]
+    prompts += [torch.randint(3, CFG.vocab_size, (n,), generator=g).tolist() for n in (C // 2 - 5, C // 2 - 9)]
     tables = [list(range(i * PAGES_PER_SEQ, (i + 1) * PAGES_PER_SEQ)) for i in range(B + n_new)]
     r.block_tables.zero_()
     for i, bt in enumerate(tables):
@@ -114,8 +124,14 @@ def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B):
     r.temperature.zero_()
     gen = [[int(t)] for t in r.ids[:B].cpu()]
     new = [PrefillSeq(B + j, prompts[B + j], 0, tables[B + j], True) for j in range(n_new)]
-    r.mixed(B, new, ring_row=int(r.ring_counter.item()))
-    torch.cuda.synchronize()
+    saved = r.mx_graphs
+    if mode == "eager":
+        r.mx_graphs = {}
+    try:
+        r.mixed(B, new, ring_row=int(r.ring_counter.item()))
+        torch.cuda.synchronize()
+    finally:
+        r.mx_graphs = saved
     mixed_logits = r.logits[:B].clone()
     for i, t in enumerate(r.ids[:B].cpu()):
         gen[i].append(int(t))
