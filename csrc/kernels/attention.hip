@@ -22,6 +22,10 @@
 #include "api.h"
 #include "gemm_epilogue.h"
 
+#ifndef DSSE_ATTN_NT
+#define DSSE_ATTN_NT 1
+#endif
+
 namespace dsse {
 
 constexpr int kPage = 32;
@@ -72,19 +76,24 @@ paged_attention_kernel(AttnParams p) {
     const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
     return DSSE_IDX(cbt[i], p.num_blocks, 0);
   };
+  // decode (QW = 1): every K/V byte is read once, by one wave -> non-temporal loads (DSSE_ATTN_NT, default on:
+  // tools/kvbench.hip measured this access pattern at 6.3 TB/s nt vs 3.6 TB/s default policy); prefill tiles
+  // (QW > 1) share the lines through L1
+  constexpr bool NT = DSSE_ATTN_NT && QW == 1;
+  auto ldkv = [&](const bf16* a) { return NT ? ld_nt_bf16x8(a) : ld_bf16x8(a); };
   auto load_k = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4]) {
     const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;
     // K rows for keys kb + r and kb + 16 + r; k-step s of the 4 lane groups = 64 contiguous bytes of a row.
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      k0[s] = ld_bf16x8(kp + (size_t)r * kD + 32 * s + 8 * g);
-      k1[s] = ld_bf16x8(kp + (size_t)(16 + r) * kD + 32 * s + 8 * g);
+      k0[s] = ldkv(kp + (size_t)r * kD + 32 * s + 8 * g);
+      k1[s] = ldkv(kp + (size_t)(16 + r) * kD + 32 * s + 8 * g);
     }
   };
   auto load_v = [&](int page, bf16x8 (&vf)[8]) {
     const bf16* vp = p.v_cache + ((size_t)page * p.hkv + h) * kD * kPage;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_bf16x8(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
+    for (int dt = 0; dt < 8; ++dt) vf[dt] = ldkv(vp + (size_t)(16 * dt + r) * kPage + 8 * g);
   };
   auto load_page = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4], bf16x8 (&vf)[8]) {
     load_k(page, k0, k1);

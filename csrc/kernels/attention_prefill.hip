@@ -24,11 +24,7 @@
 #ifndef DSSE_PREFILL_GLDS
 #define DSSE_PREFILL_GLDS 1
 #endif
-// MFMA clusters at raised wave priority (s_setprio 1), so the SIMD's two waves drift out of phase: one in its
-// QK / PV MFMAs while the other runs its softmax (variant build "pfprio" for A/B)
-#ifndef DSSE_PREFILL_PRIO
-#define DSSE_PREFILL_PRIO 0
-#endif
+
 
 namespace dsse {
 
@@ -181,7 +177,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
       const char* vb = kb + kKBytes;
       // Sᵀ[key tile kt][query tile qt]
       f32x4 s4[4][2];
-      if (DSSE_PREFILL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
@@ -194,7 +189,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
         }
       }
-      if (DSSE_PREFILL_PRIO) __builtin_amdgcn_s_setprio(0);
       const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
       bf16x8 pf[2][2];  // [qt][page t]
 #pragma unroll
@@ -261,7 +255,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           }
       }
       // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
-      if (DSSE_PREFILL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -271,7 +264,6 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
 #pragma unroll
           for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
         }
-      if (DSSE_PREFILL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
   // stage s = blocks 2s, 2s + 1 in buffers 2 (s & 1) + {0, 1}.  Loads and stores are unconditional (pages clamp

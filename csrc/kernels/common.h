@@ -32,6 +32,7 @@ DEV f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 }
 
 DEV bf16x8 ld_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
 DEV bf16x8 zero_bf16x8() {
   bf16x8 z;
 #pragma unroll
