@@ -443,10 +443,12 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     // 10.20), two with a 2-page ring beat both (below)
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int nwg = grid.x * grid.y * grid.z;
-    // 2048+ workgroups (256 streams): 2 key-split waves, each with 2 KV pages in flight (9.82 / 9.87 ms/step vs
-    // 9.91 / 9.91 for one wave without look-ahead; 64 streams: look-ahead measured slower, 4.65-4.69 vs 4.63)
-    const int kwv = p->kwv ? p->kwv : (nwg >= 2048 ? 2 : (nwg >= 512 ? 2 : 4));
-    const int pd = p->pd ? p->pd : (nwg >= 2048 && kwv == 2 ? 2 : 1);
+    // 2048+ workgroups (256 streams): one wave per (sequence, kv head), one page in flight -- with the
+    // non-temporal K/V loads 9.70 / 9.71 ms/step vs 10.11 / 10.16 for 2 waves x 2 pages (the round-2 choice
+    // under default-policy loads) and 10.31 for 2 waves x 1 page (profiles/r3/r3n_ab256.log); 512-2047: 2 waves
+    // (128 streams 6.00-6.03 vs 6.23 with 4; 64 streams: look-ahead measured slower)
+    const int kwv = p->kwv ? p->kwv : (nwg >= 2048 ? 1 : (nwg >= 512 ? 2 : 4));
+    const int pd = p->pd ? p->pd : 1;
     hipError_t e;
     if (p->group == 1) e = launch_folded<1>(kwv, pd, grid, *p, st);
     else if (p->group == 2) e = launch_folded<2>(kwv, pd, grid, *p, st);

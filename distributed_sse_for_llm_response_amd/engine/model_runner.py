@@ -635,7 +635,9 @@ class _PrefillStatic:
             o += k
         self.words = o
         self.dev_meta = torch.zeros(o, dtype=torch.int32, device=dev)
-        self.host = [torch.zeros(o, dtype=torch.int32).pin_memory() for _ in range(2)]
+        pin = dev.type == "cuda"
+        self.host = [torch.zeros(o, dtype=torch.int32).pin_memory() if pin else torch.zeros(o, dtype=torch.int32)
+                     for _ in range(2)]
         self.events = [None, None]
         self.flip = 0
         f32 = dict(device=dev, dtype=torch.float32)
@@ -707,9 +709,10 @@ class _PrefillStatic:
             self.events[k].synchronize()  # that pinned buffer's previous copy has been consumed
         q_start, q_len = self._fill(self.host[k], seqs, tb, row0)
         self.dev_meta.copy_(self.host[k], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[k] = ev
+        if self.dev_meta.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[k] = ev
         return q_start, q_len
 
     def upload_padding(self):
