@@ -134,7 +134,7 @@ class _Drain:
 
 
 class LLMEngine:
-    def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 2048,
+    def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 512,
                  idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
                  pipeline_depth: int | None = None, max_pause_s: float = 30.0, deterministic: bool | None = None):
         self.r = runner

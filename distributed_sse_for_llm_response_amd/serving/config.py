@@ -61,7 +61,7 @@ class ServeConfig:
     seed: int = 0
     max_tokens: int = 256
     temperature: float = 1.0
-    prefill_budget: int = 2048
+    prefill_budget: int = 512
     tokenizer_path: str = ""
     weights_path: str = ""
     stub_tokens: int = 50
