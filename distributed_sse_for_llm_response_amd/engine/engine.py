@@ -169,7 +169,6 @@ class LLMEngine:
         self.on_itl = None
         # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
         self.mixed = os.environ.get("DSSE_MIXED", "0") == "1" and hasattr(runner, "mixed")
-        self.mixed_rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
         self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
         self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
 
@@ -419,7 +418,7 @@ class LLMEngine:
             if self.waiting:
                 oldest = min(oldest, self.waiting[0].enq_step)
             if self.step_no - oldest <= self.mixed_boost_steps:
-                budget = min(budget, max(self.mixed_min_tokens, self.mixed_rows - B))
+                budget = min(budget, max(self.mixed_min_tokens, self.r.mixed_chunk(B)))
         chunks, finished = [], []
         for s in self.slots:
             if s is None or s.state != "prefill" or s.aborted or budget <= 0:

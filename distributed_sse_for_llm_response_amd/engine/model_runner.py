@@ -351,8 +351,12 @@ class ModelRunner:
             self._capture_mixed(decode_buckets)
 
     def mixed_chunk(self, B: int) -> int:
-        """Prompt rows a mixed step carries beside B decode rows: the rest of DSSE_MIXED_ROWS (default 128), at
-        least 64, in whole 64-row flash-prefill tiles."""
+        """Prompt rows a mixed step carries beside B decode rows: DSSE_MIXED_CHUNK when set (a fixed chunk: a whole
+        short prompt rides in one step, so the weights stream once for its prefill and the decode step), else the
+        rest of DSSE_MIXED_ROWS (default 128), at least 64; in whole 64-row flash-prefill tiles."""
+        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "0"))
+        if fixed > 0:
+            return -(-fixed // PREFILL_TILE) * PREFILL_TILE
         rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
         return max(PREFILL_TILE, -(-(rows - B) // PREFILL_TILE) * PREFILL_TILE)
 
