@@ -115,22 +115,30 @@ class _Drain:
         else:
             self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32)
 
-    def issue(self, row: int, width: int):
+        # first tokens of prompts whose prefill pass precedes a decode step in the same engine step: drained as
+        # soon as the prefill pass is done, not after the decode step (their own buffers and events per ring row)
+        self.pf_host = torch.zeros_like(self.host)
+        if self.cuda:
+            self.pf_host = self.pf_host.pin_memory()
+            self.pf_events = [torch.cuda.Event() for _ in range(RING_SIZE)]
+
+    def issue(self, row: int, width: int, first: bool = False):
+        host = self.pf_host if first else self.host
         if not self.cuda:
-            self.host[row, :width] = self.r.ring[row, :width]
+            host[row, :width] = self.r.ring[row, :width]
             return
         self.stream.wait_stream(torch.cuda.current_stream(self.r.device))
         with torch.cuda.stream(self.stream):
-            self.host[row, :width].copy_(self.r.ring[row, :width], non_blocking=True)
-            self.events[row].record(self.stream)
+            host[row, :width].copy_(self.r.ring[row, :width], non_blocking=True)
+            (self.pf_events if first else self.events)[row].record(self.stream)
 
-    def ready(self, row: int) -> bool:
-        return (not self.cuda) or self.events[row].query()
+    def ready(self, row: int, first: bool = False) -> bool:
+        return (not self.cuda) or (self.pf_events if first else self.events)[row].query()
 
-    def wait(self, row: int):
+    def wait(self, row: int, first: bool = False):
         if self.cuda:
-            self.events[row].synchronize()
-        return self.host[row]
+            (self.pf_events if first else self.events)[row].synchronize()
+        return (self.pf_host if first else self.host)[row]
 
 
 class LLMEngine:
@@ -154,7 +162,9 @@ class LLMEngine:
         self.slots: list = [None] * runner.max_batch
         self.by_conv: dict = {}
         self.step_no = 0
-        self.inflight: deque = deque()  # (step, ring_row, producers [(slot, seq)], t_enqueue)
+        # (step, ring_row, producers [(slot, seq)], t_enqueue, first): first = an early first-token drain entry
+        # (Drain.issue(first=True)); the pipeline depth counts the other entries only
+        self.inflight: deque = deque()
         self.drain = _Drain(runner)
         self._rid = itertools.count(1)
         self._dirty_slots: set = set()
@@ -482,7 +492,12 @@ class LLMEngine:
             if not mixed:
                 r.prefill(chunks, ring_row=row)
             self.stats["prefill_tokens"] += sum(len(c.tokens) for c in chunks)
-            producers += [(s.slot, s) for s in prefill_done]
+            if not mixed and dec and prefill_done:
+                # a decode step follows on the stream: drain the first tokens now (TTFT minus one decode step)
+                self.drain.issue(row, max(s.slot for s in prefill_done) + 1, first=True)
+                self.inflight.append((self.step_no, row, [(s.slot, s) for s in prefill_done], t0, True))
+            else:
+                producers += [(s.slot, s) for s in prefill_done]
             ran = True
         if dec:
             if mixed:
@@ -504,25 +519,27 @@ class LLMEngine:
         if ran:
             width = max(sl for sl, _ in producers) + 1 if producers else 1
             self.drain.issue(row, width)
-            self.inflight.append((self.step_no, row, producers, t0))
+            self.inflight.append((self.step_no, row, producers, t0, False))
             self.ring_head += 1
             self.step_no += 1
         # ---- consume drained steps: keep `depth` steps in flight, process everything that is ready
         wait = 0.0  # blocked on a drain event (GPU time, not host work)
+        n_main = sum(1 for e in self.inflight if not e[4])
         while self.inflight:
-            st, rrow, prods, tq = self.inflight[0]
-            must = len(self.inflight) > self.depth or not ran
-            if not must and (self.deterministic or not block or not self.drain.ready(rrow)):
+            st, rrow, prods, tq, first = self.inflight[0]
+            must = n_main > self.depth or not ran
+            if not must and (self.deterministic or not block or not self.drain.ready(rrow, first)):
                 break
             tw = time.perf_counter()
-            toks = self.drain.wait(rrow)
+            toks = self.drain.wait(rrow, first)
+            n_main -= 0 if first else 1
             wait += time.perf_counter() - tw
             self.inflight.popleft()
             self._consume(toks, prods, events)
         # aborted sequences leave at this boundary
         for s in list(self.slots):
             if s is not None and s.aborted and s.state != "finished" and not any(
-                    s is p for _, _, prods, _ in self.inflight for _, p in prods):
+                    s is p for _, _, prods, _, _ in self.inflight for _, p in prods):
                 self._finish(s, events, reason="abort")
         self.stats["steps"] += 1
         dt = time.perf_counter() - t0
