@@ -177,6 +177,10 @@ class LLMEngine:
         self._pending: list = []  # events raised between steps (aborts of queued requests), returned by the next
         self.on_ttft = None
         self.on_itl = None
+        # on_flush(events): called with the events gathered so far before the step blocks on a drain that is not
+        # ready yet (the serving loop publishes them at once: early-drained first tokens do not wait for the
+        # decode step behind them); what is left is returned by step() as usual
+        self.on_flush = None
         # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
         self.mixed = os.environ.get("DSSE_MIXED", "0") == "1" and hasattr(runner, "mixed")
         self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
@@ -530,6 +534,9 @@ class LLMEngine:
             must = n_main > self.depth or not ran
             if not must and (self.deterministic or not block or not self.drain.ready(rrow, first)):
                 break
+            if self.on_flush is not None and events and not self.drain.ready(rrow, first):
+                self.on_flush(list(events))
+                events.clear()
             tw = time.perf_counter()
             toks = self.drain.wait(rrow, first)
             n_main -= 0 if first else 1

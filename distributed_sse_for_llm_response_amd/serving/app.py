@@ -89,6 +89,8 @@ class EngineLoop(threading.Thread):
         else:
             engine.on_ttft = rt.observe_ttft
             engine.on_itl = rt.observe_itl
+        if isinstance(engine, LLMEngine):  # (a TP leader post-processes the events of its step itself)
+            engine.on_flush = self._flush
 
     def _params(self, req) -> SamplingParams:
         d = self.engine.default_params
@@ -103,6 +105,12 @@ class EngineLoop(threading.Thread):
         """Flow-control transitions from the runtime plus pauses that outlived ``max_pause_s``."""
         ev = list(self.rt.pop_flow_events())
         return ev + [(c, False) for c in self.engine.expired_pauses()]
+
+    def _flush(self, events):
+        """Events the engine hands over before it blocks on a drain (LLMEngine.on_flush)."""
+        if self.faults.active:
+            events = self.faults.filter_events(events)
+        self.publish(events)
 
     def publish(self, events):
         if not events:
