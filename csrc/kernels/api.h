@@ -105,7 +105,7 @@ hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::Samp
                             hipStream_t st);
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
                         const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
-                        int vocab, void* sync, int sync_rows, hipStream_t st);
+                        int vocab, hipStream_t st);
 hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv, const int* positions,
                               const int* slots, const float2* rope, void* q_out, void* k_cache,
                               void* v_cache, int num_slots, int rope_len, hipStream_t st);

@@ -459,12 +459,9 @@ void gemm_qkv_rope(const Tensor& x, const Tensor& w, const Tensor& positions, co
   run_gemm(dsse::kQkvRope, x, w, ep);
 }
 
-// sync: optional int32 workspace of the row-split norm (elementwise.hip rmsnorm_split_kernel), 9 words per row
-// (four 8-byte granules + one generation word), owned by ONE caller (a model runner): two launches sharing it
-// must never run concurrently.  Zero-initialised once; never reset.
 void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::optional<Tensor>& delta,
              const c10::optional<Tensor>& embed, const c10::optional<Tensor>& ids,
-             const c10::optional<Tensor>& part, int64_t nsplit, const c10::optional<Tensor>& sync) {
+             const c10::optional<Tensor>& part, int64_t nsplit) {
   check_gpu(resid, "resid");
   check_gpu(w, "w");
   check_gpu(y, "y");
@@ -504,16 +501,8 @@ void rmsnorm(Tensor& resid, const Tensor& w, Tensor& y, double eps, const c10::o
     mode = 3;
     pptr = part->data_ptr<float>();
   }
-  void* sptr = nullptr;
-  int sync_rows = 0;
-  if (sync.has_value() && env_int("DSSE_NORM_SPLIT", 0)) {
-    check_gpu(*sync, "sync");
-    check_dtype(*sync, at::kInt, "sync");
-    sync_rows = (int)(sync->numel() / 9);
-    if (sync_rows >= M) sptr = sync->data_ptr();
-  }
   DSSE_CHECK_HIP(dsse_rmsnorm(mode, M, resid.data_ptr<float>(), H, dptr, eptr, iptr, w.data_ptr(),
-                              y.data_ptr(), (float)eps, pptr, (int)nsplit, vocab, sptr, sync_rows, cur_stream()));
+                              y.data_ptr(), (float)eps, pptr, (int)nsplit, vocab, cur_stream()));
 }
 
 void rope_kv_write(const Tensor& qkv, const Tensor& positions, const Tensor& slots, const Tensor& rope,
@@ -861,7 +850,7 @@ void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, do
                                  reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 10; }
+int64_t kernels_abi_version() { return 11; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -899,7 +888,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("gemm_qkv_rope(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
-        "Tensor? ids=None, Tensor? part=None, int nsplit=0, Tensor(c!)? sync=None) -> ()");
+        "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
   m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
   m.def("refresh_env() -> ()", &refresh_env);
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "

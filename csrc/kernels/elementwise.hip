@@ -94,97 +94,6 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
   }
 }
 
-// ---- K2, row-split form (decode): 4 workgroups per row -----------------------------------------
-// A decode batch has 64-256 rows, so one workgroup per row leaves 3/4 of the 256 CUs idle and each row's
-// (S + 1) x 16 KiB of slab + residual reads queue on one CU (rmsnorm_kernel<3>: 5.1 us per call at 64 rows,
-// profiles/decode_step_64_r2_final.md).  Here workgroup (m, q) owns columns [q H/4, (q+1) H/4) of row m: it adds
-// the slabs / delta into its quarter of the residual, publishes its partial sum of squares as ONE 8-byte {ss,
-// tag} granule (agent-scope relaxed store = global_store_dwordx2 sc1, untorn: MI355X_MICROARCH.md "Valid forms",
-// R2 granules), polls the row's four granules with sc1 loads, and normalises its quarter with the total summed
-// in quarter order (bit-identical on the four workgroups).  The tag is the row's call generation gen[m] + 1:
-// every workgroup of the row reads gen[m] before it publishes, and quarter 0 bumps gen[m] only after it has seen
-// all four granules, so no workgroup of the row can read the bumped value in the same call.  The four workgroups
-// of a row are consecutive block ids (dispatched together; the whole grid, <= 2048 workgroups of 256 threads,
-// fits the chip at once).  H / 16 threads per workgroup (H = 4096: 256).  A poll that exceeds kSpinLimit sleeps (~0.3 s) gives up with its own partial x 4
-// (wrong norm, recorded in the checked build) instead of hanging the GPU.
-constexpr int kNormSplit = 4;
-constexpr int kSpinLimit = 1 << 20;
-
-template <int MODE>
-__global__ void __launch_bounds__(512)
-rmsnorm_split_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta, const bf16* __restrict__ w,
-                     bf16* __restrict__ y, float eps, const float* __restrict__ part, int nsplit, int M,
-                     unsigned long long* __restrict__ gran, unsigned int* __restrict__ gen) {
-  const int m = blockIdx.x / kNormSplit, q = blockIdx.x % kNormSplit, tid = threadIdx.x;
-  const int i = q * (H / kNormSplit) + tid * 4;  // host: H == kNormSplit * 4 * blockDim.x
-  unsigned int g = 0;
-  if (tid == 0) g = __hip_atomic_load(gen + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + i);
-  float* rp = resid + (size_t)m * H + i;
-  float4 x = *reinterpret_cast<const float4*>(rp);
-  if constexpr (MODE == 1) {
-    const bf16x4 d = *reinterpret_cast<const bf16x4*>(delta + (size_t)m * H + i);
-    x.x += bf2f(d[0]); x.y += bf2f(d[1]); x.z += bf2f(d[2]); x.w += bf2f(d[3]);
-  }
-  if constexpr (MODE == 3) {
-    const float* p = part + (size_t)m * H + i;
-    const size_t slab = (size_t)M * H;
-    int s = 0;
-    for (; s + 4 <= nsplit; s += 4) {
-      const float4 d0 = *reinterpret_cast<const float4*>(p + (s + 0) * slab);
-      const float4 d1 = *reinterpret_cast<const float4*>(p + (s + 1) * slab);
-      const float4 d2 = *reinterpret_cast<const float4*>(p + (s + 2) * slab);
-      const float4 d3 = *reinterpret_cast<const float4*>(p + (s + 3) * slab);
-      x.x += (d0.x + d1.x) + (d2.x + d3.x);
-      x.y += (d0.y + d1.y) + (d2.y + d3.y);
-      x.z += (d0.z + d1.z) + (d2.z + d3.z);
-      x.w += (d0.w + d1.w) + (d2.w + d3.w);
-    }
-    for (; s < nsplit; ++s) {
-      const float4 d = *reinterpret_cast<const float4*>(p + s * slab);
-      x.x += d.x; x.y += d.y; x.z += d.z; x.w += d.w;
-    }
-  }
-  if constexpr (MODE != 0) *reinterpret_cast<float4*>(rp) = x;
-  float ss = wave_sum(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
-  __shared__ float red[8];
-  __shared__ float tot_s;
-  if ((tid & 63) == 0) red[tid >> 6] = ss;
-  __syncthreads();
-  if (tid == 0) {
-    float mine = 0.f;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) mine += red[k];
-    unsigned long long* row = gran + (size_t)m * kNormSplit;
-    __hip_atomic_store(row + q, ((unsigned long long)g << 32) | __float_as_uint(mine), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    float part_ss[kNormSplit];
-    bool ok = true;
-    for (int k = 0; k < kNormSplit; ++k) {
-      unsigned long long v = __hip_atomic_load(row + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int spins = 0;
-      while ((unsigned int)(v >> 32) != g && ++spins < kSpinLimit) {
-        __builtin_amdgcn_s_sleep(1);
-        v = __hip_atomic_load(row + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      ok = ok && (unsigned int)(v >> 32) == g;
-      part_ss[k] = k == q ? mine : __uint_as_float((unsigned int)v);
-    }
-    float t = 0.f;
-    for (int k = 0; k < kNormSplit; ++k) t += ok ? part_ss[k] : mine;
-    (void)DSSE_IDX(ok ? 0 : 1, 1, 0);  // checked build: a timed-out rendezvous is recorded
-    tot_s = t;
-    if (q == 0) __hip_atomic_store(gen + m, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const float inv = rsqrtf(tot_s / (float)H + eps);
-  bf16x4 o;
-  o[0] = f2bf(x.x * inv * bf2f(wv[0]));
-  o[1] = f2bf(x.y * inv * bf2f(wv[1]));
-  o[2] = f2bf(x.z * inv * bf2f(wv[2]));
-  o[3] = f2bf(x.w * inv * bf2f(wv[3]));
-  *reinterpret_cast<bf16x4*>(y + (size_t)m * H + i) = o;
-}
-
 // ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
 // qkv: [T, (hq + 2 hkv) * 128] bf16 in the engine's permuted column order (inside each 16-column
 // tile j of a head: columns 0..7 = dims 8j..8j+7, columns 8..15 = dims 64+8j..64+8j+7).
@@ -280,26 +189,12 @@ using namespace dsse;
 
 extern "C" hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta,
                                    const void* embed, const int* ids, const void* w, void* y,
-                                   float eps, const float* part, int nsplit, int vocab, void* sync, int sync_rows,
-                                   hipStream_t st) {
+                                   float eps, const float* part, int nsplit, int vocab, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   const bf16* d = reinterpret_cast<const bf16*>(delta);
   const bf16* e = reinterpret_cast<const bf16*>(embed);
   const bf16* wp = reinterpret_cast<const bf16*>(w);
   bf16* yp = reinterpret_cast<bf16*>(y);
-  // row-split form: a sync workspace for >= M rows ([sync_rows][4] 8-byte granules, then sync_rows generations)
-  if (sync != nullptr && mode != 2 && M <= sync_rows && H % (kNormSplit * 4 * 64) == 0 && H / 16 <= 512) {
-    auto* gran = reinterpret_cast<unsigned long long*>(sync);
-    auto* gen = reinterpret_cast<unsigned int*>(gran + (size_t)sync_rows * kNormSplit);
-    const dim3 grid(M * kNormSplit), block(H / (kNormSplit * 4));
-    switch (mode) {
-      case 0: hipLaunchKernelGGL(rmsnorm_split_kernel<0>, grid, block, 0, st, resid, H, d, wp, yp, eps, part, nsplit, M, gran, gen); break;
-      case 1: hipLaunchKernelGGL(rmsnorm_split_kernel<1>, grid, block, 0, st, resid, H, d, wp, yp, eps, part, nsplit, M, gran, gen); break;
-      case 3: hipLaunchKernelGGL(rmsnorm_split_kernel<3>, grid, block, 0, st, resid, H, d, wp, yp, eps, part, nsplit, M, gran, gen); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
   // nit float4s per thread, nt threads: H == 4 nt nit exactly (H = 5120: 640 threads x 2), nt whole waves
   const int nit = (H / 4 + 1023) / 1024, nt = H / 4 / nit;
   if (nit > 2 || 4 * nt * nit != H || nt % 64 != 0) return hipErrorInvalidValue;

@@ -136,9 +136,6 @@ class ModelRunner:
         ws = max(decode_partitioning(b, nkv, max_model_len)[1] * b for b in batch_buckets(Bm))
         self.part_o = torch.zeros(max(1, ws) * nkv * 16 * 128, device=dev, dtype=torch.float32)
         self.part_ml = torch.zeros(max(1, ws) * nkv * 16 * 2, device=dev, dtype=torch.float32)
-        # row-split RMSNorm rendezvous workspace (decode rows; ops.rmsnorm sync=): owned by this runner, whose
-        # launches are all on one stream
-        self.norm_sync = ops.norm_sync_workspace(Bm, dev) if dev.type == "cuda" else None
         # TP decode: the residual all-reduces on the fused IPC kernel (parallel/comm.py IpcAllReduce), RCCL otherwise
         self.fast_ar_reason = self.comm.enable_ipc_allreduce(dev, Bm, H) if self.comm.size > 1 else "tp=1"
         if self.comm.size > 1 and self.comm.rank == 0:
@@ -170,18 +167,18 @@ class ModelRunner:
             self._qkv_attention(li, L, B, x, part, nparts)
             if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
                 ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
-                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
+                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
             else:
                 ops.gemm_out(self.attn[r], L.wo_t, self.tmp[r])
-                comm.all_reduce_rmsnorm(self.tmp[r], resid, L.ffn_norm, x, eps, sync=self.norm_sync)
+                comm.all_reduce_rmsnorm(self.tmp[r], resid, L.ffn_norm, x, eps)
             ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             if comm.size == 1:
                 ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
-                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
+                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
             else:
                 ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
-                comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps, sync=self.norm_sync)
+                comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps)
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
@@ -230,10 +227,10 @@ class ModelRunner:
         eps = self.cfg.rms_eps
         if self.comm.size == 1:
             ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
-            ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns, sync=self.norm_sync)
+            ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns)
         else:
             ops.gemm_out(a, wt, tmp)
-            self.comm.all_reduce_rmsnorm(tmp, resid, norm_w, x, eps, sync=self.norm_sync)
+            self.comm.all_reduce_rmsnorm(tmp, resid, norm_w, x, eps)
 
     def _sample_commit(self, B: int) -> None:
         """Candidates per (row, vocab chunk) on each rank -> (TP: all-gather, 8 B per candidate) -> pick."""

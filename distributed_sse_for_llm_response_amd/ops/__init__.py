@@ -108,20 +108,12 @@ def refresh_env() -> None:
         torch.ops.dsse.refresh_env()
 
 
-def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0, sync=None):
-    """resid (+= delta | sum of `nsplit` split-K slabs in `part` | = embed[ids]); y = rmsnorm(resid) * w.
-
-    `sync` (HIP only): an int32 workspace of 9 words per row (``norm_sync_workspace``) owned by one caller; with
-    it each row is normalised by four workgroups that exchange partial sums (elementwise.hip rmsnorm_split_kernel)."""
+def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nsplit=0):
+    """resid (+= delta | sum of `nsplit` split-K slabs in `part` | = embed[ids]); y = rmsnorm(resid) * w."""
     if _hip(resid):
-        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit, sync)
+        torch.ops.dsse.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
     else:
         ref.rmsnorm(resid, w, y, eps, delta, embed, ids, part, nsplit)
-
-
-def norm_sync_workspace(rows: int, device) -> torch.Tensor:
-    """Zeroed workspace for the row-split RMSNorm of up to `rows` rows (never reset afterwards)."""
-    return torch.zeros(9 * rows, dtype=torch.int32, device=device)
 
 
 def rope_kv_write(qkv, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv):

@@ -88,7 +88,7 @@ class TPComm:
         self.fast_ar = ar
         return why
 
-    def all_reduce_rmsnorm(self, tmp, resid, norm_w, y, eps: float, sync=None) -> None:
+    def all_reduce_rmsnorm(self, tmp, resid, norm_w, y, eps: float) -> None:
         """resid += all_reduce(tmp); y = rmsnorm(resid) * norm_w (the TP decode residual step)."""
         from .. import ops
 
@@ -96,7 +96,7 @@ class TPComm:
             self.fast_ar(tmp, resid, norm_w, y, eps)
             return
         self.all_reduce(tmp)
-        ops.rmsnorm(resid, norm_w, y, eps, delta=tmp, sync=sync)
+        ops.rmsnorm(resid, norm_w, y, eps, delta=tmp)
 
 
 class IpcAllReduce:
