@@ -229,7 +229,13 @@ TCfg pick_tiled(int M, int N, int K) {
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
     const int narrow = env_int("DSSE_T_NARROW_CFG", 1);
-    if (narrow >= 0 && narrow <= 4 && N <= 8192 && M > 128 && M <= kMaxDecodeM) cfg = narrow;
+    if (narrow >= 0 && narrow <= 4 && N <= 8192 && M > 128 && M <= 256) cfg = narrow;
+    // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: per shape from the
+    // tools/bench_gemm_tiled.py sweep over every config (profiles/r3/prefill_chunk_gemm.md): 257-512 rows down
+    // (K 14336) on the phased 256x256 tile split 8 ways (69 vs 92 us), qkv / o on 256x128 (46 / 33 vs 49 / 35
+    // us); 513-1024 rows N <= 4096 (o, down) on 128x128 (50 / 153 vs 65 / 205 us)
+    if (env_int("DSSE_T_NARROW_CFG", -1) < 0 && N <= 8192 && M > 256 && M <= 512) cfg = K > 8192 ? 4 : 0;
+    if (env_int("DSSE_T_NARROW_CFG", -1) < 0 && N <= 4096 && M > 512 && M <= 1024) cfg = 1;
     // wide projections of those buckets (gate_up, LM head): DSSE_T_WIDE_CFG (default by the rule above)
     const int wide = env_int("DSSE_T_WIDE_CFG", -1);
     if (wide >= 0 && wide <= 4 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
