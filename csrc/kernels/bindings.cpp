@@ -228,7 +228,11 @@ TCfg pick_tiled(int M, int N, int K) {
     // narrow projections of the wide decode buckets (N <= 8192, 128 < M <= 512: qkv / o / down at 192-256
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
-    const int narrow = env_int("DSSE_T_NARROW_CFG", 1);
+    // round 3 (profiles/r3/decode_bucket_gemm.md): in the 129-192-row bucket qkv (N 6144) and down (K 14336) on
+    // 256x128 -- alone 27 vs 30 us and 42 vs 50 us, 192-stream step 8.30 vs 8.43 ms; at 193-256 rows the same
+    // change measured 9.81 vs 9.71 ms per step (twice the split-K slabs for the consuming norm / attention),
+    // so 128x128 stays there
+    const int narrow = env_int("DSSE_T_NARROW_CFG", (M <= 192 && !(N <= 4096 && K <= 4096)) ? 0 : 1);
     if (narrow >= 0 && narrow <= 4 && N <= 8192 && M > 128 && M <= 256) cfg = narrow;
     // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: per shape from the
     // tools/bench_gemm_tiled.py sweep over every config (profiles/r3/prefill_chunk_gemm.md): 257-512 rows down
