@@ -1,7 +1,7 @@
 """Tiled LDS-DMA GEMM (gemm_tiled.hip) vs the library GEMM (torch.matmul -> hipBLASLt) at the Mistral-7B
 prefill and wide-decode shapes, on the same random bf16 operands, interleaved rounds in one process.
 
-    python tools/bench_gemm_tiled.py [--M 8192,2048,256] [--cfg 0,1,2] [--iters 20] [--rounds 3]
+    python tools/bench_gemm_tiled.py [--M 8192,2048,256] [--cfg auto,0,1,2] [--iters 20] [--rounds 3]
 
 Prints one line per (shape, M, kernel) with the median time and TFLOP/s, then a JSON summary.
 """
@@ -57,18 +57,17 @@ def main():
             if not args.no_library:
                 arms["library"] = lambda: torch.matmul(x, w.t(), out=out)
             for cfg in args.cfg.split(","):
-                def run(cfg=cfg):
-                    os.environ["DSSE_GEMM_IMPL"] = "4"
-                    os.environ["DSSE_T_CFG"] = cfg
-                    ops.refresh_env()
-                    return lambda: ops.gemm_out(x, wt, out)
-                arms[f"tiled{cfg}"] = run()
+                # "auto": the engine's default dispatch for this shape (any kernel family); else a gemm_tiled cfg
+                arms["auto" if cfg == "auto" else f"tiled{cfg}"] = lambda: ops.gemm_out(x, wt, out)
             times = {k: [] for k in arms}
             for _ in range(args.rounds):
                 for k, fn in arms.items():
+                    os.environ.pop("DSSE_GEMM_IMPL", None)
+                    os.environ.pop("DSSE_T_CFG", None)
                     if k.startswith("tiled"):
+                        os.environ["DSSE_GEMM_IMPL"] = "4"
                         os.environ["DSSE_T_CFG"] = k[5:]
-                        ops.refresh_env()
+                    ops.refresh_env()
                     times[k].append(timeit(fn, args.iters))
             for k, ts in times.items():
                 us = sorted(ts)[len(ts) // 2]
