@@ -50,7 +50,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .kv_cache import PAGE, BlockAllocator, blocks_needed
-from .model_runner import PREFILL_GRAPH_SEQS, RING_SIZE, ModelRunner, PrefillSeq, batch_buckets
+from .model_runner import PREFILL_GRAPH_SEQS, RING_SIZE, ModelRunner, PrefillSeq, batch_buckets, mixed_min_b, mixed_mode
 
 
 @dataclass
@@ -185,7 +185,8 @@ class LLMEngine:
         # decode step behind them); what is left is returned by step() as usual
         self.on_flush = None
         # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
-        self.mixed = os.environ.get("DSSE_MIXED", "0") == "1" and hasattr(runner, "mixed")
+        self.mixed = mixed_mode() != "0" and hasattr(runner, "mixed")
+        self.mixed_min_b = mixed_min_b()  # "auto": mixed steps only from this decode bucket up
         self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
         self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
 
@@ -415,6 +416,10 @@ class LLMEngine:
             self.r.move_slots(src, dst)
             self.stats["compactions"] += 1
 
+    def _decode_bucket(self) -> int:
+        hi = max((s.slot for s in self.slots if s is not None and s.state == "decode"), default=-1) + 1
+        return next(b for b in batch_buckets(self.r.max_batch) if b >= hi) if hi > 0 else 0
+
     def _mixed_fits(self, B: int, chunks: list) -> bool:
         graphs = getattr(self.r, "mx_graphs", None)
         if not graphs:  # no captured mixed steps (CPU, or DSSE_MIXED_GRAPHS=0): the eager mixed step takes any size
@@ -425,7 +430,7 @@ class LLMEngine:
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
         budget = self.prefill_budget if running_decode else self.idle_prefill_budget
-        if running_decode and self.mixed:
+        if running_decode and self.mixed and self._decode_bucket() >= self.mixed_min_b:
             # the chunk rides in the decode step: keep B + chunk near the next row bucket, unless a prompt has
             # waited too long (counted in steps: identical on every TP rank)
             hi = max((s.slot for s in self.slots if s is not None and s.state == "decode"), default=-1) + 1
@@ -494,7 +499,7 @@ class LLMEngine:
                and not s.stop_after_enqueue and not s.paused]
         B = next(b for b in batch_buckets(r.max_batch) if b >= max(s.slot for s in dec) + 1) if dec else 0
         # a mixed step only when the chunks fit its captured graph (a starved prompt's big budget: separate passes)
-        mixed = bool(chunks) and bool(dec) and self.mixed and self._mixed_fits(B, chunks)
+        mixed = bool(chunks) and bool(dec) and self.mixed and B >= self.mixed_min_b and self._mixed_fits(B, chunks)
         if chunks:
             if not mixed:
                 r.prefill(chunks, ring_row=row)

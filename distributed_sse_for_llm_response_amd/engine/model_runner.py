@@ -51,6 +51,19 @@ PREFILL_GRAPH_SEQS = 16  # sequences per captured prefill batch (more: eager)
 DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
 
 
+def mixed_mode() -> str:
+    """DSSE_MIXED: "0" = prompt chunks as separate prefill passes, "1" = mixed prefill + decode steps whenever
+    streams decode, "auto" = mixed steps only for decode buckets of >= DSSE_MIXED_MIN_B rows (default 192): at
+    that load a separate pass per prompt chunk (a whole extra weight stream) pushes the engine into bigger
+    buckets and longer steps, while below it separate passes keep TTFT 30-35 % lower
+    (profiles/r3/serving_arrivals.md)."""
+    return os.environ.get("DSSE_MIXED", "0")
+
+
+def mixed_min_b() -> int:
+    return int(os.environ.get("DSSE_MIXED_MIN_B", "192" if mixed_mode() == "auto" else "0"))
+
+
 def batch_buckets(max_batch: int):
     """Captured decode batch sizes: powers of two up to 64, then every 64 (less padding at 65-256 streams)."""
     out, b = [], 1
@@ -344,14 +357,14 @@ class ModelRunner:
                 self.graph_pool = g.pool()
             self.pf_graphs[tb] = g
         torch.cuda.synchronize(self.device)
-        if os.environ.get("DSSE_MIXED", "0") == "1" and os.environ.get("DSSE_MIXED_GRAPHS", "1") != "0":
-            self._capture_mixed(decode_buckets)
+        if mixed_mode() != "0" and os.environ.get("DSSE_MIXED_GRAPHS", "1") != "0":
+            self._capture_mixed([b for b in decode_buckets if b >= mixed_min_b()])
 
     def mixed_chunk(self, B: int) -> int:
         """Prompt rows a mixed step carries beside B decode rows: DSSE_MIXED_CHUNK when set (a fixed chunk: a whole
         short prompt rides in one step, so the weights stream once for its prefill and the decode step), else the
         rest of DSSE_MIXED_ROWS (default 128), at least 64; in whole 64-row flash-prefill tiles."""
-        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "0"))
+        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "256" if mixed_mode() == "auto" else "0"))
         if fixed > 0:
             return -(-fixed // PREFILL_TILE) * PREFILL_TILE
         rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
