@@ -65,6 +65,26 @@ struct AttnParams {
   bf16* v_out;              // = v_cache, writable
 };
 
+// Persistent decode MLP block (decode_mega.hip): O projection -> residual + RMSNorm -> gate_up + SiLU·mul -> down
+// -> residual + RMSNorm, one launch of 256 resident workgroups for <= 64 rows (Mistral-7B shapes, TP = 1).
+struct MegaMlpParams {
+  const bf16* attn;    // [M, H] O-projection input
+  const bf16* wo;      // tiled [H, H]
+  const bf16* wgu;     // tiled [2F, H], gate/up rows interleaved in 8-row blocks
+  const bf16* wd;      // tiled [H, F]
+  float* resid;        // [M, H] fp32 residual stream (in / out)
+  const bf16* w_ffn;   // [H] post-attention norm weight
+  const bf16* w_next;  // [H] next layer's input norm (or the final norm)
+  bf16* xm;            // [M, H] gate_up input
+  bf16* h;             // [M, F] SiLU(gate)·up
+  bf16* x;             // [M, H] next layer's input
+  float* slabs;        // [8, M, H] split-K partial products
+  unsigned* sync;      // dsse_mega_sync_words() words, zeroed once at allocation, never reset
+  unsigned* err;       // set to 1 when a bounded wait timed out (the engine's health word, read at drain time)
+  int M;
+  float eps;
+};
+
 struct SampleParams {
   const float* logits;  // [B, ld]
   int ld, V;            // row stride, local vocab size
@@ -113,6 +133,9 @@ hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
 hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
                             int max_blocks, int num_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
 hipError_t dsse_ring_advance(int* counter, hipStream_t st);
+// persistent decode MLP block (decode_mega.hip)
+size_t dsse_mega_sync_words();
+hipError_t dsse_mega_mlp(const dsse::MegaMlpParams* p, hipStream_t st);
 hipError_t dsse_prefetch(const void* src, int64_t bytes, int wgs, unsigned* sink, hipStream_t st);
 // TP all-reduce + residual + RMSNorm over IPC peer buffers (allreduce.hip)
 size_t dsse_ar_buffer_bytes(int rows, int H);

@@ -860,7 +860,62 @@ void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, do
                                  reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 11; }
+// Persistent decode MLP block (decode_mega.hip): O -> residual + RMSNorm -> gate_up + SiLU·mul -> down -> residual +
+// RMSNorm in ONE launch of 256 resident workgroups (one per CU).  Mistral-7B shapes (H 4096, F 14336), TP = 1, M <= 64.
+// sync: int32 [mega_sync_words()] zeroed once, owned by one decode context (never used by two launches at once).
+bool mega_supported() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  return cus == 256;
+}
+int64_t mega_sync_words() { return (int64_t)dsse_mega_sync_words(); }
+void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Tensor& wd, Tensor& resid,
+              const Tensor& w_ffn, const Tensor& w_next, Tensor& xm, Tensor& h, Tensor& x, Tensor& slabs, Tensor& sync,
+              Tensor& err, double eps) {
+  for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
+                          (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
+                          (const Tensor*)&err})
+    check_gpu(*t, "mega_mlp tensor");
+  for (const Tensor* t : {&attn, &wo, &wgu, &wd, &w_ffn, &w_next, (const Tensor*)&xm, (const Tensor*)&h,
+                          (const Tensor*)&x})
+    check_dtype(*t, at::kBFloat16, "mega_mlp bf16 tensor");
+  check_dtype(resid, at::kFloat, "resid");
+  check_dtype(slabs, at::kFloat, "slabs");
+  check_dtype(sync, at::kInt, "sync");
+  check_dtype(err, at::kInt, "err");
+  constexpr int H = 4096, F = 14336;
+  const int M = (int)attn.size(0);
+  TORCH_CHECK(attn.dim() == 2 && attn.size(1) == H && M >= 1 && M <= 64, "mega_mlp: attn must be [M <= 64, 4096]");
+  TORCH_CHECK(wo.size(0) == H && wo.size(1) == H && wgu.size(0) == 2 * F && wgu.size(1) == H && wd.size(0) == H &&
+                  wd.size(1) == F, "mega_mlp: weights must be Mistral-7B shaped (tiled layout)");
+  TORCH_CHECK(resid.dim() == 2 && resid.size(0) >= M && resid.size(1) == H, "mega_mlp: resid [>= M, 4096]");
+  TORCH_CHECK(xm.size(0) >= M && xm.size(1) == H && x.size(0) >= M && x.size(1) == H, "mega_mlp: xm / x [>= M, 4096]");
+  TORCH_CHECK(h.size(0) >= M && h.size(1) == F, "mega_mlp: h [>= M, 14336]");
+  TORCH_CHECK(w_ffn.numel() == H && w_next.numel() == H, "mega_mlp: norm weights [4096]");
+  TORCH_CHECK(slabs.numel() >= (int64_t)8 * M * H, "mega_mlp: slabs hold 8 x M x 4096 floats");
+  TORCH_CHECK(sync.numel() >= mega_sync_words(), "mega_mlp: sync block too small");
+  TORCH_CHECK(mega_supported(), "mega_mlp: needs a 256-CU gfx950 device");
+  dsse::MegaMlpParams p{};
+  p.attn = reinterpret_cast<const bf16*>(attn.data_ptr());
+  p.wo = reinterpret_cast<const bf16*>(wo.data_ptr());
+  p.wgu = reinterpret_cast<const bf16*>(wgu.data_ptr());
+  p.wd = reinterpret_cast<const bf16*>(wd.data_ptr());
+  p.resid = resid.data_ptr<float>();
+  p.w_ffn = reinterpret_cast<const bf16*>(w_ffn.data_ptr());
+  p.w_next = reinterpret_cast<const bf16*>(w_next.data_ptr());
+  p.xm = reinterpret_cast<bf16*>(xm.data_ptr());
+  p.h = reinterpret_cast<bf16*>(h.data_ptr());
+  p.x = reinterpret_cast<bf16*>(x.data_ptr());
+  p.slabs = slabs.data_ptr<float>();
+  p.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
+  p.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  p.M = M;
+  p.eps = (float)eps;
+  DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
+}
+
+int64_t kernels_abi_version() { return 12; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -924,6 +979,10 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
   m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
         "Tensor(c!) epoch, Tensor(d!) err) -> ()");
+  m.def("mega_supported() -> bool", &mega_supported);
+  m.def("mega_sync_words() -> int", &mega_sync_words);
+  m.def("mega_mlp(Tensor attn, Tensor wo, Tensor wgu, Tensor wd, Tensor(a!) resid, Tensor w_ffn, Tensor w_next, "
+        "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
@@ -947,4 +1006,5 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
   m.impl("ar_rmsnorm", &ar_rmsnorm);
+  m.impl("mega_mlp", &mega_mlp);
 }

@@ -1,0 +1,376 @@
+// Persistent decode MLP block ("mega" kernel): one launch per layer runs
+//
+//     O projection (split-K slabs) -> residual + RMSNorm -> gate_up + SiLU·mul -> down (split-K slabs)
+//     -> residual + RMSNorm with the next layer's weight
+//
+// for <= 64 decode rows (MT = 4 MFMA row tiles), replacing five launches of the launch-per-op step
+// (gemm_ring o, rmsnorm<3>, gemm_ring gate_up, gemm_ring down, rmsnorm<3>; profiles/r3/decode_step_64_r3.md:
+// ~45 us of fixed cost per 131 us layer, 7 launches, VERDICT round 3 "next 1").
+//
+// Why it can be faster.  Every HBM byte a decode MLP block reads (weights: 33.5 + 235 + 117 MB) is independent of
+// the activations; only the 0.5-1.8 MB activation hand-offs are on the dependency chain.  Between launches the weight
+// stream stops (tail of one grid, launch boundary, first-load latency of the next: 5.5-7.5 us per GEMM launch).  Here
+// each workgroup's weight ring keeps streaming ACROSS the seams: a compute wave always has its next two 4 KiB weight
+// chunks in flight, and at an item boundary those are the next item's chunks, issued before the workgroup waits for
+// that item's inputs (MI355X_MICROARCH.md price list, prefetch-credit; engine-vs-launches 0.87-0.89x at batch 1).
+//
+// Structure (256 workgroups = one per CU, 9 waves each):
+//   * waves 0-7 compute: each owns one 16-column weight tile of the current work item and a private 3-slot LDS
+//     ring of 4 KiB weight chunks (buffer_load ... lds, non-temporal), filled two GEMM steps ahead by itself and
+//     waited for by its own counted vmcnt (gemm_ring2's weight ring, csrc/kernels/gemm_stream.hip);
+//   * wave 8 loads X (the activation, 64 rows x 128 columns per step = 16 KiB, XOR-swizzled image) into a 3-slot
+//     ring by global_load_lds, after waiting for the item's dependency counter and an agent-scope acquire;
+//   * one s_barrier per GEMM step publishes X(step) and retires the compute waves' reads of step - 1.
+//   Static work split (each workgroup: one O item, one gate_up item, one down item; rows' norms on 64 + 64
+//   workgroups), in dependency order per workgroup:
+//       O    item b:  columns 128 (b >> 3) .. +128 (8 tiles), K chunks 4 (b & 7) .. +4      -> slab (b & 7)
+//       N1   row b (b < 64):  resid += sum of the 8 O slabs; xm = rmsnorm(resid) * w_ffn
+//       GU   item b:  gate/up tiles 7b .. 7b + 6 (waves 0-6), all 32 K chunks              -> h (SiLU·mul)
+//       D    item b:  columns 128 (b >> 3) .. +128, K chunks 14 (b & 7) .. +14 (h columns)   -> slab (b & 7)
+//       N2   row b - 64 (64 <= b < 128): resid += sum of the 8 D slabs; x = rmsnorm(resid) * w_next
+//   Dependencies (counters in `sync`, never reset: see below): N1 <- all 256 O items; GU <- all 64 N1 rows;
+//   D item (ks) <- the 32 GU items that produce its K range (h columns 1792 ks .. +1792); N2 <- all 256 D items.
+//
+// Hand-offs (cdna_hip_programming.md Guideline 16, the "sc1 payload + agent atomic" row of MI355X_MICROARCH.md's
+// valid forms): every handed-off byte (slabs, h, xm, resid, x) is stored write-through (sc1) by buffer stores; each
+// storing wave drains its stores (counted vmcnt, below), the workgroup meets at an s_barrier, and ONE lane adds 1 to
+// the item's counter (agent scope, relaxed; O / D counters sharded by XCD label b & 7 on their own 128-B lines).
+// Consumers poll relaxed (one lane per shard, s_sleep, bounded) and then either load with sc1 buffer loads to
+// registers (norm rows: acquire-free) or, for the X ring's LDS-DMA, take ONE agent acquire first.
+// Counters are monotonic (never zeroed): a workgroup reads every counter it will poll at its start, before it has
+// contributed anything, and since every counter's completion needs ALL O items (the first item of every workgroup),
+// none can be complete at that time; the target is base + expected with base = v0 - v0 % expected (expected a power
+// of two, so the uint32 wrap-around keeps the multiples).
+//
+// Deadlock freedom needs all 256 workgroups resident at once (one per CU: 147 KiB of LDS each), i.e. an exclusive
+// GPU -- the engine enables this path only then (engine/model_runner.py).  Every spin is bounded: a timeout sets
+// the engine's health word p.err (read after each drained step) and the kernel completes with wrong values instead
+// of hanging the GPU.
+//
+// W vmcnt accounting per compute wave: 4 LDS-DMA instructions per GEMM step (dummy steps load through a 0-byte
+// descriptor: no memory traffic, same count), so "W(step) landed" is vmcnt(4) (W(step + 1) may stay in flight).
+// Item-end stores are issued before that step's weight refill, so the same vmcnt(4) retires them.
+#include "gemm_epilogue.h"
+
+namespace dsse {
+
+namespace mega {
+constexpr int kH = 4096, kF = 14336;         // Mistral-7B hidden / FFN (host-checked)
+constexpr int kKCH = kH / 128, kKCF = kF / 128;  // K chunks: 32 / 112
+constexpr int kWGs = 256;                    // one workgroup per CU
+constexpr int kCW = 8;                       // compute waves
+constexpr int kThreads = 64 * (kCW + 1);     // + the X loader wave
+constexpr int kRows = 64;                    // MT = 4 row tiles
+constexpr int kXSlot = kRows * 256;          // 64 rows x 128 columns bf16, 16 KiB
+constexpr int kWSlot = 4096;                 // one (16-column tile, 128-deep chunk) weight block
+constexpr int kD = 3;                        // ring slots (X and W): 2 steps in flight + 1 being read
+constexpr int kLdsW = kD * kXSlot;           // weight rings after the X ring
+constexpr int kLdsCtl = kLdsW + kCW * kD * kWSlot;
+constexpr int kLds = kLdsCtl + 256;
+// GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50)
+constexpr int kOSteps = 4, kGUSteps = kKCH, kDSteps = kKCF / 8;
+constexpr int kGU0 = kOSteps, kD0 = kGU0 + kGUSteps, kSteps = kD0 + kDSteps;
+// sync words: counter k, shard s at word (8 k + s) * 32 (one 128-B line each)
+enum { kCntO = 0, kCntN1 = 1, kCntGU = 2 /* + group 0..7 */, kCntD = 10, kSyncCounters = 11 };
+constexpr int kSpinLimit = 1 << 21;
+constexpr int kAuxSc1 = 16;   // buffer cache policy: sc1 (write-through / L1-bypassing)
+__host__ __device__ constexpr int sync_word(int k, int s) { return (8 * k + s) * 32; }
+}  // namespace mega
+
+
+namespace {
+
+using namespace mega;
+
+DEV void mega_glds16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(src),
+                                   reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                       reinterpret_cast<uintptr_t>(lds_base)),
+                                   16, 0, 0);
+}
+
+DEV __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t bytes) {
+  const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return make_rsrc(reinterpret_cast<const void*>(((unsigned long long)hi << 32) | lo), bytes);
+}
+
+// Counter poll by one wave: lanes < nshards read one shard each (relaxed, agent scope), the sum is compared with
+// the target (wrapping).  Bounded: on timeout sets the error word and returns.
+DEV void wait_counter(unsigned* sync, unsigned* err, int k, int nshards, unsigned base, unsigned expected, int lane) {
+  unsigned* cnt = sync + sync_word(k, 0);
+  for (int spins = 0;; ++spins) {
+    unsigned v = lane < nshards ? __hip_atomic_load(cnt + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) v += __shfl_xor(v, o);
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (v - base >= expected) return;
+    if (spins >= kSpinLimit) {
+      if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+DEV void signal_counter(unsigned* sync, int k, int shard) {
+  __hip_atomic_fetch_add(sync + sync_word(k, shard), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Raw barrier after this wave's own vmcnt wait (no __syncthreads: its fence would drain the weight DMA in flight).
+template <int N>
+DEV void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams p) {
+  using namespace mega;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const bool loader = w == kCW;
+  const int M = p.M;
+  const int ks = b & 7, cg = b >> 3;   // O / D item: split and 128-column group
+  float* red = reinterpret_cast<float*>(smem + kLdsCtl);
+
+  // ---- compute-wave weight stream: GEMM step gs -> this wave's (tile, chunk) block ----
+  auto w_src = [&](int gs, uint32_t& bytes) -> const bf16* {
+    bytes = kWSlot;
+    if (gs < kGU0) return p.wo + ((size_t)(8 * cg + w) * kKCH + 4 * ks + gs) * kTileChunk;
+    if (gs < kD0) {
+      if (w >= 7) bytes = 0;  // gate_up items are 7 tiles: wave 7 streams nothing (range-failed dummy loads)
+      return p.wgu + ((size_t)(7 * b + min(w, 6)) * kKCH + (gs - kGU0)) * kTileChunk;
+    }
+    if (gs < kSteps) return p.wd + ((size_t)(8 * cg + w) * kKCF + kDSteps * ks + (gs - kD0)) * kTileChunk;
+    bytes = 0;
+    return p.wo;
+  };
+  auto issue_w = [&](int gs) {
+    uint32_t bytes;
+    const bf16* src = w_src(gs, bytes);
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src, bytes);
+    char* dst = smem + kLdsW + (w * kD + gs % kD) * kWSlot;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(dst + 1024 * s)),
+          16, 1024 * s + lane * 16, 0, 0, kAuxNT);
+  };
+
+  // ---- loader: X(gs) = 64 rows x 128 columns of the step's activation into X slot gs % 3 ----
+  auto issue_x = [&](int gs) {
+    const bf16* X;
+    int ldx, col;
+    if (gs < kGU0) { X = p.attn; ldx = kH; col = 128 * (4 * ks + gs); }
+    else if (gs < kD0) { X = p.xm; ldx = kH; col = 128 * (gs - kGU0); }
+    else { X = p.h; ldx = kF; col = 128 * (kDSteps * ks + gs - kD0); }
+    char* base = smem + (gs % kD) * kXSlot;
+#pragma unroll
+    for (int i = 0; i < kRows / 4; ++i) {  // 16 DMA instructions of 4 rows x 256 B
+      const int row = 4 * i + g;
+      mega_glds16(X + (size_t)min(row, M - 1) * ldx + col + 8 * (r ^ swz(row & 15)), base + i * 1024);
+    }
+  };
+
+  // ---- counters this workgroup polls: bases read before it contributes anything ----
+  unsigned base_o = 0, base_n1 = 0, base_gu = 0, base_d = 0;
+  if (loader) {
+    auto rd = [&](int k, int s) { return __hip_atomic_load(p.sync + sync_word(k, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    unsigned vo = lane < 8 ? rd(kCntO, lane) : 0u, vd = lane < 8 ? rd(kCntD, lane) : 0u;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) { vo += __shfl_xor(vo, o); vd += __shfl_xor(vd, o); }
+    vo = __builtin_amdgcn_readfirstlane(vo);
+    vd = __builtin_amdgcn_readfirstlane(vd);
+    const unsigned vn1 = __builtin_amdgcn_readfirstlane(rd(kCntN1, 0));
+    const unsigned vgu = __builtin_amdgcn_readfirstlane(rd(kCntGU + ks, 0));
+    base_o = vo - vo % 256u;
+    base_d = vd - vd % 256u;
+    base_n1 = vn1 - vn1 % 64u;
+    base_gu = vgu - vgu % 32u;
+  }
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!loader) {
+    issue_w(0);
+    issue_w(1);
+  }
+
+  // ---- one GEMM item: steps [gs0, gs0 + nc) ----
+  // kind 0 = O / D (fp32 slab ks), 1 = gate_up (SiLU·mul -> h).  dep: counter polled before the first X load.
+  auto gemm_item = [&](int gs0, int nc, int kind, int active, int dep_k, int dep_shards, unsigned dep_base,
+                       unsigned dep_exp, int sig_k, int sig_shard) {
+    if (loader) {
+      if (dep_k >= 0) {
+        wait_counter(p.sync, p.err, dep_k, dep_shards, dep_base, dep_exp, lane);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // X arrives by LDS-DMA: drop this CU's stale lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      int issued = gs0;
+      issue_x(issued++);
+      if (nc > 1) issue_x(issued++);
+      for (int c = 0; c < nc; ++c) {
+        const int gs = gs0 + c;
+        if (issued - gs - 1 >= 1) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (issued < gs0 + nc) issue_x(issued++);
+      }
+      __builtin_amdgcn_s_barrier();  // end of item
+      return;
+    }
+    const bool on = w < active;
+    for (int c = 0; c < nc; ++c) {
+      const int gs = gs0 + c;
+      vm_barrier<4>();  // own W(gs) landed; X(gs) published by the loader
+      if (on) {
+        const char* xb = smem + (gs % kD) * kXSlot;
+        const char* wb = smem + kLdsW + (w * kD + gs % kD) * kWSlot + lane * 16;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ch = ((4 * g + s) ^ swz(r)) << 4;
+          bf16x8 xf[4];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) xf[mt] = *reinterpret_cast<const bf16x8*>(xb + (16 * mt + r) * 256 + ch);
+          const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wb + 1024 * s);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x16x32(xf[mt], wf, acc[mt]);
+        }
+      }
+      if (c == nc - 1 && on) {
+        if (kind == 0) {
+          // fp32 slab ks: part[ks][m][n], rows >= M dropped by the descriptor's range check
+          const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(p.slabs + (size_t)ks * M * kH, (uint32_t)M * kH * 4);
+          const int n = 16 * (8 * cg + w) + r;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][i]), rs,
+                                                    (uint32_t)(((16 * mt + 4 * g + i) * kH + n) * 4), 0, kAuxSc1);
+        } else {
+          // SiLU·mul (silu_epilogue4's lane pairing): tile t -> h columns 8t .. 8t + 7
+          const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(p.h, (uint32_t)M * kF * 2);
+          const int t = 7 * b + w;
+          const bool lo = r < 8;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            float pr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pr[i] = __shfl_xor(acc[mt][i], 8);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const float gate = lo ? acc[mt][k] : pr[2 + k], up = lo ? pr[k] : acc[mt][2 + k];
+              const int m = 16 * mt + 4 * g + (lo ? k : 2 + k);
+              const bf16 hv = f2bf(silu(gate) * up);
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), rs,
+                                                    (uint32_t)((m * kF + 8 * t + (r & 7)) * 2), 0, kAuxSc1);
+            }
+          }
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      issue_w(gs + kD - 1);  // after the item-end stores: the next vmcnt(4) retires them
+    }
+    vm_barrier<4>();  // end of item: every wave's stores retired
+    if (w == 0 && lane == 0) signal_counter(p.sync, sig_k, sig_shard);
+  };
+
+  // ---- one norm row: resid[m] += sum of the 8 slabs; y[m] = rmsnorm(resid[m]) * wn (sc1 loads / stores) ----
+  auto norm_item = [&](int m, const bf16* wn, bf16* y, int dep_k, int dep_shards, unsigned dep_base, int sig_k) {
+    if (loader) {
+      wait_counter(p.sync, p.err, dep_k, dep_shards, dep_base, 256u, lane);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+      return;
+    }
+    __builtin_amdgcn_s_barrier();  // the loader's poll matched: the slabs are complete (sc1 loads below)
+    const bool live = m < M;
+    const int c0 = 8 * (64 * w + lane);  // this thread's 8 columns
+    float v[8];
+    if (live) {
+      const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.resid + (size_t)m * kH, kH * 4);
+      const __amdgpu_buffer_rsrc_t sr = uniform_rsrc(p.slabs + (size_t)m * kH, (uint32_t)(7 * M * kH + kH) * 4);
+      typedef float f32x4v __attribute__((ext_vector_type(4)));
+      f32x4v a0 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rr, c0 * 4, 0, kAuxSc1));
+      f32x4v a1 = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rr, c0 * 4 + 16, 0, kAuxSc1));
+      f32x4v s0[8], s1[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const uint32_t off = (uint32_t)(s * M * kH + c0) * 4;
+        s0[s] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(sr, off, 0, kAuxSc1));
+        s1[s] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(sr, off + 16, 0, kAuxSc1));
+      }
+      f32x4v d0 = s0[0], d1 = s1[0];
+#pragma unroll
+      for (int s = 1; s < 8; ++s) { d0 += s0[s]; d1 += s1[s]; }
+      a0 += d0;
+      a1 += d1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = a0[j]; v[4 + j] = a1[j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    ss = wave_sum(ss);
+    if (lane == 0) red[w] = ss;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kCW; ++i) tot += red[i];
+    const float inv = rsqrtf(tot / (float)kH + p.eps);
+    if (live) {
+      const bf16x8 wv = *reinterpret_cast<const bf16x8*>(wn + c0);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] * inv * bf2f(wv[j]));
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t yr = uniform_rsrc(y + (size_t)m * kH, kH * 2);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), yr, c0 * 2, 0, kAuxSc1);
+      const __amdgpu_buffer_rsrc_t rr = uniform_rsrc(p.resid + (size_t)m * kH, kH * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                                   __float_as_uint(v[3])}, rr, c0 * 4, 0, kAuxSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
+                                                   __float_as_uint(v[7])}, rr, c0 * 4 + 16, 0, kAuxSc1);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (sig_k >= 0 && w == 0 && lane == 0) signal_counter(p.sync, sig_k, 0);
+  };
+
+  // ---- this workgroup's schedule ----
+  gemm_item(0, kOSteps, 0, 8, -1, 0, 0u, 0u, kCntO, ks);
+  if (b < kRows) norm_item(b, p.w_ffn, p.xm, kCntO, 8, base_o, kCntN1);
+  gemm_item(kGU0, kGUSteps, 1, 7, kCntN1, 1, base_n1, 64u, kCntGU + (b >> 5), 0);
+  gemm_item(kD0, kDSteps, 0, 8, kCntGU + ks, 1, base_gu, 32u, kCntD, ks);
+  if (b >= kRows && b < 2 * kRows) norm_item(b - kRows, p.w_next, p.x, kCntD, 8, base_d, -1);
+  // the look-ahead weight loads past the last step are range-failed dummies, but they still write the LDS: drain
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace dsse
+
+using namespace dsse;
+
+extern "C" size_t dsse_mega_sync_words() { return (size_t)mega::kSyncCounters * 8 * 32; }
+
+// Shapes are the Mistral-7B ones (H 4096, F 14336) and M <= 64; the caller (bindings.cpp) validates them.
+extern "C" hipError_t dsse_mega_mlp(const MegaMlpParams* p, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mega_mlp_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mega::kLds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  if (p->M < 1 || p->M > mega::kRows) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mega_mlp_kernel, dim3(mega::kWGs), dim3(mega::kThreads), mega::kLds, st, *p);
+  return hipGetLastError();
+}

@@ -69,11 +69,7 @@ def _parallel(jobs, verbose):
 
 
 KERNEL_VARIANTS = {
-    "checked": ["-DDSSE_KERNEL_CHECKS=1"],
-    "noxcd": ["-DDSSE_XCD_SPLITK=0"],  # experiment build (split-K workgroups in plain dispatch order)
-    "pfregs": ["-DDSSE_PREFILL_GLDS=0"],  # experiment build: flash-prefill K/V staged through registers (round 1)
-    "attdef": ["-DDSSE_ATTN_NT=0"],       # experiment build: decode attention K/V with default-policy loads
-    "wdef": ["-DDSSE_W_DEFAULT=1"],     # experiment build (default cache policy on gemm_stream weights)
+    "checked": ["-DDSSE_KERNEL_CHECKS=1"],  # device index-check debug build (tools/check_kernels.py)
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
 

@@ -103,11 +103,23 @@ class Sequence:
     enq_step: int = 0           # engine step at which it was queued (the mixed-step TTFT boost counts steps)
 
 
+class EngineFault(RuntimeError):
+    """A device-side health word was set (a bounded in-kernel wait timed out: persistent decode kernel, TP peer):
+    the step's tokens cannot be trusted.  The serving loop ends every live stream with [ERROR], drops readiness
+    and exits non-zero (no re-exec of a process that has touched the GPU)."""
+
+
 class _Drain:
     def __init__(self, runner: ModelRunner):
         self.r = runner
         self.cuda = runner.device.type == "cuda"
         B = runner.max_batch
+        # the runner's health words ride along with every ring row (same side stream, same event)
+        nh = runner.health.numel()
+        self.health = torch.zeros(RING_SIZE, nh, dtype=torch.int32)
+        self.pf_health = torch.zeros(RING_SIZE, nh, dtype=torch.int32)
+        if self.cuda:
+            self.health, self.pf_health = self.health.pin_memory(), self.pf_health.pin_memory()
         if self.cuda:
             self.host = torch.zeros(RING_SIZE, B, dtype=torch.int32).pin_memory()
             self.stream = torch.cuda.Stream(runner.device)
@@ -124,13 +136,20 @@ class _Drain:
 
     def issue(self, row: int, width: int, first: bool = False):
         host = self.pf_host if first else self.host
+        health = self.pf_health if first else self.health
         if not self.cuda:
             host[row, :width] = self.r.ring[row, :width]
+            health[row].copy_(self.r.health)
             return
         self.stream.wait_stream(torch.cuda.current_stream(self.r.device))
         with torch.cuda.stream(self.stream):
             host[row, :width].copy_(self.r.ring[row, :width], non_blocking=True)
+            health[row].copy_(self.r.health, non_blocking=True)
             (self.pf_events if first else self.events)[row].record(self.stream)
+
+    def faults(self, row: int, first: bool = False) -> list:
+        """Health faults recorded with ring row `row` (after wait())."""
+        return self.r.health_faults((self.pf_health if first else self.health)[row].tolist())
 
     def ready(self, row: int, first: bool = False) -> bool:
         return (not self.cuda) or (self.pf_events if first else self.events)[row].query()
@@ -548,6 +567,9 @@ class LLMEngine:
                 events.clear()
             tw = time.perf_counter()
             toks = self.drain.wait(rrow, first)
+            bad = self.drain.faults(rrow, first)
+            if bad:
+                raise EngineFault("; ".join(bad))
             n_main -= 0 if first else 1
             wait += time.perf_counter() - tw
             self.inflight.popleft()
@@ -590,6 +612,18 @@ class LLMEngine:
                 self._finish(s, events, reason="stop")
             elif s.produced >= s.params.max_tokens or s.orig_len + s.produced >= self.r.max_model_len:
                 self._finish(s, events, reason="length")
+
+    def fail_all(self, text: str = "[ERROR]") -> list:
+        """Terminal `text` events for every live conversation (running, paused, queued), after an EngineFault: the
+        clients see the reference's upstream-error token (llm-stream-proxy main.go:166-186) instead of a hang or
+        tokens computed from untrusted state.  Nothing else is enqueued on the device."""
+        events = []
+        self.inflight.clear()
+        for s in list(self.slots) + list(self.waiting):
+            if s is not None and s.state != "finished":
+                self._finish(s, events, reason="abort", text=text)
+        self.waiting.clear()
+        return events
 
     def run_until_idle(self, max_steps: int = 100000) -> list:
         out = []

@@ -49,6 +49,43 @@ PREFILL_GRAPH_SEQS = 16  # sequences per captured prefill batch (more: eager)
 # gemm_wide / gemm_tiled by row count (bindings.cpp gemm_impl).  Round 1 measured the split at 128 rows
 # (profiles/bucket_ab_r1.md).
 DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
+# Health words (runner.health, int32 on the device, copied to the host with every drained step; nonzero = the step's
+# outputs cannot be trusted and the engine fails: engine.py EngineFault).
+HEALTH_MEGA_WAIT = 0    # a bounded wait inside the persistent decode MLP kernel timed out (decode_mega.hip)
+HEALTH_TP_PEER = 1      # a TP peer's all-reduce row did not arrive in time (allreduce.hip)
+HEALTH_WORDS = ("persistent decode kernel wait timed out", "TP peer all-reduce wait timed out")
+
+
+def mega_reason(runner) -> str:
+    """Why the persistent decode MLP kernel (csrc/kernels/decode_mega.hip) is NOT used ("" = it is).
+
+    It runs the O / gate_up / down projections and both norms of a layer in one launch of 256 workgroups that must all
+    be resident at once (one per CU), so it needs the Mistral-7B MLP shapes at TP = 1, a 256-CU device, and a GPU this
+    process does not share with other ranks (DSSE_GPU_SHARED=1, or more local ranks than devices, turns it off: two
+    processes' persistent grids on one device could each hold half the CUs).  DSSE_MEGA=0 turns it off."""
+    if os.environ.get("DSSE_MEGA", "1") == "0":
+        return "DSSE_MEGA=0"
+    if runner.device.type != "cuda":
+        return "not on a GPU"
+    if runner.comm.size > 1:
+        return "TP > 1"
+    w = runner.w
+    if runner.cfg.hidden_size != 4096 or w.ffn != 14336:
+        return "not the Mistral-7B MLP shape"
+    if os.environ.get("DSSE_GPU_SHARED", "0") == "1":
+        return "DSSE_GPU_SHARED=1"
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if local_world > max(1, torch.cuda.device_count()):
+        return "several ranks share a GPU"
+    if not ops.mega_supported():
+        return "device is not a 256-CU gfx950"
+    return ""
+
+
+# decode buckets run on the persistent MLP kernel (rows <= 64; smaller buckets keep the launch-per-op path unless
+# DSSE_MEGA_MIN_B lowers the bound)
+MEGA_MIN_B = int(os.environ.get("DSSE_MEGA_MIN_B", "33"))
+MEGA_MAX_B = 64
 
 
 def mixed_mode() -> str:
@@ -140,6 +177,12 @@ class ModelRunner:
         self.tmp = torch.zeros(Bm, H, **bf)
         # fp32 split-K slabs of the residual projections (reduced inside the next RMSNorm)
         self.split_part = torch.zeros(32 * Bm * H, device=dev, dtype=torch.float32)
+        self.health = torch.zeros(4, device=dev, dtype=torch.int32)
+        self.mega_reason = mega_reason(self)
+        self.mega = not self.mega_reason and Bm >= MEGA_MIN_B
+        if self.mega:
+            self.xm = torch.zeros(min(Bm, MEGA_MAX_B), H, **bf)
+            self.mega_sync = ops.mega_sync(dev)
         self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
         nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
         self._cand = {b: torch.zeros(b, nch, 2, device=dev, dtype=torch.float32) for b in batch_buckets(Bm)}
@@ -151,6 +194,9 @@ class ModelRunner:
         self.part_ml = torch.zeros(max(1, ws) * nkv * 16 * 2, device=dev, dtype=torch.float32)
         # TP decode: the residual all-reduces on the fused IPC kernel (parallel/comm.py IpcAllReduce), RCCL otherwise
         self.fast_ar_reason = self.comm.enable_ipc_allreduce(dev, Bm, H) if self.comm.size > 1 else "tp=1"
+        if self.comm.fast_ar is not None:
+            # a timed-out peer wait now marks this runner's health word (checked at every drained step)
+            self.comm.fast_ar.err = self.health[HEALTH_TP_PEER:HEALTH_TP_PEER + 1]
         if self.comm.size > 1 and self.comm.rank == 0:
             print(f"[engine] TP={self.comm.size} decode all-reduce: "
                   f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
@@ -175,6 +221,18 @@ class ModelRunner:
         nl = len(w.layers)
         if B > DECODE_GEMM_MAX_M:
             self._decode_layers_wide(B, resid, x, part, nparts)
+            return
+        if self.mega and MEGA_MIN_B <= B <= MEGA_MAX_B:
+            # per layer: QKV + attention (2 launches), then the persistent MLP block (1 launch): O -> norm ->
+            # gate_up -> down -> norm with the weight stream running across the seams (decode_mega.hip)
+            for li, L in enumerate(w.layers):
+                self._qkv_attention(li, L, B, x, part, nparts)
+                w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
+                ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm, w_next, self.xm[r], self.h[r],
+                             x, self.split_part, self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps)
+            ops.gemm_out(x, w.lm_head_t, self.logits[r])
+            self._sample_commit(B)
+            ops.ring_advance(self.ring_counter)
             return
         for li, L in enumerate(w.layers):
             self._qkv_attention(li, L, B, x, part, nparts)
@@ -258,6 +316,18 @@ class ModelRunner:
             self.comm.all_gather_into(cand_all, cand)
         ops.sample_pick(cand_all, self.active[r], self.ids[r], self.ring, self.ring_counter, self.positions[r],
                         vocab=self.cfg.vocab_size)
+
+    def health_faults(self, words) -> list:
+        """Descriptions of the nonzero health words in `words` (a host copy of self.health)."""
+        return [HEALTH_WORDS[i] for i in range(min(len(HEALTH_WORDS), len(words))) if int(words[i]) != 0]
+
+    def close(self) -> None:
+        """Release the TP all-reduce's IPC mappings and buffer (the device is synchronised first)."""
+        if self.comm.fast_ar is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.comm.fast_ar.close()
+            self.comm.fast_ar = None
 
     def bucket_for(self, n_active_max_slot: int) -> int:
         for b in batch_buckets(self.max_batch):

@@ -183,6 +183,27 @@ def qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, 
     return 0
 
 
+def mega_supported() -> bool:
+    """The persistent decode MLP kernel needs a 256-CU gfx950 device (one resident workgroup per CU)."""
+    return torch.cuda.is_available() and load_library() and bool(torch.ops.dsse.mega_supported())
+
+
+def mega_sync(device) -> torch.Tensor:
+    """Counter block of the persistent decode MLP kernel: zeroed once, then owned by one decode context."""
+    load_library(required=True)
+    return torch.zeros(int(torch.ops.dsse.mega_sync_words()), dtype=torch.int32, device=device)
+
+
+def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps):
+    """Decode MLP block in one launch (HIP, <= 64 rows, Mistral-7B shapes): resid += attn·woᵀ; xm = norm(resid)·w_ffn;
+    h = silu(xm·w_gᵀ)·(xm·w_uᵀ); resid += h·w_dᵀ; x = norm(resid)·w_next.  `err` [1] int32 is set when a bounded
+    in-kernel wait timed out (the engine's health word)."""
+    if _hip(attn):
+        torch.ops.dsse.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps)
+    else:
+        ref.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps)
+
+
 def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):
     """Per-rank pass: cand [B, C, 2] <- best (score, index) of each vocab chunk (Gumbel-max / argmax)."""
     if _hip(logits):

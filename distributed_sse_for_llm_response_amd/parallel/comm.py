@@ -66,6 +66,12 @@ class TPComm:
         if self.size > 1:
             dist.barrier(group=self.group)
 
+    def close(self) -> None:
+        """Tear down the IPC all-reduce context (IPC handles closed, buffer freed); RCCL stays usable."""
+        if self.fast_ar is not None:
+            self.fast_ar.close()
+            self.fast_ar = None
+
     # ---- fused all-reduce + residual + RMSNorm (decode) ------------------------------------------------------
     fast_ar: object = None  # IpcAllReduce once enable_ipc_allreduce succeeded on every rank
 
@@ -153,6 +159,18 @@ class IpcAllReduce:
         if int(flag.item()) == 0:
             return None, why or "another rank of the TP group failed the IPC all-reduce self-test"
         return ctx, ""
+
+    def close(self) -> None:
+        """Unmap the peers' buffers and free this rank's (idempotent; the caller has synchronised the device, and
+        no graph that captured this context may be replayed afterwards)."""
+        if not self.peer_ptrs:
+            return
+        for q, ptr in enumerate(self.peer_ptrs):
+            if q != self.comm.rank and ptr:
+                torch.ops.dsse.ar_close(int(ptr), True)
+        if self.own_ptr:
+            torch.ops.dsse.ar_close(int(self.own_ptr), False)
+        self.peer_ptrs, self.own_ptr = [], 0
 
     def __call__(self, tmp, resid, norm_w, y, eps: float) -> None:
         torch.ops.dsse.ar_rmsnorm(tmp, resid, norm_w, y, eps, self.peers, self.comm.rank, self.rows, self.epoch,

@@ -19,7 +19,7 @@ import time
 import torch
 
 from .. import runtime as rt_mod
-from ..engine.engine import FINISH_CODES, LLMEngine, SamplingParams, TokenEvent
+from ..engine.engine import FINISH_CODES, EngineFault, LLMEngine, SamplingParams, TokenEvent
 from ..engine.kv_cache import KVCache
 from ..engine.model_runner import ModelRunner
 from ..models.mistral import TINY, get_config, init_standard_weights
@@ -193,7 +193,16 @@ class EngineLoop(threading.Thread):
                 self.last_progress = time.monotonic()
                 self._observe()
                 if self.faults.active:
-                    self.faults.after_step()
+                    self.faults.after_step(self.engine)
+        except EngineFault as e:
+            # untrusted device state: every live stream ends with [ERROR] now, readiness drops, the process exits
+            # non-zero through serve_forever (the orchestrator restarts it; nothing re-execs in this process)
+            self.error = e
+            self.rt.set_ready(False)
+            print(f"[engine] FAULT: {e}; ending {self.engine.num_running() + len(self.engine.waiting)} streams",
+                  flush=True)
+            self.publish(self.engine.fail_all())
+            raise
         except Exception as e:  # noqa: BLE001 - surfaced to the operator, readiness drops
             self.error = e
             self.rt.set_ready(False)
@@ -240,12 +249,16 @@ class ServingApp:
             self.loop.stop_flag.set()
             self.loop.join(timeout=10)
         self.rt.stop()
+        if self.engine is not None and (self.loop is None or not self.loop.is_alive()):
+            self.engine.r.close()  # TP: unmap the IPC all-reduce peers' buffers
 
     def serve_forever(self):
         try:
             while True:
                 time.sleep(0.5)
                 if self.loop is not None and not self.loop.is_alive():
+                    if isinstance(self.loop.error, EngineFault):
+                        time.sleep(0.5)  # let the I/O threads write the [ERROR] frames already on the bus
                     raise RuntimeError(f"engine loop died: {self.loop.error!r}")
         except KeyboardInterrupt:
             pass

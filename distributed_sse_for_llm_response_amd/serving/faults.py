@@ -11,7 +11,10 @@ a first-token timeout only).  Here:
     ``crash_after_steps=N``    hard-exit the process after N engine steps (no goodbye: the DP router
                                must detect it by heartbeat and requeue / terminate its conversations)
     ``error_after_steps=N``    raise inside the loop after N steps (readiness drops, /readyz -> 503)
-    ``stall_after_steps=N:MS`` block the loop for MS ms once after N steps (trips the watchdog)
+    ``stall_after_steps=N:MS`` block the loop for MS ms once after N steps (trips the watchdog; on a TP
+                               follower: the leader's IPC all-reduce times out instead)
+    ``health_after_steps=N``   set the runner's device health word after N steps, as a timed-out in-kernel wait
+                               does (the next drained step raises EngineFault: every stream ends with [ERROR])
     ``seed=S``                 RNG seed for drop_token
   ``DSSE_FAULTS_RANKS=1,3`` restricts the faults to those ranks (e.g. crash one DP replica of eight).
 * ``Watchdog`` — marks the replica not-ready while it has work but no step completed for ``timeout_s``
@@ -37,6 +40,7 @@ class FaultPlan:
         self.error_after_steps = 0
         self.stall_after_steps = 0
         self.stall_ms = 0
+        self.health_after_steps = 0
         seed = 0
         for item in filter(None, (x.strip() for x in spec.split(","))):
             k, _, v = item.partition("=")
@@ -51,6 +55,8 @@ class FaultPlan:
             elif k == "stall_after_steps":
                 n, _, ms = v.partition(":")
                 self.stall_after_steps, self.stall_ms = int(n), int(ms or 1000)
+            elif k == "health_after_steps":
+                self.health_after_steps = int(v)
             elif k == "seed":
                 seed = int(v)
             else:
@@ -75,8 +81,10 @@ class FaultPlan:
             return events
         return [e for e in events if e.done or self.rng.random() >= self.drop_token]
 
-    def after_step(self):
+    def after_step(self, engine=None):
         self.steps += 1
+        if self.health_after_steps and self.steps == self.health_after_steps and engine is not None:
+            engine.r.health[0] = 1  # what a bounded device wait does on timeout (model_runner.HEALTH_WORDS)
         if self.crash_after_steps and self.steps >= self.crash_after_steps:
             os._exit(17)  # simulated process death: no cleanup, no goodbye to the router
         if self.error_after_steps and self.steps >= self.error_after_steps:

@@ -19,9 +19,10 @@ import torch.distributed as dist
 
 from .. import runtime as rt_mod
 from ..parallel.comm import TPComm, init_distributed
+from ..engine.engine import EngineFault
 from .app import EngineLoop, ServingApp, build_engine
 from .config import ServeConfig
-from .faults import Watchdog
+from .faults import FaultPlan, Watchdog
 from .tp import TPLeader, follower_loop, make_plan_channel, make_tp_groups
 
 
@@ -31,6 +32,11 @@ class TPLeaderLoop(EngineLoop):
     def __init__(self, runtime, engine, tokenizer, cfg, channel):
         super().__init__(runtime, engine, tokenizer, cfg)
         self.drv = TPLeader(engine, channel)
+
+    def _flush(self, events):
+        """Mid-step events (engine.on_flush) go through the same rid bookkeeping as the step's own events."""
+        self.drv.forget(events)
+        super()._flush(events)
 
     def run(self):
         import gc
@@ -61,6 +67,12 @@ class TPLeaderLoop(EngineLoop):
                 self.steps += 1
                 self.last_progress = time.monotonic()
                 self._observe()
+        except EngineFault as e:
+            self.error = e
+            self.rt.set_ready(False)
+            print(f"[engine] TP leader FAULT: {e}", flush=True)
+            self.publish(self.engine.fail_all())
+            raise
         except Exception as e:  # noqa: BLE001 - surfaced to the operator, readiness drops
             self.error = e
             self.rt.set_ready(False)
@@ -79,7 +91,10 @@ def serve_tp(cfg: ServeConfig, rank: int, local: int, world: int, tp: int, devic
     dp = world // tp
     if rank != leader:
         engine, _ = build_engine(cfg, device=device, comm=comm)
-        follower_loop(engine, channel)
+        try:
+            follower_loop(engine, channel, faults=FaultPlan.from_env())
+        finally:
+            engine.r.close()
         return 0
     if dp == 1:  # one replica: the leader owns the sockets
         app = ServingApp(cfg, device=device, comm=comm)

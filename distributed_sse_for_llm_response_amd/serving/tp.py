@@ -221,19 +221,31 @@ class GlooPlanChannel:
 
 
 def make_plan_channel(plan_group, leader: int, group_index: int, tp: int):
-    """Shared-memory plan rings when the TP group is on this node (always, for the single-node launcher), gloo
-    otherwise (``DSSE_TP_PLAN=gloo`` forces it)."""
+    """Shared-memory plan rings when every rank of the TP group runs on this node, gloo otherwise
+    (``DSSE_TP_PLAN=gloo`` forces it).  Co-location is decided from the ranks' host names, gathered over the plan
+    group, so every rank takes the same branch; a shared-memory open that still fails (e.g. /dev/shm not shared
+    between containers of one host) is voted on by the whole group, which then falls back to gloo together."""
     import os
+    import socket
 
     rank = dist.get_rank()
     ranks = list(range(leader, leader + tp))
-    if os.environ.get("DSSE_TP_PLAN", "shm") != "gloo":
-        return ShmPlanChannel(plan_group, leader, rank, ranks, tag=f"{os.environ.get('MASTER_PORT', '0')}-{group_index}")
-    return GlooPlanChannel(plan_group, leader)
-
-
-class PlanChannel(GlooPlanChannel):
-    """Backwards-compatible name of the gloo channel."""
+    hosts = [None] * tp
+    dist.all_gather_object(hosts, socket.gethostname(), group=plan_group)
+    if os.environ.get("DSSE_TP_PLAN", "shm") == "gloo" or len(set(hosts)) > 1:
+        return GlooPlanChannel(plan_group, leader)
+    ch, err = None, ""
+    try:
+        ch = ShmPlanChannel(plan_group, leader, rank, ranks, tag=f"{os.environ.get('MASTER_PORT', '0')}-{group_index}")
+    except Exception as e:  # noqa: BLE001 - voted on below, every rank falls back together
+        err = f"{type(e).__name__}: {e}"
+    ok = [None] * tp
+    dist.all_gather_object(ok, err, group=plan_group)
+    if any(ok):
+        if rank == leader:
+            print(f"[serve] TP plan rings unavailable ({'; '.join(x for x in ok if x)}); using gloo", flush=True)
+        return GlooPlanChannel(plan_group, leader)
+    return ch
 
 
 def follower_conv(rid: int) -> str:
@@ -282,12 +294,17 @@ class TPLeader:
             self.ch.send(plan)
         apply_plan(self.engine, plan.roundtrip(), self._conv.__getitem__)
         events = self.engine.step() if run else []
-        for e in events:  # forget finished conversations
+        self.forget(events)
+        return events
+
+    def forget(self, events) -> None:
+        """Drop the rid mappings of conversations that finished in `events` (every event path calls this: the
+        step's return value and the events the engine flushes mid-step through on_flush)."""
+        for e in events:
             if e.done:
                 rid = self._rid.pop(e.conversation_id, None)
                 if rid is not None:
                     self._conv.pop(rid, None)
-        return events
 
     def sync(self) -> None:
         """Ask the followers to run their sync hook now (the leader runs its own right after)."""
@@ -299,8 +316,10 @@ class TPLeader:
             self.ch.send(Plan(stop=True))
 
 
-def follower_loop(engine, channel, on_sync=None) -> None:
-    """A follower rank: mirror the leader's plans until it sends stop."""
+def follower_loop(engine, channel, on_sync=None, faults=None) -> None:
+    """A follower rank: mirror the leader's plans until it sends stop.  `faults` (serving/faults.py FaultPlan, e.g.
+    ``DSSE_FAULTS=stall_after_steps=N:MS DSSE_FAULTS_RANKS=1``) drills a stalled or crashed TP follower: the
+    leader's IPC all-reduce then times out, its health word fails the step, and its streams end with [ERROR]."""
     while True:
         plan = channel.recv()
         if plan.stop:
@@ -308,6 +327,8 @@ def follower_loop(engine, channel, on_sync=None) -> None:
         apply_plan(engine, plan)
         if plan.step:
             engine.step()
+            if faults is not None and faults.active:
+                faults.after_step(engine)
         if plan.sync and on_sync is not None:
             on_sync()
 

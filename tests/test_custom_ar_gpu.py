@@ -97,3 +97,106 @@ def test_ipc_allreduce_rmsnorm_multiprocess_one_gpu(gpu, world):
     # identical bits on every rank (rank-order fp32 sum): the TP ranks' residual streams never drift apart
     assert all(r["digest"] == res[0]["digest"] for r in res)
 
+
+
+def _replay_worker(rank, world, port, buckets, iters, out):
+    """One TP rank: all_reduce_rmsnorm captured into one hipGraph per bucket, replayed `iters` times in a seeded mixed
+    bucket order (the same on every rank), every result checked against torch fp32 on the device."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import random
+
+    from distributed_sse_for_llm_response_amd.parallel.comm import TPComm
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {"why": "", "bad": [], "digest": [], "err": -1}
+    try:
+        comm = TPComm(rank=rank, size=world, group=None)
+        H, rows = 4096, max(buckets)
+        res["why"] = comm.enable_ipc_allreduce(dev, rows, H)
+        if res["why"]:
+            out[rank] = res
+            return
+        w = (1 + 0.1 * torch.sin(torch.arange(H, device=dev, dtype=torch.float32))).bfloat16()
+        st = {b: dict(tmp=torch.zeros(b, H, dtype=torch.bfloat16, device=dev), r=torch.zeros(b, H, device=dev),
+                      y=torch.zeros(b, H, dtype=torch.bfloat16, device=dev)) for b in buckets}
+        graphs = {}
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        for b in buckets:  # capture only (no eager warm-up: the kernel needs no library init)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                comm.all_reduce_rmsnorm(st[b]["tmp"], st[b]["r"], w, st[b]["y"], 1e-5)
+            graphs[b] = g
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        n = torch.arange(H, device=dev, dtype=torch.float32)
+        order = random.Random(5).choices(buckets, k=iters)
+
+        def partial(q, it, b):  # rank q's partial rows of iteration it (every rank can rebuild every partial)
+            m = torch.arange(b, device=dev, dtype=torch.float32)[:, None]
+            return torch.sin(0.37 * q + 0.011 * it + 0.13 * m + 0.007 * n[None, :] * (q + 1)).bfloat16()
+
+        for it, b in enumerate(order):
+            t = st[b]
+            r0 = torch.cos(0.05 * it + 0.21 * torch.arange(b, device=dev)[:, None] + 0.003 * n[None, :])
+            t["tmp"].copy_(partial(rank, it, b))
+            t["r"].copy_(r0)
+            graphs[b].replay()
+            tot = torch.zeros(b, H, device=dev)
+            for q in range(world):
+                tot += partial(q, it, b).float()
+            r_ref = r0 + tot
+            y_ref = (r_ref * torch.rsqrt(r_ref.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()).bfloat16()
+            er = float((t["r"] - r_ref).abs().max())
+            ey = float((t["y"].float() - y_ref.float()).abs().max())
+            if er > 1e-4 or ey > 3e-2:
+                res["bad"].append((it, b, er, ey))
+            res["digest"].append(float(t["r"].double().sum()) + float(t["y"].double().sum()))
+        torch.cuda.synchronize(dev)
+        res["err"] = int(comm.fast_ar.err.item())
+        dist.barrier()
+        comm.close()  # IPC handles closed, buffer freed (ar_close)
+        res["closed"] = comm.fast_ar is None
+        out[rank] = res
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+# 8 ranks at 1 and 64 rows; 256 rows with 2 ranks.  On the one-GPU box all ranks' workgroups share its CUs: 8 ranks x
+# 256 rows = 2048 workgroups of 512 threads against ~1024 resident slots, and ranks replay asynchronously, so half the
+# ranks' grids could fill the GPU while waiting for the other half's rows.  On the 8-GPU node each rank's grid has
+# its own device.
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,buckets", [(8, (1, 64)), (2, (1, 64, 256))])
+def test_ipc_allreduce_graph_replay_multiprocess(gpu, world, buckets):
+    """The decode path's form of the IPC all-reduce: captured into hipGraphs per bucket and replayed 200 times in
+    mixed bucket order (the per-row epoch counters live in device memory across replays); every replay equals the
+    fp32 sum of all ranks' partials + residual and its norm, identical bits on every rank, no peer wait timed out,
+    and the context is torn down with ar_close."""
+    with mp.Manager() as m:
+        out = m.dict()
+        ctx = mp.get_context("spawn")
+        port = _port()
+        procs = [ctx.Process(target=_replay_worker, args=(r, world, port, list(buckets), 200, out))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(540)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(10)
+        codes = [p.exitcode for p in procs]
+        res = [out.get(r) for r in range(world)]
+    assert codes == [0] * world, codes
+    assert all(r is not None for r in res)
+    assert res[0]["why"] == "", res[0]["why"]
+    for r in res:
+        assert r["err"] == 0, "a peer wait timed out"
+        assert r["bad"] == [], r["bad"][:5]
+        assert r["closed"]
+    assert all(r["digest"] == res[0]["digest"] for r in res)

@@ -96,6 +96,36 @@ def test_error_fault_drops_readiness(monkeypatch):
         app.stop()
 
 
+def test_device_health_fault_ends_every_stream_with_error(monkeypatch):
+    """A device health word (what a timed-out in-kernel wait sets: persistent decode kernel, TP peer all-reduce) fails
+    the engine at the next drained step: every live stream ends with the reference's [ERROR] token (done=true)
+    instead of tokens from untrusted state, and readiness drops (the process then exits non-zero)."""
+    from distributed_sse_for_llm_response_amd.engine.engine import EngineFault
+
+    monkeypatch.setenv("DSSE_FAULTS", "health_after_steps=2")
+    app = _app(max_tokens=64)
+    try:
+        port = app.port("edge")
+        out = []
+        ts = [threading.Thread(target=lambda: out.append(request(H, port, "POST", "/chat", {"message": f"m{i}"},
+                                                                 timeout=30)))
+              for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(40)
+        assert len(out) == 3
+        for r in out:
+            toks = [json.loads(e.data) for e in r.events if e.event == "token"]
+            assert toks and toks[-1]["done"] and toks[-1]["token"] == "[ERROR]", [e.data for e in r.events][-3:]
+            assert all(not t["done"] for t in toks[:-1])
+        assert request(H, port, "GET", "/readyz").status == 503
+        assert isinstance(app.loop.error, EngineFault)
+        assert "timed out" in str(app.loop.error)
+    finally:
+        app.stop()
+
+
 def _free_port():
     s = socket.socket()
     s.bind((H, 0))

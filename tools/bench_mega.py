@@ -1,0 +1,95 @@
+"""A/B of the decode MLP block at M rows: the launch-per-op chain (gemm_ring o -> rmsnorm<3> -> gate_up -> down ->
+rmsnorm<3>) vs the persistent kernel (decode_mega.hip), both captured as hipGraphs of 32 blocks over 8 distinct
+weight sets (3 GB, far past the 256 MB Infinity Cache), replayed alternately in one process (guide §5.4 rule 24).
+
+    python tools/bench_mega.py [--M 64] [--rounds 10]
+"""
+import argparse
+import math
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_sse_for_llm_response_amd import ops  # noqa: E402
+from distributed_sse_for_llm_response_amd.ops import reference as R  # noqa: E402
+
+H, F = 4096, 14336
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--sets", type=int, default=8)
+    ap.add_argument("--blocks", type=int, default=32)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ops.load_library(required=True)
+    torch.manual_seed(0)
+
+    def w(n, k):  # random bf16 directly on the device (tiled layout is a permutation: random stays random)
+        return (torch.randn(n, k, device=dev) / math.sqrt(k)).bfloat16()
+
+    sets = [dict(wo=w(H, H), wgu=w(2 * F, H), wd=w(H, F),
+                 w_ffn=torch.ones(H, device=dev).bfloat16(), w_next=torch.ones(H, device=dev).bfloat16())
+            for _ in range(a.sets)]
+    M = a.M
+    attn = torch.randn(M, H, device=dev).bfloat16()
+    resid = torch.randn(M, H, device=dev)
+    xm = torch.zeros(M, H, device=dev, dtype=torch.bfloat16)
+    x = torch.zeros_like(xm)
+    h = torch.zeros(M, F, device=dev, dtype=torch.bfloat16)
+    part = torch.zeros(32 * 64 * H, device=dev)
+    sync = ops.mega_sync(dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def unfused():
+        for i in range(a.blocks):
+            s = sets[i % a.sets]
+            ns = ops.gemm_resid_split(attn, s["wo"], resid, part)
+            ops.rmsnorm(resid, s["w_ffn"], xm, 1e-5, part=part, nsplit=ns)
+            ops.gemm_silu(xm, s["wgu"], h)
+            ns = ops.gemm_resid_split(h, s["wd"], resid, part)
+            ops.rmsnorm(resid, s["w_next"], x, 1e-5, part=part, nsplit=ns)
+
+    def fused():
+        for i in range(a.blocks):
+            s = sets[i % a.sets]
+            ops.mega_mlp(attn, s["wo"], s["wgu"], s["wd"], resid, s["w_ffn"], s["w_next"], xm, h, x, part, sync, err,
+                         1e-5)
+
+    graphs = {}
+    for name, fn in (("unfused", unfused), ("mega", fused)):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            fn()
+        torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        graphs[name] = g
+    times = {k: [] for k in graphs}
+    for _ in range(a.rounds):
+        for name, g in graphs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            times[name].append(e0.elapsed_time(e1) * 1000 / a.blocks)
+    assert int(err.item()) == 0, "mega kernel: a bounded wait timed out"
+    byts = (H * H + 2 * F * H + H * F) * 2
+    for name, t in times.items():
+        t = sorted(t)
+        med = t[len(t) // 2]
+        print(f"{name:8s} M={M}: per block median {med:7.2f} us  min {t[0]:7.2f} us  "
+              f"({byts / med / 1e6:.2f} TB/s weight stream)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
