@@ -1739,28 +1739,39 @@ FramePtr with_token(const FramePtr& f, const std::string& token) {
 }
 }  // namespace
 
-void InspectionGate::inline_frame(RemoteInspector& ri, const FramePtr& f, std::vector<FramePtr>& out) {
+void InspectionGate::fail_closed(const std::string& conv, const std::string& why) {
+  metrics().inspection_fail_closed_total.inc();
+  srv_.kill_conversation(conv, "[ERROR]", why);
+}
+
+bool InspectionGate::inline_frame(RemoteInspector& ri, const FramePtr& f, std::vector<FramePtr>& out) {
   TokenMessage m;
   if (f->done || !parse_token_message(f->json(), m)) {
     out.push_back(f);
-    return;
+    return false;
   }
   InspectionResult r;
   if (!ri.inspect(Bus::subject_for(f->conversation_id), m.token, m.sequence, m.timestamp, &r)) {
     metrics().inspection_remote_errors_total.inc();
-    out.push_back(f);  // fail open
-    return;
+    if (srv_.config().inspection_fail_open) {
+      metrics().inspection_fail_open_total.inc();
+      out.push_back(f);
+      return false;
+    }
+    fail_closed(f->conversation_id, "inspection unavailable");
+    return true;
   }
   if (r.action == InspectAction::kDrop) {
     metrics().inspection_dropped_total.inc();
-    return;
+    return false;
   }
   if (r.action == InspectAction::kRedact) {
     metrics().inspection_redacted_total.inc();
     out.push_back(with_token(f, r.redacted_content));
-    return;
+    return false;
   }
   out.push_back(f);
+  return false;
 }
 
 void InspectionGate::hybrid_flush(RemoteInspector& ri, const std::string& conv, Held& h, std::vector<FramePtr>& out) {
@@ -1780,7 +1791,13 @@ void InspectionGate::hybrid_flush(RemoteInspector& ri, const std::string& conv, 
     r.action = InspectAction::kAllow;
   } else if (!ri.inspect(Bus::subject_for(conv), text, seq, ts, &r)) {
     metrics().inspection_remote_errors_total.inc();
-    r.action = InspectAction::kAllow;  // fail open
+    if (!srv_.config().inspection_fail_open) {
+      h.frames.clear();
+      fail_closed(conv, "inspection unavailable");
+      return;
+    }
+    metrics().inspection_fail_open_total.inc((double)h.frames.size());
+    r.action = InspectAction::kAllow;
   }
   if (r.action == InspectAction::kDrop) {
     metrics().inspection_killed_total.inc();
@@ -1831,17 +1848,30 @@ void InspectionGate::run(Worker& w) {
       batch.swap(w.q);
     }
     std::vector<FramePtr> out;
-    // overload (a slow endpoint, the circuit just opened, a token burst): past kBypassDepth queued frames the batch
-    // is forwarded uninspected, in order (fail open), so the queue and the delivery delay stay bounded
-    if (!hybrid && batch.size() > kBypassDepth) {
-      metrics().inspection_remote_errors_total.inc((double)batch.size());
+    // overload (a slow endpoint, a token burst): the backlog stays bounded either way.  Fail-open: past kBypassDepth
+    // queued frames the batch is forwarded uninspected, in order.  Fail-closed: every frame is inspected; only past
+    // kOverloadDepth are the backlog's conversations ended with [ERROR] (nothing uninspected reaches a client).
+    if (!hybrid && cfg.inspection_fail_open && batch.size() > kBypassDepth) {
+      metrics().inspection_fail_open_total.inc((double)batch.size());
       out.assign(batch.begin(), batch.end());
+      batch.clear();
+    } else if (!hybrid && batch.size() > kOverloadDepth) {
+      for (const auto& f : batch)
+        if (w.dead.insert(f->conversation_id).second) fail_closed(f->conversation_id, "inspection overloaded");
       batch.clear();
     }
     for (const auto& f : batch) {
-      if (hybrid) hybrid_frame(ri, held, f, out);
-      else inline_frame(ri, f, out);
+      if (w.dead.count(f->conversation_id)) {  // ended fail-closed: later frames (its [DONE] too) are dropped
+        if (f->done) w.dead.erase(f->conversation_id);
+        continue;
+      }
+      if (hybrid) {
+        hybrid_frame(ri, held, f, out);
+      } else {
+        if (inline_frame(ri, f, out)) w.dead.insert(f->conversation_id);
+      }
     }
+    if (w.dead.size() > 65536) w.dead.clear();
     if (hybrid) {  // buffer windows that ran out; forget conversations idle for 10 minutes
       const int64_t now = mono_ns();
       for (auto it = held.begin(); it != held.end();) {

@@ -39,6 +39,7 @@ int main() {
   c.inspection_buffer_ms = (int)env_long("INSPECTION_BUFFER_MS", 150);
   c.inspection_endpoint = env_str("INSPECTION_ENDPOINT", "");
   c.inspection_timeout_ms = (int)env_long("INSPECTION_TIMEOUT_MS", c.inspection_timeout_ms);
+  c.inspection_fail_open = env_long("INSPECTION_FAIL_OPEN", 0) != 0;
   c.dedupe_window_s = (int)env_long("DEDUPE_WINDOW_SEC", c.dedupe_window_s);
   c.flow_high_water = (size_t)env_long("FLOW_HIGH_WATER", (long)c.flow_high_water);
   const int stub_tokens = (int)env_long("STUB_TOKENS", 50);

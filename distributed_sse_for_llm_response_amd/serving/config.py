@@ -43,6 +43,7 @@ class ServeConfig:
     inspection_buffer_ms: int = 150
     inspection_endpoint: str = ""  # remote inspector URL (POST /inspect of the reference's Spin function)
     inspection_timeout_ms: int = 250
+    inspection_fail_open: int = 0  # 1: a failed / overloaded inline inspector delivers uninspected (default: [ERROR])
     dedupe_window_s: int = 30      # bus duplicate window (the bridge's DEDUPE_WINDOW_SEC; 0 = off)
     log_level: str = "info"
     model_name: str = "mistralai/Mistral-7B-Instruct-v0.3"
@@ -89,6 +90,7 @@ class ServeConfig:
         c.inspection_buffer_ms = _env("INSPECTION_BUFFER_MS", c.inspection_buffer_ms, int)
         c.inspection_endpoint = _env("INSPECTION_ENDPOINT", c.inspection_endpoint)
         c.inspection_timeout_ms = _env("INSPECTION_TIMEOUT_MS", c.inspection_timeout_ms, int)
+        c.inspection_fail_open = _env("INSPECTION_FAIL_OPEN", c.inspection_fail_open, int)
         c.dedupe_window_s = _env("DEDUPE_WINDOW_SEC", c.dedupe_window_s, int)
         c.log_level = _env("LOG_LEVEL", c.log_level)
         c.model_name = _env("MODEL_NAME", c.model_name)
@@ -139,7 +141,7 @@ class ServeConfig:
         d = asdict(self)
         keys = ("host", "sse_port", "origin_port", "metrics_port", "resp_port", "io_threads", "llm_proxy_url",
                 "upstream_url", "inspection_mode", "inspection_buffer_ms", "inspection_endpoint",
-                "inspection_timeout_ms", "dedupe_window_s", "model_name", "keepalive_ms",
+                "inspection_timeout_ms", "inspection_fail_open", "dedupe_window_s", "model_name", "keepalive_ms",
                 "first_token_timeout_ms", "flow_high_water")
         out = {k: d[k] for k in keys}
         if self.ui_path != "none":

@@ -557,17 +557,35 @@ def test_inspection_endpoint_hybrid_inspects_the_buffered_text_and_kills():
         insp.close()
 
 
-def test_inspection_endpoint_failure_fails_open_and_async_uses_it():
+def test_inspection_endpoint_failure_fails_closed_by_default_and_async_uses_it():
+    """inline inspection is fail-closed like the reference ("inspector down = streaming stops",
+    docs/security-inspection-patterns.md:38): the stream ends with [ERROR] and the unchecked token never reaches the
+    client.  INSPECTION_FAIL_OPEN=1 delivers it instead, counted in inspection_fail_open_total."""
     insp = _Inspector(fail=True)
     r = make_rt(inspection_mode="inline", inspection_endpoint=insp.url)
     try:
-        e0 = _metric(r, "inspection_remote_errors_total")
+        e0, c0 = _metric(r, "inspection_remote_errors_total"), _metric(r, "inspection_fail_closed_total")
+        th, got = _stream_in_thread(r, "failclosed")
+        r.publish("failclosed", "evil but unchecked", 1, False, 0)
+        r.publish("failclosed", "more", 2, False, 0)
+        r.publish("failclosed", "[DONE]", 3, True, 0)
+        th.join(5)
+        assert [(t["token"], t["done"]) for t in tokens_of(got[0])] == [("[ERROR]", True)]
+        assert _metric(r, "inspection_remote_errors_total") - e0 == 1  # later frames are not re-inspected
+        assert _metric(r, "inspection_fail_closed_total") - c0 == 1
+    finally:
+        r.stop()
+        insp.close()
+    insp = _Inspector(fail=True)
+    r = make_rt(inspection_mode="inline", inspection_endpoint=insp.url, inspection_fail_open=1)
+    try:
+        o0 = _metric(r, "inspection_fail_open_total")
         th, got = _stream_in_thread(r, "failopen")
         r.publish("failopen", "evil but unchecked", 1, False, 0)
         r.publish("failopen", "[DONE]", 2, True, 0)
         th.join(5)
         assert [t["token"] for t in tokens_of(got[0])] == ["evil but unchecked", "[DONE]"]
-        assert _metric(r, "inspection_remote_errors_total") - e0 == 1
+        assert _metric(r, "inspection_fail_open_total") - o0 == 1
     finally:
         r.stop()
         insp.close()
@@ -604,14 +622,16 @@ def test_redelivered_first_token_after_done_is_a_duplicate(bare_rt):
     assert bare_rt.last_sequence(conv) == 3
 
 
-def test_black_holed_inspection_endpoint_fails_open_quickly():
+@pytest.mark.parametrize("fail_open", [0, 1])
+def test_black_holed_inspection_endpoint_fails_quickly(fail_open):
     """an INSPECTION_ENDPOINT that accepts TCP but never answers must not stall every token for the
-    timeout: the first failure opens the circuit and the stream is delivered (uninspected) at once."""
+    timeout: the first failure opens the circuit.  Fail-closed (default) the stream ends at once with [ERROR];
+    with INSPECTION_FAIL_OPEN=1 it is delivered, uninspected, at once."""
     hole = socket.socket()
     hole.bind((H, 0))
     hole.listen(1)  # the kernel completes the handshake; nobody ever reads or answers
     r = make_rt(inspection_mode="inline", inspection_endpoint=f"http://{H}:{hole.getsockname()[1]}/inspect",
-                inspection_timeout_ms=300)
+                inspection_timeout_ms=300, inspection_fail_open=fail_open)
     try:
         th, got = _stream_in_thread(r, "hole")
         t0 = time.monotonic()
@@ -619,7 +639,8 @@ def test_black_holed_inspection_endpoint_fails_open_quickly():
             r.publish("hole", f"t{i}", i + 1, False, 0)
         r.publish("hole", "[DONE]", 41, True, 0)
         th.join(10)
-        assert [t["token"] for t in tokens_of(got[0])] == [f"t{i}" for i in range(40)] + ["[DONE]"]
+        want = [f"t{i}" for i in range(40)] + ["[DONE]"] if fail_open else ["[ERROR]"]
+        assert [t["token"] for t in tokens_of(got[0])] == want
         assert time.monotonic() - t0 < 3.0  # 40 tokens x 2 attempts x 300 ms without the circuit breaker
     finally:
         r.stop()
