@@ -19,8 +19,8 @@
 //   softmax    = online, base 2, masked scores contribute exactly 0 (fully masked columns stay 0).
 #include "api.h"
 
-// K/V staging by LDS-DMA (global_load_lds, no VGPRs, no ds_write pass) -- 1, default -- or through registers
-// (0, variant build "pfregs": the round-1 form, kept for A/B).
+// K/V staging by LDS-DMA (global_load_lds, no VGPRs, no ds_write pass; the round-1 register-staged form measured
+// slower and was removed).
 #ifndef DSSE_PREFILL_GLDS
 #define DSSE_PREFILL_GLDS 1
 #endif

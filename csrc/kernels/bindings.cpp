@@ -148,7 +148,7 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
 
 // gemm_stream launch, or its LDS-DMA ring form (gemm_ring_kernel) where that applies: 33-64 rows, one 16-column
 // tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 7 / 8 (the 7-8-wave shapes; LDS; gate_up on 7
-// waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8, DSSE_S_RING7=0).  DSSE_S_RING=0 turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
+// waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8).  DSSE_S_RING=0 turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
 // waves 4.55 / 4.66 (gate_up 45.8 -> 43.5 us, LM head 52.5 -> 48.3; profiles/r2/ring_*.log).
 // Ring GEMM variant: DSSE_RING2 unset = the decoupled-look-ahead kernel (gemm_ring2) for 65-128 rows only
 // (128-stream step 6.19-6.22 vs 6.32-6.34 ms; at 33-64 rows 4.44 vs 4.40 ms: profiles/r3/ring2_ab.log,
@@ -163,14 +163,14 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
   const int ring = env_int("DSSE_S_RING", 1);
   // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
   const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32) ||
-                         (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4 && env_int("DSSE_RING128", 1));
+                         (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4);
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
-    int nw = c.nw >= 7 ? (c.nw == 7 && env_int("DSSE_S_RING7", 1) ? 7 : 8) : 4;
+    int nw = c.nw >= 7 ? c.nw : 4;
     if (c.ring_nw > 0 && (N / 16) % c.ring_nw == 0 && M <= 64)
       return dsse_gemm_ring(mode, c.ring_nw, S, partial_only, ring2_for(M), X, K, M, W, K, N, ep, part, cur_stream());
     // QKV at 33-64 rows: 3 waves (384 tiles -> 128 x S 2 = 256 workgroups instead of 192; 64-stream step
-    // 4.38-4.40 vs 4.41-4.42 ms, profiles/r2/qkv_ring3_ab.log; DSSE_QKV_RING3=0 = 4 waves)
-    if (mode == dsse::kQkvRope && c.mt == 4 && env_int("DSSE_QKV_RING3", 1) && (N / 16) % 3 == 0) nw = 3;
+    // 4.38-4.40 vs 4.41-4.42 ms, profiles/r2/qkv_ring3_ab.log)
+    if (mode == dsse::kQkvRope && c.mt == 4 && (N / 16) % 3 == 0) nw = 3;
     if ((N / 16) % nw == 0)
       return dsse_gemm_ring(mode, nw, S, partial_only, ring2_for(M), X, K, M, W, K, N, ep, part, cur_stream());
   }
@@ -227,24 +227,20 @@ TCfg pick_tiled(int M, int N, int K) {
     cfg = (N % 256 == 0 && big_tiles >= 160) ? 4 : (M > 128 ? 0 : 1);
     // narrow projections of the wide decode buckets (N <= 8192, 128 < M <= 512: qkv / o / down at 192-256
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
-    // (same box, alternating; profiles/experiments_r2.md).  DSSE_T_NARROW_CFG overrides.
+    // (same box, alternating; profiles/experiments_r2.md).
     // round 3 (profiles/r3/decode_bucket_gemm.md): in the 129-192-row bucket qkv (N 6144) and down (K 14336) on
     // 256x128 -- alone 27 vs 30 us and 42 vs 50 us, 192-stream step 8.30 vs 8.43 ms; at 193-256 rows the same
     // change measured 9.81 vs 9.71 ms per step (twice the split-K slabs for the consuming norm / attention),
     // so 128x128 stays there
-    const int narrow = env_int("DSSE_T_NARROW_CFG", (M <= 192 && !(N <= 4096 && K <= 4096)) ? 0 : 1);
-    if (narrow >= 0 && narrow <= 4 && N <= 8192 && M > 128 && M <= 256) cfg = narrow;
+    if (N <= 8192 && M > 128 && M <= 256) cfg = (M <= 192 && !(N <= 4096 && K <= 4096)) ? 0 : 1;
     // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: per shape from the
     // tools/bench_gemm_tiled.py sweep over every config (profiles/r3/prefill_chunk_gemm.md): 257-512 rows down
     // (K 14336) on the phased 256x256 tile split 8 ways (69 vs 92 us), qkv / o on 256x128 (46 / 33 vs 49 / 35
     // us); 513-1024 rows N <= 4096 (o, down) on 128x128 (50 / 153 vs 65 / 205 us)
-    if (env_int("DSSE_T_NARROW_CFG", -1) < 0 && N <= 8192 && M > 256 && M <= 512) cfg = K > 8192 ? 4 : 0;
-    if (env_int("DSSE_T_NARROW_CFG", -1) < 0 && N <= 4096 && M > 512 && M <= 1024) cfg = 1;
-    // wide projections of those buckets (gate_up, LM head): DSSE_T_WIDE_CFG (default by the rule above)
-    const int wide = env_int("DSSE_T_WIDE_CFG", -1);
-    if (wide >= 0 && wide <= 4 && N > 8192 && M > 128 && M <= kMaxDecodeM) cfg = wide;
+    if (N <= 8192 && M > 256 && M <= 512) cfg = K > 8192 ? 4 : 0;
+    if (N <= 4096 && M > 512 && M <= 1024) cfg = 1;
   }
-  const int min_wgs = env_int("DSSE_T_MIN_WGS", 160);  // split K until this many workgroups (M <= 512)
+  constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
   // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
   static constexpr int kBM[5] = {256, 128, 256, 256, 256};
   static constexpr int kBN[5] = {128, 128, 64, 256, 256};
@@ -272,18 +268,18 @@ int gemm_impl(int M, int N, int K) {
     // every branch returns a kernel whose shape contract holds (or -1): prefill calls arrive with any M and
     // tensor-parallel shard shapes
     // 65-128 rows, narrow N (4-wave stream shapes: qkv / o / down): the ring kernel with 8 row tiles, 3 slots;
-    // 128-stream step 6.19 / 6.23 vs 6.36 / 6.37 ms on gemm_wide (profiles/r2/ring128_ab.log); DSSE_RING128=0
-    if (impl < 0 && M <= 128 && env_int("DSSE_RING128", 1)) {
+    // 128-stream step 6.19 / 6.23 vs 6.36 / 6.37 ms on gemm_wide (profiles/r2/ring128_ab.log)
+    if (impl < 0 && M <= 128) {
       const SCfg sc = pick_stream(M, N, K);
       if (sc.ok && sc.mt == 8 && sc.nt == 1 && sc.nw == 4) return 2;
     }
     const bool tiled_ok = pick_tiled(M, N, K).ok;
-    if (tiled_ok && (M > kMaxDecodeM || impl == 4 || (impl < 0 && M > env_int("DSSE_TILED_MIN_M", 128)))) return 4;
+    if (tiled_ok && (M > kMaxDecodeM || impl == 4 || (impl < 0 && M > 128))) return 4;
     if (M > kMaxDecodeM) return -1;  // the decode kernels stop at kMaxDecodeM rows
     const bool wide_ok = pick_wide(M, N, K).ok, stream_ok = pick_stream(M, N, K).ok;
     if (impl == 3 && wide_ok) return 3;
     if (impl == 2 && stream_ok) return 2;
-    if (wide_ok && M > env_int("DSSE_WIDE_MIN_M", 64)) return 3;  // 3 = gemm_wide (32x32 MFMAs, M <= 256)
+    if (wide_ok && M > 64) return 3;  // 3 = gemm_wide (32x32 MFMAs, M <= 256)
     if (stream_ok) return 2;
     if (wide_ok) return 3;
     return tiled_ok ? 4 : -1;
@@ -714,9 +710,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
     const WCfg c = pick_wide(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
   } else {
-    SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
-    const int qnw = env_int("DSSE_QKV_NW", 0);  // ring waves per workgroup (with DSSE_QKV_SPLIT)
-    if (qnw > 0 && M > 32 && M <= 64 && (N / 16) % qnw == 0) c.ring_nw = qnw;  // 33-64 rows: the MT = 4 ring
+    const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
     DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, S, 1, X, M, w.data_ptr(), K, N, &ep, sl));
   }
   p.qkv_part = sl;

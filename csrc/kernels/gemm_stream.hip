@@ -31,10 +31,6 @@
 #define DSSE_XCD_SPLITK 1  // XCD-grouped split-K workgroup mapping (see the kernel)
 #endif
 
-#ifndef DSSE_W_DEFAULT
-#define DSSE_W_DEFAULT 0  // experiment build "wdef": default cache policy on the weight stream
-#endif
-
 namespace dsse {
 
 // K-chunks of 128 per LDS slice: two slices of 16·MT rows stay within 128 KiB of LDS (MT <= 4: 512 columns,
@@ -96,7 +92,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
 #pragma unroll
   for (int t = 0; t < NT; ++t)
     wrs[t] = make_rsrc(W + ((size_t)(tgu * NT + t) * KC + (k0u >> 7)) * kTileChunk, (uint32_t)nch * kTileChunk * 2);
-  constexpr int WAUX = (SHARED_W || DSSE_W_DEFAULT) ? 0 : kAuxNT;
+  constexpr int WAUX = SHARED_W ? 0 : kAuxNT;  // row blocks share weights through L2
   auto load_w = [&](int c, bf16x8 (&wf)[NT][4]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -331,7 +327,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
                                           // last one (same bytes to the same LDS address: a benign duplicate)
   static_assert(D >= 3 && G::LDS <= 160 * 1024, "ring of >= 3 slots within the CU's LDS");
   constexpr int PER = XI + 4;             // VMEM instructions per wave per chunk
-  constexpr int WAUX = DSSE_W_DEFAULT ? 0 : kAuxNT;
+  constexpr int WAUX = kAuxNT;  // weights streamed once: non-temporal
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -494,7 +490,7 @@ gemm_ring2_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
   static_assert(XN % XL == 0, "X instructions split evenly over the loader waves");
   constexpr int XI = XN / XL;             // per loader wave per chunk
   static_assert(DX >= 3 && DW >= 3 && G::LDS <= 160 * 1024, "rings of >= 3 slots within the CU's LDS");
-  constexpr int WAUX = DSSE_W_DEFAULT ? 0 : kAuxNT;
+  constexpr int WAUX = kAuxNT;  // weights streamed once: non-temporal
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -166,7 +166,7 @@ def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S, r2):
     x = _rand(M, K, dev=gpu, gen=g)
     w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
     for k, v in {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": ring, "DSSE_S_NW": nw, "DSSE_S_SPLIT": S,
-                 "DSSE_RING128": "1", "DSSE_RING2": r2}.items():
+                 "DSSE_RING2": r2}.items():
         monkeypatch.setenv(k, v)
     ops.refresh_env()
     out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
