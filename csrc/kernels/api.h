@@ -79,6 +79,9 @@ struct MegaMlpParams {
   bf16* h;             // [M, F] SiLU(gate)·up
   bf16* x;             // [M, H] next layer's input
   float* slabs;        // [8, M, H] split-K partial products
+  const bf16* wqkv;    // optional: the NEXT layer's tiled QKV weight [(nh + 2 nkv) * 128 = 6144, H]; its projection of x
+                       // runs as the block's last phase (4 fp32 split-K slabs into qkv_slabs, for the folded attention)
+  float* qkv_slabs;    // [4, M, 6144] (may alias slabs: written only after every slab above was consumed)
   unsigned* sync;      // dsse_mega_sync_words() words, zeroed once at allocation, never reset
   unsigned* err;       // set to 1 when a bounded wait timed out (the engine's health word, read at drain time)
   int M;

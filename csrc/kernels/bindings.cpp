@@ -658,7 +658,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
                              int64_t nkv, Tensor& slabs, const Tensor& block_tables, const Tensor& q_start,
                              const Tensor& q_len, const Tensor& ctx_len, const Tensor& work_seq,
                              const Tensor& work_tile, Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part,
-                             int64_t nparts) {
+                             int64_t nparts, int64_t slabs_ready) {
   check_gpu(x, "x");
   check_gpu(w, "w");
   check_gpu(slabs, "slabs");
@@ -668,7 +668,8 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
                         N == (nh + 2 * nkv) * 128;
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
   int S = 0;
-  if (impl == 4) S = pick_tiled(M, N, K).S;
+  if (slabs_ready > 0) S = (int)slabs_ready;  // the persistent MLP kernel already wrote the QKV slabs (decode_mega.hip)
+  else if (impl == 4) S = pick_tiled(M, N, K).S;
   else if (impl == 3) S = pick_wide(M, N, K).S;
   else if (impl == 2) {
     S = pick_stream(M, N, K, dsse::kQkvRope).S;
@@ -680,7 +681,10 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   auto q3 = q_out.view({-1, nh, 128});
   auto o3 = out.view({-1, nh, 128});
   const bool group_ok = nkv > 0 && nh % nkv == 0 && (nh / nkv == 1 || nh / nkv == 2 || nh / nkv == 4);  // attention.hip
-  if (S <= 0 || !group_ok || slabs.numel() < (int64_t)S * M * N || env_int("DSSE_FUSED_QKV_ATTN", 1) == 0) {
+  TORCH_CHECK(slabs_ready <= 0 || (group_ok && slabs.numel() >= (int64_t)S * M * N),
+              "qkv_attention_decode: slabs_ready needs a GQA group of 1 / 2 / 4 and S x M x N slabs");
+  if (slabs_ready <= 0 &&
+      (S <= 0 || !group_ok || slabs.numel() < (int64_t)S * M * N || env_int("DSSE_FUSED_QKV_ATTN", 1) == 0)) {
     gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv);
     paged_attention(0, q3, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, o3, part_o,
                     part_ml, part, nparts);
@@ -703,7 +707,9 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   dsse::GemmEpi ep{};
   const void* X = x.data_ptr();
   float* sl = slabs.data_ptr<float>();
-  if (impl == 4) {
+  if (slabs_ready > 0) {
+    // slabs written by an earlier kernel on this stream
+  } else if (impl == 4) {
     const TCfg c = pick_tiled(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_tiled(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
   } else if (impl == 3) {
@@ -866,7 +872,7 @@ bool mega_supported() {
 int64_t mega_sync_words() { return (int64_t)dsse_mega_sync_words(); }
 void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Tensor& wd, Tensor& resid,
               const Tensor& w_ffn, const Tensor& w_next, Tensor& xm, Tensor& h, Tensor& x, Tensor& slabs, Tensor& sync,
-              Tensor& err, double eps) {
+              Tensor& err, double eps, const c10::optional<Tensor>& wqkv, const c10::optional<Tensor>& qkv_slabs) {
   for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
                           (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
                           (const Tensor*)&err})
@@ -890,6 +896,16 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
   TORCH_CHECK(slabs.numel() >= (int64_t)8 * M * H, "mega_mlp: slabs hold 8 x M x 4096 floats");
   TORCH_CHECK(sync.numel() >= mega_sync_words(), "mega_mlp: sync block too small");
   TORCH_CHECK(mega_supported(), "mega_mlp: needs a 256-CU gfx950 device");
+  const bool q = wqkv.has_value() && wqkv->defined();
+  if (q) {
+    TORCH_CHECK(qkv_slabs.has_value() && qkv_slabs->defined(), "mega_mlp: wqkv needs qkv_slabs");
+    check_gpu(*wqkv, "wqkv");
+    check_gpu(*qkv_slabs, "qkv_slabs");
+    check_dtype(*wqkv, at::kBFloat16, "wqkv");
+    check_dtype(*qkv_slabs, at::kFloat, "qkv_slabs");
+    TORCH_CHECK(wqkv->size(0) == 6144 && wqkv->size(1) == H, "mega_mlp: wqkv must be [6144, 4096] (tiled)");
+    TORCH_CHECK(qkv_slabs->numel() >= (int64_t)4 * M * 6144, "mega_mlp: qkv_slabs hold 4 x M x 6144 floats");
+  }
   dsse::MegaMlpParams p{};
   p.attn = reinterpret_cast<const bf16*>(attn.data_ptr());
   p.wo = reinterpret_cast<const bf16*>(wo.data_ptr());
@@ -904,6 +920,8 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
   p.slabs = slabs.data_ptr<float>();
   p.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
   p.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  p.wqkv = q ? reinterpret_cast<const bf16*>(wqkv->data_ptr()) : nullptr;
+  p.qkv_slabs = q ? qkv_slabs->data_ptr<float>() : nullptr;
   p.M = M;
   p.eps = (float)eps;
   DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
@@ -963,7 +981,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("qkv_attention_decode(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor(d!) slabs, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(e!) out, "
-        "Tensor(f!) part_o, Tensor(g!) part_ml, int part, int nparts) -> int");
+        "Tensor(f!) part_o, Tensor(g!) part_ml, int part, int nparts, int slabs_ready=0) -> int");
   m.def("sample_candidates(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
@@ -976,7 +994,8 @@ TORCH_LIBRARY(dsse, m) {
   m.def("mega_supported() -> bool", &mega_supported);
   m.def("mega_sync_words() -> int", &mega_sync_words);
   m.def("mega_mlp(Tensor attn, Tensor wo, Tensor wgu, Tensor wd, Tensor(a!) resid, Tensor w_ffn, Tensor w_next, "
-        "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps) -> ()");
+        "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps, "
+        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);

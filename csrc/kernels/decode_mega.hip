@@ -28,8 +28,12 @@
 //       GU   item b:  gate/up tiles 7b .. 7b + 6 (waves 0-6), all 32 K chunks              -> h (SiLU·mul)
 //       D    item b:  columns 128 (b >> 3) .. +128, K chunks 14 (b & 7) .. +14 (h columns)   -> slab (b & 7)
 //       N2   row b - 64 (64 <= b < 128): resid += sum of the 8 D slabs; x = rmsnorm(resid) * w_next
+//       Q    (optional, every layer but the last) the next layer's QKV projection of x: columns 96 (b >> 2) .. +96
+//            (6 tiles, waves 0-5), K chunks 8 (b & 3) .. +8 -> fp32 slab (b & 3) of qkv_slabs, summed + RoPE'd by the
+//            folded decode attention kernel that runs next (attention.hip mode 3)
 //   Dependencies (counters in `sync`, never reset: see below): N1 <- all 256 O items; GU <- all 64 N1 rows;
-//   D item (ks) <- the 32 GU items that produce its K range (h columns 1792 ks .. +1792); N2 <- all 256 D items.
+//   D item (ks) <- the 32 GU items that produce its K range (h columns 1792 ks .. +1792); N2 <- all 256 D items;
+//   Q <- all 64 N2 rows.
 //
 // Hand-offs (cdna_hip_programming.md Guideline 16, the "sc1 payload + agent atomic" row of MI355X_MICROARCH.md's
 // valid forms): every handed-off byte (slabs, h, xm, resid, x) is stored write-through (sc1) by buffer stores; each
@@ -67,11 +71,13 @@ constexpr int kD = 3;                        // ring slots (X and W): 2 steps in
 constexpr int kLdsW = kD * kXSlot;           // weight rings after the X ring
 constexpr int kLdsCtl = kLdsW + kCW * kD * kWSlot;
 constexpr int kLds = kLdsCtl + 256;
-// GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50)
+// GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50), next layer's QKV [50, 58)
 constexpr int kOSteps = 4, kGUSteps = kKCH, kDSteps = kKCF / 8;
 constexpr int kGU0 = kOSteps, kD0 = kGU0 + kGUSteps, kSteps = kD0 + kDSteps;
+constexpr int kQN = 6144, kQTiles = 6, kQSplit = 4, kQSteps = kKCH / kQSplit;  // 64 x 96-col groups x 4 K splits
+constexpr int kQ0 = kSteps, kSteps2 = kQ0 + kQSteps;
 // sync words: counter k, shard s at word (8 k + s) * 32 (one 128-B line each)
-enum { kCntO = 0, kCntN1 = 1, kCntGU = 2 /* + group 0..7 */, kCntD = 10, kSyncCounters = 11 };
+enum { kCntO = 0, kCntN1 = 1, kCntGU = 2 /* + group 0..7 */, kCntD = 10, kCntN2 = 11, kSyncCounters = 12 };
 constexpr int kSpinLimit = 1 << 21;
 constexpr int kAuxSc1 = 16;   // buffer cache policy: sc1 (write-through / L1-bypassing)
 __host__ __device__ constexpr int sync_word(int k, int s) { return (8 * k + s) * 32; }
@@ -145,6 +151,11 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
       return p.wgu + ((size_t)(7 * b + min(w, 6)) * kKCH + (gs - kGU0)) * kTileChunk;
     }
     if (gs < kSteps) return p.wd + ((size_t)(8 * cg + w) * kKCF + kDSteps * ks + (gs - kD0)) * kTileChunk;
+    if (gs < kSteps2 && p.wqkv != nullptr) {  // next layer's QKV: 6 tiles (waves 0-5) x 8 chunks
+      if (w >= kQTiles) bytes = 0;
+      return p.wqkv + ((size_t)(kQTiles * (b >> 2) + min(w, kQTiles - 1)) * kKCH + kQSteps * (b & 3) + (gs - kQ0)) *
+                          kTileChunk;
+    }
     bytes = 0;
     return p.wo;
   };
@@ -166,7 +177,8 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
     int ldx, col;
     if (gs < kGU0) { X = p.attn; ldx = kH; col = 128 * (4 * ks + gs); }
     else if (gs < kD0) { X = p.xm; ldx = kH; col = 128 * (gs - kGU0); }
-    else { X = p.h; ldx = kF; col = 128 * (kDSteps * ks + gs - kD0); }
+    else if (gs < kSteps) { X = p.h; ldx = kF; col = 128 * (kDSteps * ks + gs - kD0); }
+    else { X = p.x; ldx = kH; col = 128 * (kQSteps * (b & 3) + gs - kQ0); }
     char* base = smem + (gs % kD) * kXSlot;
 #pragma unroll
     for (int i = 0; i < kRows / 4; ++i) {  // 16 DMA instructions of 4 rows x 256 B
@@ -176,7 +188,7 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   };
 
   // ---- counters this workgroup polls: bases read before it contributes anything ----
-  unsigned base_o = 0, base_n1 = 0, base_gu = 0, base_d = 0;
+  unsigned base_o = 0, base_n1 = 0, base_gu = 0, base_d = 0, base_n2 = 0;
   if (loader) {
     auto rd = [&](int k, int s) { return __hip_atomic_load(p.sync + sync_word(k, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     unsigned vo = lane < 8 ? rd(kCntO, lane) : 0u, vd = lane < 8 ? rd(kCntD, lane) : 0u;
@@ -186,6 +198,8 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
     vd = __builtin_amdgcn_readfirstlane(vd);
     const unsigned vn1 = __builtin_amdgcn_readfirstlane(rd(kCntN1, 0));
     const unsigned vgu = __builtin_amdgcn_readfirstlane(rd(kCntGU + ks, 0));
+    const unsigned vn2 = __builtin_amdgcn_readfirstlane(rd(kCntN2, 0));
+    base_n2 = vn2 - vn2 % 64u;
     base_o = vo - vo % 256u;
     base_d = vd - vd % 256u;
     base_n1 = vn1 - vn1 % 64u;
@@ -201,7 +215,8 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   }
 
   // ---- one GEMM item: steps [gs0, gs0 + nc) ----
-  // kind 0 = O / D (fp32 slab ks), 1 = gate_up (SiLU·mul -> h).  dep: counter polled before the first X load.
+  // kind 0 = O / D (fp32 slab ks), 1 = gate_up (SiLU·mul -> h), 2 = next layer's QKV (fp32 slab b & 3 of
+  // qkv_slabs).  dep: counter polled before the first X load; sig_k < 0: no completion counter.
   auto gemm_item = [&](int gs0, int nc, int kind, int active, int dep_k, int dep_shards, unsigned dep_base,
                        unsigned dep_exp, int sig_k, int sig_shard) {
     if (loader) {
@@ -241,7 +256,17 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
         }
       }
       if (c == nc - 1 && on) {
-        if (kind == 0) {
+        if (kind == 2) {
+          const __amdgpu_buffer_rsrc_t rs =
+              uniform_rsrc(p.qkv_slabs + (size_t)(b & 3) * M * kQN, (uint32_t)M * kQN * 4);
+          const int n = 16 * (kQTiles * (b >> 2) + w) + r;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][i]), rs,
+                                                    (uint32_t)(((16 * mt + 4 * g + i) * kQN + n) * 4), 0, kAuxSc1);
+        } else if (kind == 0) {
           // fp32 slab ks: part[ks][m][n], rows >= M dropped by the descriptor's range check
           const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(p.slabs + (size_t)ks * M * kH, (uint32_t)M * kH * 4);
           const int n = 16 * (8 * cg + w) + r;
@@ -277,7 +302,7 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
       issue_w(gs + kD - 1);  // after the item-end stores: the next vmcnt(4) retires them
     }
     vm_barrier<4>();  // end of item: every wave's stores retired
-    if (w == 0 && lane == 0) signal_counter(p.sync, sig_k, sig_shard);
+    if (sig_k >= 0 && w == 0 && lane == 0) signal_counter(p.sync, sig_k, sig_shard);
   };
 
   // ---- one norm row: resid[m] += sum of the 8 slabs; y[m] = rmsnorm(resid[m]) * wn (sc1 loads / stores) ----
@@ -350,7 +375,8 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   if (b < kRows) norm_item(b, p.w_ffn, p.xm, kCntO, 8, base_o, kCntN1);
   gemm_item(kGU0, kGUSteps, 1, 7, kCntN1, 1, base_n1, 64u, kCntGU + (b >> 5), 0);
   gemm_item(kD0, kDSteps, 0, 8, kCntGU + ks, 1, base_gu, 32u, kCntD, ks);
-  if (b >= kRows && b < 2 * kRows) norm_item(b - kRows, p.w_next, p.x, kCntD, 8, base_d, -1);
+  if (b >= kRows && b < 2 * kRows) norm_item(b - kRows, p.w_next, p.x, kCntD, 8, base_d, kCntN2);
+  if (p.wqkv != nullptr) gemm_item(kQ0, kQSteps, 2, kQTiles, kCntN2, 1, base_n2, 64u, -1, 0);
   // the look-ahead weight loads past the last step are range-failed dummies, but they still write the LDS: drain
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

@@ -235,13 +235,18 @@ class ModelRunner:
             self._decode_layers_wide(B, resid, x, part, nparts)
             return
         if self.mega and MEGA_MIN_B <= B <= MEGA_MAX_B:
-            # per layer: QKV + attention (2 launches), then the persistent MLP block (1 launch): O -> norm ->
-            # gate_up -> down -> norm with the weight stream running across the seams (decode_mega.hip)
+            # two launches per layer: the folded decode attention (QKV slab sum + RoPE + K/V write + attention), then
+            # the persistent block (decode_mega.hip): O -> norm -> gate_up -> down -> norm -> the NEXT layer's QKV
+            # projection, one launch whose weight stream runs across every seam.  Layer 0's QKV is its own launch.
+            fused_qkv = os.environ.get("DSSE_MEGA_QKV", "1") != "0"
             for li, L in enumerate(w.layers):
-                self._qkv_attention(li, L, B, x, part, nparts)
-                w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-                ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm, w_next, self.xm[r], self.h[r],
-                             x, self.split_part, self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps)
+                self._qkv_attention(li, L, B, x, part, nparts, slabs_ready=4 if (fused_qkv and li > 0) else 0)
+                nxt = w.layers[li + 1] if li + 1 < nl else None
+                ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm,
+                             nxt.attn_norm if nxt is not None else w.final_norm, self.xm[r], self.h[r], x,
+                             self.split_part, self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps,
+                             wqkv=nxt.wqkv_t if (fused_qkv and nxt is not None) else None,
+                             qkv_slabs=self.split_part)
             ops.gemm_out(x, w.lm_head_t, self.logits[r])
             self._sample_commit(B)
             ops.ring_advance(self.ring_counter)
@@ -293,7 +298,7 @@ class ModelRunner:
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
 
-    def _qkv_attention(self, li: int, L, B: int, x, part: int, nparts: int) -> None:
+    def _qkv_attention(self, li: int, L, B: int, x, part: int, nparts: int, slabs_ready: int = 0) -> None:
         """QKV projection + RoPE + KV write + decode attention of layer li.  The projection's split-K slabs go
         to split_part (free here: the previous norm consumed it) and the attention kernel folds their reduction,
         RoPE and the K/V write in (ops.qkv_attention_decode)."""
@@ -302,7 +307,7 @@ class ModelRunner:
         ops.qkv_attention_decode(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
                                  self.kv.v[li], nh, nkv, self.split_part, self.block_tables[r], self.q_start[r],
                                  self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], self.attn[r],
-                                 self.part_o, self.part_ml, part, nparts)
+                                 self.part_o, self.part_ml, part, nparts, slabs_ready)
 
     def _resid_proj(self, a, wt, resid, norm_w, x, tmp) -> None:
         """resid += a·wᵀ (TP: all-reduced), then x = RMSNorm(resid)·norm_w.  TP = 1: split-K slabs (if the GEMM

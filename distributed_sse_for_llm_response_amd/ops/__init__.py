@@ -168,14 +168,15 @@ def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx
 
 
 def qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, slabs, block_tables, q_start,
-                         q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts) -> int:
+                         q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts,
+                         slabs_ready: int = 0) -> int:
     """Decode QKV projection + RoPE + KV write + attention.  HIP: the GEMM leaves fp32 split-K slabs in `slabs`
     and the attention kernel folds the reduction, RoPE and the K/V write in (returns the slab count; 0 = it ran
     gemm_qkv_rope + paged_attention instead).  Same result as those two ops."""
     if _hip(x):
         return int(torch.ops.dsse.qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv,
                                                        slabs, block_tables, q_start, q_len, ctx_len, work_seq,
-                                                       work_tile, out, part_o, part_ml, part, nparts))
+                                                       work_tile, out, part_o, part_ml, part, nparts, slabs_ready))
     B = x.shape[0]
     ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
     ref.paged_attention(0, q_out.view(B, nh, 128), k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
@@ -194,14 +195,16 @@ def mega_sync(device) -> torch.Tensor:
     return torch.zeros(int(torch.ops.dsse.mega_sync_words()), dtype=torch.int32, device=device)
 
 
-def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps):
+def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv=None, qkv_slabs=None):
     """Decode MLP block in one launch (HIP, <= 64 rows, Mistral-7B shapes): resid += attn·woᵀ; xm = norm(resid)·w_ffn;
-    h = silu(xm·w_gᵀ)·(xm·w_uᵀ); resid += h·w_dᵀ; x = norm(resid)·w_next.  `err` [1] int32 is set when a bounded
-    in-kernel wait timed out (the engine's health word)."""
+    h = silu(xm·w_gᵀ)·(xm·w_uᵀ); resid += h·w_dᵀ; x = norm(resid)·w_next; with `wqkv` also the next layer's QKV
+    projection of x as 4 fp32 split-K slabs in `qkv_slabs` (for qkv_attention_decode(..., slabs_ready=4)).  `err` [1]
+    int32 is set when a bounded in-kernel wait timed out (the engine's health word)."""
     if _hip(attn):
-        torch.ops.dsse.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps)
+        torch.ops.dsse.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv,
+                                qkv_slabs)
     else:
-        ref.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps)
+        ref.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps, wqkv, qkv_slabs)
 
 
 def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):

@@ -130,3 +130,21 @@ def test_mega_mlp_repeated_launches_and_graph_replay(gpu, block):
     for k, v in want.items():
         assert torch.equal(b[k], v), f"graph replay changed {k}"
     assert torch.equal(b["attn"], attn)
+
+
+def test_mega_mlp_next_layer_qkv_slabs(gpu, block):
+    """The optional last phase: the next layer's QKV projection of x as 4 fp32 split-K slabs (their sum = x·Wqkvᵀ),
+    and qkv_attention_decode(slabs_ready=4) on them equals the unfused QKV + RoPE + attention."""
+    d = block
+    M = 64
+    g = torch.Generator().manual_seed(21)
+    wq = R.tile_weight((torch.randn(6144, H, generator=g) / math.sqrt(H)).bfloat16()).to(gpu)
+    slabs = torch.zeros(8 * M * H, device=gpu)
+    b = _bufs(M, gpu, 13)
+    ops.mega_mlp(b["attn"], d["wo"], d["wgu"], d["wd"], b["resid"], d["w_ffn"], d["w_next"], b["xm"], b["h"], b["x"],
+                 slabs, d["sync"], d["err"], 1e-5, wqkv=wq, qkv_slabs=slabs)
+    torch.cuda.synchronize()
+    assert int(d["err"].item()) == 0
+    got = slabs[: 4 * M * 6144].view(4, M, 6144).sum(0)
+    ref = b["x"].float() @ R.untile_weight(wq).float().t()
+    _close(got, ref, 2e-3, 2e-3, "qkv slabs")
