@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 #include <atomic>
 #include <string>
@@ -733,6 +734,27 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   return S;
 }
 
+// The decode QKV projection alone, as S fp32 split-K slabs [S, M, N] in `slabs` (the layer-0 input of the persistent
+// layer kernel, decode_mega.hip: every later layer's slabs come from the previous layer's launch).  Returns S.
+int64_t gemm_qkv_slabs(const Tensor& x, const Tensor& w, Tensor& slabs) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(slabs, "slabs");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(slabs, at::kFloat, "slabs");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == K && K % 128 == 0 && N % 16 == 0 && M >= 1 && M <= 64,
+              "gemm_qkv_slabs: [M <= 64, K] x [N, K]");
+  const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
+  TORCH_CHECK(gemm_impl(M, N, K) == 2 && c.ok && c.S > 1, "gemm_qkv_slabs: shape outside the split-K stream kernels");
+  TORCH_CHECK(slabs.numel() >= (int64_t)c.S * M * N, "gemm_qkv_slabs: slabs too small");
+  dsse::GemmEpi ep{};
+  DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, c.S, 1, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
+                               slabs.data_ptr<float>()));
+  return c.S;
+}
+
 dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
                                  const Tensor& seeds, const Tensor& positions,
                                  const c10::optional<Tensor>& active, int B) {
@@ -872,7 +894,12 @@ bool mega_supported() {
 int64_t mega_sync_words() { return (int64_t)dsse_mega_sync_words(); }
 void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Tensor& wd, Tensor& resid,
               const Tensor& w_ffn, const Tensor& w_next, Tensor& xm, Tensor& h, Tensor& x, Tensor& slabs, Tensor& sync,
-              Tensor& err, double eps, const c10::optional<Tensor>& wqkv, const c10::optional<Tensor>& qkv_slabs) {
+              Tensor& err, double eps, const c10::optional<Tensor>& wqkv, const c10::optional<Tensor>& qkv_slabs,
+              const c10::optional<Tensor>& qkv_in, int64_t qkv_in_S, const c10::optional<Tensor>& k_cache,
+              const c10::optional<Tensor>& v_cache, const c10::optional<Tensor>& block_tables,
+              const c10::optional<Tensor>& q_len, const c10::optional<Tensor>& ctx_len,
+              const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
+              const c10::optional<Tensor>& rope) {
   for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
                           (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
                           (const Tensor*)&err})
@@ -907,7 +934,7 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
     TORCH_CHECK(qkv_slabs->numel() >= (int64_t)4 * M * 6144, "mega_mlp: qkv_slabs hold 4 x M x 6144 floats");
   }
   dsse::MegaMlpParams p{};
-  p.attn = reinterpret_cast<const bf16*>(attn.data_ptr());
+  p.attn = reinterpret_cast<bf16*>(attn.data_ptr());
   p.wo = reinterpret_cast<const bf16*>(wo.data_ptr());
   p.wgu = reinterpret_cast<const bf16*>(wgu.data_ptr());
   p.wd = reinterpret_cast<const bf16*>(wd.data_ptr());
@@ -922,6 +949,42 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
   p.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
   p.wqkv = q ? reinterpret_cast<const bf16*>(wqkv->data_ptr()) : nullptr;
   p.qkv_slabs = q ? qkv_slabs->data_ptr<float>() : nullptr;
+  if (qkv_in.has_value() && qkv_in->defined()) {
+    // the layer's decode attention as the first phase (GQA 32 / 8 heads, page 32, one query per sequence)
+    for (const c10::optional<Tensor>* t : {&k_cache, &v_cache, &block_tables, &q_len, &ctx_len, &positions, &slots, &rope})
+      TORCH_CHECK(t->has_value() && (*t)->defined(), "mega_mlp: the attention phase needs every attention tensor");
+    for (const Tensor* t : {&*qkv_in, &*k_cache, &*v_cache, &*block_tables, &*q_len, &*ctx_len, &*positions, &*slots,
+                            &*rope})
+      check_gpu(*t, "mega_mlp attention tensor");
+    check_dtype(*qkv_in, at::kFloat, "qkv_in");
+    check_dtype(*rope, at::kFloat, "rope");
+    for (const Tensor* t : {&*block_tables, &*q_len, &*ctx_len, &*positions, &*slots}) check_dtype(*t, at::kInt, "metadata");
+    check_dtype(*k_cache, at::kBFloat16, "k_cache");
+    check_dtype(*v_cache, at::kBFloat16, "v_cache");
+    TORCH_CHECK(qkv_in_S >= 1 && qkv_in->numel() >= qkv_in_S * M * 6144, "mega_mlp: qkv_in holds S x M x 6144 floats");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == 8 && k_cache->size(2) == dsse::kBS && k_cache->size(3) == 128,
+                "mega_mlp: k_cache [blocks, 8, 32, 128]");
+    TORCH_CHECK(v_cache->sizes() == at::IntArrayRef({k_cache->size(0), 8, 128, dsse::kBS}), "mega_mlp: v_cache [blocks, 8, 128, 32]");
+    TORCH_CHECK(block_tables->dim() == 2 && block_tables->size(0) >= M, "mega_mlp: block_tables [>= M, max_blocks]");
+    TORCH_CHECK(q_len->numel() >= M && ctx_len->numel() >= M && positions->numel() >= M && slots->numel() >= M,
+                "mega_mlp: per-row metadata too short");
+    TORCH_CHECK(rope->dim() == 3 && rope->size(1) == 64 && rope->size(2) == 2, "mega_mlp: rope [P, 64, 2]");
+    p.qkv_in = qkv_in->data_ptr<float>();
+    p.qkv_in_S = (int)qkv_in_S;
+    p.k_cache = reinterpret_cast<bf16*>(k_cache->data_ptr());
+    p.v_cache = reinterpret_cast<bf16*>(v_cache->data_ptr());
+    p.block_tables = block_tables->data_ptr<int>();
+    p.max_blocks = (int)block_tables->size(1);
+    p.num_blocks = (int)k_cache->size(0);
+    p.num_slots = (int)(k_cache->size(0) * dsse::kBS);
+    p.q_len = q_len->data_ptr<int>();
+    p.ctx_len = ctx_len->data_ptr<int>();
+    p.positions = positions->data_ptr<int>();
+    p.slots = slots->data_ptr<int>();
+    p.rope = reinterpret_cast<const float2*>(rope->data_ptr<float>());
+    p.rope_len = (int)rope->size(0);
+    p.scale_log2 = 1.4426950408889634f / std::sqrt(128.f);
+  }
   p.M = M;
   p.eps = (float)eps;
   DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
@@ -991,11 +1054,14 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
   m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
         "Tensor(c!) epoch, Tensor(d!) err) -> ()");
+  m.def("gemm_qkv_slabs(Tensor x, Tensor w, Tensor(a!) slabs) -> int");
   m.def("mega_supported() -> bool", &mega_supported);
   m.def("mega_sync_words() -> int", &mega_sync_words);
   m.def("mega_mlp(Tensor attn, Tensor wo, Tensor wgu, Tensor wd, Tensor(a!) resid, Tensor w_ffn, Tensor w_next, "
         "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps, "
-        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None) -> ()");
+        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None, Tensor? qkv_in=None, int qkv_in_S=0, "
+        "Tensor(i!)? k_cache=None, Tensor(j!)? v_cache=None, Tensor? block_tables=None, Tensor? q_len=None, "
+        "Tensor? ctx_len=None, Tensor? positions=None, Tensor? slots=None, Tensor? rope=None) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
@@ -1020,4 +1086,5 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("sample_pick", &sample_pick);
   m.impl("ar_rmsnorm", &ar_rmsnorm);
   m.impl("mega_mlp", &mega_mlp);
+  m.impl("gemm_qkv_slabs", &gemm_qkv_slabs);
 }

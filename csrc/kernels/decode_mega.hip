@@ -70,14 +70,17 @@ constexpr int kWSlot = 4096;                 // one (16-column tile, 128-deep ch
 constexpr int kD = 3;                        // ring slots (X and W): 2 steps in flight + 1 being read
 constexpr int kLdsW = kD * kXSlot;           // weight rings after the X ring
 constexpr int kLdsCtl = kLdsW + kCW * kD * kWSlot;
-constexpr int kLds = kLdsCtl + 256;
+constexpr int kLdsFq = kLdsCtl + 1024;           // attention phase: per wave 6 x 128 bf16 (4 q heads, k, v)
+constexpr int kLds = kLdsFq + kCW * 6 * 256;     // 160,000 B
+static_assert(kLds <= 160 * 1024, "LDS budget");
+static_assert(2 * 3 * 32 * 64 * 4 <= kD * kXSlot, "attention merge area fits the X ring");
 // GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50), next layer's QKV [50, 58)
 constexpr int kOSteps = 4, kGUSteps = kKCH, kDSteps = kKCF / 8;
 constexpr int kGU0 = kOSteps, kD0 = kGU0 + kGUSteps, kSteps = kD0 + kDSteps;
 constexpr int kQN = 6144, kQTiles = 6, kQSplit = 4, kQSteps = kKCH / kQSplit;  // 64 x 96-col groups x 4 K splits
 constexpr int kQ0 = kSteps, kSteps2 = kQ0 + kQSteps;
 // sync words: counter k, shard s at word (8 k + s) * 32 (one 128-B line each)
-enum { kCntO = 0, kCntN1 = 1, kCntGU = 2 /* + group 0..7 */, kCntD = 10, kCntN2 = 11, kSyncCounters = 12 };
+enum { kCntO = 0, kCntN1 = 1, kCntGU = 2 /* + group 0..7 */, kCntD = 10, kCntN2 = 11, kCntA = 12, kSyncCounters = 13 };
 constexpr int kSpinLimit = 1 << 21;
 constexpr int kAuxSc1 = 16;   // buffer cache policy: sc1 (write-through / L1-bypassing)
 __host__ __device__ constexpr int sync_word(int k, int s) { return (8 * k + s) * 32; }
@@ -188,14 +191,17 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   };
 
   // ---- counters this workgroup polls: bases read before it contributes anything ----
-  unsigned base_o = 0, base_n1 = 0, base_gu = 0, base_d = 0, base_n2 = 0;
+  unsigned base_o = 0, base_n1 = 0, base_gu = 0, base_d = 0, base_n2 = 0, base_a = 0;
   if (loader) {
     auto rd = [&](int k, int s) { return __hip_atomic_load(p.sync + sync_word(k, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     unsigned vo = lane < 8 ? rd(kCntO, lane) : 0u, vd = lane < 8 ? rd(kCntD, lane) : 0u;
+    unsigned va = lane < 8 ? rd(kCntA, lane) : 0u;
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) { vo += __shfl_xor(vo, o); vd += __shfl_xor(vd, o); }
+    for (int o = 1; o < 8; o <<= 1) { vo += __shfl_xor(vo, o); vd += __shfl_xor(vd, o); va += __shfl_xor(va, o); }
     vo = __builtin_amdgcn_readfirstlane(vo);
     vd = __builtin_amdgcn_readfirstlane(vd);
+    va = __builtin_amdgcn_readfirstlane(va);
+    base_a = va - va % 256u;
     const unsigned vn1 = __builtin_amdgcn_readfirstlane(rd(kCntN1, 0));
     const unsigned vgu = __builtin_amdgcn_readfirstlane(rd(kCntGU + ks, 0));
     const unsigned vn2 = __builtin_amdgcn_readfirstlane(rd(kCntN2, 0));
@@ -370,8 +376,203 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
     if (sig_k >= 0 && w == 0 && lane == 0) signal_counter(p.sync, sig_k, 0);
   };
 
+  // ---- attention phase (optional): units (sequence, kv head) = (u >> 3, u & 7), u = 2b + (w >> 2), four key-split
+  // waves (w & 3) each; attention.hip paged_attention_kernel<1, 4, 1, 4>'s folded-QKV decode path (GQA group 4,
+  // one query per sequence, one partition), merged through the X ring region (free: O's X depends on this phase) ----
+  auto attn_item = [&]() {
+    float* mo = reinterpret_cast<float*>(smem);                    // [2 units][3 waves][32][64]
+    float* mml = reinterpret_cast<float*>(smem + kLdsCtl + 64);    // [2 units][4 waves][16] x (m, l)
+    const int j = w >> 2, kw = w & 3;
+    const int u = 2 * b + j, sq = u >> 3, hh = u & 7;
+    f32x4 o[8];
+    float m_run = -1e30f, l_run = 0.f;
+    bool col_valid = false;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int qlen = (!loader && sq < M) ? p.q_len[sq] : 0;
+    if (qlen > 0) {
+      const int ctx = p.ctx_len[sq];
+      const int qi = r >> 2;  // column r: query r / 4 (only query 0 exists in decode), head 4 hh + r % 4
+      col_valid = qi < qlen;
+      const int col_limit = col_valid ? ctx - qlen + qi + 1 : 0;
+      const int kend = ctx;
+      const int* bt = p.block_tables + (size_t)sq * p.max_blocks;
+      auto page_of = [&](int kb) {
+        const int i = __builtin_amdgcn_readfirstlane(DSSE_IDX(kb / 32, p.max_blocks, 0));
+        const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
+        return DSSE_IDX(cbt[i], p.num_blocks, 0);
+      };
+      // folded QKV epilogue: sum the slabs of this unit's 4 q heads, k and v; RoPE; regroup through LDS
+      const size_t slab = (size_t)M * kQN;
+      const int kn_page = (ctx - 1) & ~31;
+      const int sl = p.slots[sq];
+      const bool owner = sl >= 0 && ((kn_page / 32) & 3) == kw;
+      const int t = lane >> 3, jj = lane & 7;
+      const float* base = p.qkv_in + (size_t)sq * kQN + 16 * t + jj;
+      auto unit_col = [&](int uu) { return uu < 4 ? (4 * hh + uu) * 128 : (uu == 4 ? (32 + hh) * 128 : (40 + hh) * 128); };
+      float xa[6][2];
+#pragma unroll
+      for (int uu = 0; uu < 6; ++uu) xa[uu][0] = xa[uu][1] = 0.f;
+      for (int s = 0; s < p.qkv_in_S; ++s) {
+#pragma unroll
+        for (int uu = 0; uu < 6; ++uu) {
+          xa[uu][0] += base[s * slab + unit_col(uu)];
+          xa[uu][1] += base[s * slab + unit_col(uu) + 8];
+        }
+      }
+      const float2 cs = p.rope[(size_t)DSSE_IDX(p.positions[sq], p.rope_len, 0) * 64 + 8 * t + jj];
+      bf16* fq = reinterpret_cast<bf16*>(smem + kLdsFq + w * 1536);
+      const int d = 8 * t + jj;
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        fq[uu * 128 + d] = f2bf(xa[uu][0] * cs.x - xa[uu][1] * cs.y);
+        fq[uu * 128 + 64 + d] = f2bf(xa[uu][1] * cs.x + xa[uu][0] * cs.y);
+      }
+      if (owner) {
+        fq[4 * 128 + d] = f2bf(xa[4][0] * cs.x - xa[4][1] * cs.y);
+        fq[4 * 128 + 64 + d] = f2bf(xa[4][1] * cs.x + xa[4][0] * cs.y);
+        fq[5 * 128 + d] = f2bf(xa[5][0]);
+        fq[5 * 128 + 64 + d] = f2bf(xa[5][1]);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's own LDS rows
+      __builtin_amdgcn_wave_barrier();
+      bf16x8 qf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        qf[s] = col_valid ? *reinterpret_cast<const bf16x8*>(&fq[(r & 3) * 128 + 32 * s + 8 * g]) : zero_bf16x8();
+      float sc_new = -INFINITY;
+      int key_limit = col_limit;
+      if (owner) {
+        key_limit = col_limit - 1;  // the newest key is attended here, not in the page loop
+        bf16x8 kn[4];
+        float dot = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          kn[q] = *reinterpret_cast<const bf16x8*>(&fq[4 * 128 + 32 * q + 8 * g]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot += bf2f(qf[q][e]) * bf2f(kn[q][e]);
+        }
+        dot += __shfl_xor(dot, 16);
+        dot += __shfl_xor(dot, 32);
+        sc_new = col_valid ? dot * p.scale_log2 : -INFINITY;
+        const int sidx = DSSE_IDX(sl, p.num_slots, 0), blk = sidx / 32, off = sidx % 32;
+        if (r == (off & 15)) {
+          bf16* kdst = p.k_cache + (((size_t)blk * 8 + hh) * 32 + off) * 128 + 8 * g;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(kdst + 32 * q) = kn[q];
+        }
+        bf16* vdst = p.v_cache + ((size_t)blk * 8 + hh) * 128 * 32 + vperm_tok(off);
+        vdst[(size_t)d * 32] = f2bf(xa[5][0]);
+        vdst[(size_t)(64 + d) * 32] = f2bf(xa[5][1]);
+        if (col_valid) {  // the newest key opens the online softmax: m = its score, p = 1, o = its V row
+          m_run = sc_new;
+          l_run = g == 0 ? 1.f : 0.f;
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) {
+            const bf16x4 vq = *reinterpret_cast<const bf16x4*>(&fq[5 * 128 + 16 * dt + 4 * g]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[dt][i] = bf2f(vq[i]);
+          }
+        }
+      }
+      auto compute_page = [&](int kb, const bf16x8 (&k0)[4], const bf16x8 (&k1)[4], const bf16x8 (&vf)[8]) {
+        f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          s0 = mfma16x16x32(k0[s], qf[s], s0);
+          s1 = mfma16x16x32(k1[s], qf[s], s1);
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ka = kb + 4 * g + i, kb2 = kb + 16 + 4 * g + i;
+          s0[i] = (ka < key_limit) ? s0[i] * p.scale_log2 : -INFINITY;
+          s1[i] = (kb2 < key_limit) ? s1[i] * p.scale_log2 : -INFINITY;
+          tmax = fmaxf(tmax, fmaxf(s0[i], s1[i]));
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+        const float m_new = fmaxf(m_run, tmax);
+        const float alpha = exp2f(m_run - m_new);
+        m_run = m_new;
+        bf16x8 pf;
+        float psum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e0 = exp2f(s0[i] - m_new), e1 = exp2f(s1[i] - m_new);
+          psum += e0 + e1;
+          pf[i] = f2bf(e0);
+          pf[4 + i] = f2bf(e1);
+        }
+        l_run = l_run * alpha + psum;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+      };
+      int kb = 32 * kw;
+      int page = kb < kend ? page_of(kb) : 0;
+      for (; kb < kend; kb += 128) {
+        const bf16* kp = p.k_cache + ((size_t)page * 8 + hh) * 32 * 128;
+        const bf16* vp = p.v_cache + ((size_t)page * 8 + hh) * 128 * 32;
+        bf16x8 k0[4], k1[4], vf[8];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          k0[s] = ld_nt_bf16x8(kp + (size_t)r * 128 + 32 * s + 8 * g);
+          k1[s] = ld_nt_bf16x8(kp + (size_t)(16 + r) * 128 + 32 * s + 8 * g);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) vf[dt] = ld_nt_bf16x8(vp + (size_t)(16 * dt + r) * 32 + 8 * g);
+        page = page_of(min(kb + 128, kend - 1));
+        compute_page(kb, k0, k1, vf);
+      }
+      l_run += __shfl_xor(l_run, 16);
+      l_run += __shfl_xor(l_run, 32);
+      if (kw != 0) {
+        float* mw = mo + ((size_t)(j * 3 + kw - 1) * 32) * 64;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mw[(dt * 4 + i) * 64 + lane] = o[dt][i];
+      }
+      if (g == 0) {
+        mml[((j * 4 + kw) * 16 + r) * 2] = m_run;
+        mml[((j * 4 + kw) * 16 + r) * 2 + 1] = l_run;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // partials of every key-split wave in LDS
+    if (qlen > 0 && kw == 0 && col_valid) {
+      float mm = m_run;
+#pragma unroll
+      for (int v = 1; v < 4; ++v) mm = fmaxf(mm, mml[((j * 4 + v) * 16 + r) * 2]);
+      float scv[4], ll = 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float mv = v == 0 ? m_run : mml[((j * 4 + v) * 16 + r) * 2];
+        const float lv = v == 0 ? l_run : mml[((j * 4 + v) * 16 + r) * 2 + 1];
+        scv[v] = exp2f(mv - mm);
+        ll += lv * scv[v];
+      }
+      const float inv = ll > 0.f ? 1.f / ll : 0.f;
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(p.attn + (size_t)sq * kH, kH * 2);
+      const int col0 = (4 * hh + (r & 3)) * 128;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float a = o[dt][i] * scv[0];
+#pragma unroll
+          for (int v = 1; v < 4; ++v) a += mo[((size_t)(j * 3 + v - 1) * 32 + dt * 4 + i) * 64 + lane] * scv[v];
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, f2bf(a * inv)), rs,
+                                                (uint32_t)((col0 + 16 * dt + 4 * g + i) * 2), 0, kAuxSc1);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // attn rows stored (write-through)
+    if (w == 0 && lane == 0) signal_counter(p.sync, kCntA, b & 7);
+  };
+
   // ---- this workgroup's schedule ----
-  gemm_item(0, kOSteps, 0, 8, -1, 0, 0u, 0u, kCntO, ks);
+  const bool fused_attn = p.qkv_in != nullptr;
+  if (fused_attn) attn_item();
+  gemm_item(0, kOSteps, 0, 8, fused_attn ? kCntA : -1, 8, base_a, 256u, kCntO, ks);
   if (b < kRows) norm_item(b, p.w_ffn, p.xm, kCntO, 8, base_o, kCntN1);
   gemm_item(kGU0, kGUSteps, 1, 7, kCntN1, 1, base_n1, 64u, kCntGU + (b >> 5), 0);
   gemm_item(kD0, kDSteps, 0, 8, kCntGU + ks, 1, base_gu, 32u, kCntD, ks);

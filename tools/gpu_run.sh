@@ -1,0 +1,44 @@
+#!/bin/bash
+# One parameterised GPU-box session (replaces the per-experiment tools/gpu_r3*.sh scripts).
+#   tools/gpu_run.sh OUTDIR STEP [STEP ...]
+# Steps (each under its own time limit; a crash, fault or timeout ends the session at once):
+#   mega_test     tests/test_mega_gpu.py                 mega_bench    tools/bench_mega.py --M 64
+#   model_test    tests/test_model_full_dims_gpu.py      ar_test       tests/test_custom_ar_gpu.py
+#   gpu_tests     the whole GPU suite (pytest -m gpu)    smoke         __graft_entry__.smoke()
+#   bench64       bench.py (driver form, 64 streams)     bench64_off   the same with DSSE_MEGA=0
+#   bench256      bench.py --streams 256                 prof64        rocprofv3 kernel trace of bench.py
+#   ttft8k        tools/bench_ttft.py --prompt-len 8192  c3stub        8 paced stub replicas x 256 streams (CPU only)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+out=gpurun_out/$1; shift
+mkdir -p "$out"
+export TMPDIR=/tmp
+step() {  # name, timeout, cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" >> "$out/session.log"
+  timeout -k 10 "$t" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >> "$out/session.log"
+  tail -3 "$out/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
+for s in "$@"; do
+  case $s in
+    mega_test) step mega_test 300 $PYT tests/test_mega_gpu.py ;;
+    mega_bench) step mega_bench 300 python -u tools/bench_mega.py --M 64 ;;
+    model_test) step model_test 600 $PYT tests/test_model_full_dims_gpu.py ;;
+    ar_test) step ar_test 900 $PYT tests/test_custom_ar_gpu.py ;;
+    gpu_tests) step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench64) step bench64 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench64_off) DSSE_MEGA=0 step bench64_off 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
+    prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
+    ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
+    c3stub) HIP_VISIBLE_DEVICES= DSSE_DIST_BACKEND=gloo step c3stub 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 8 --streams 256 --steps 64 --warmup 8 --stub-step-ms 9.7 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "session done"
