@@ -70,8 +70,9 @@ constexpr int kWSlot = 4096;                 // one (16-column tile, 128-deep ch
 constexpr int kD = 3;                        // ring slots (X and W): 2 steps in flight + 1 being read
 constexpr int kLdsW = kD * kXSlot;           // weight rings after the X ring
 constexpr int kLdsCtl = kLdsW + kCW * kD * kWSlot;
-constexpr int kLdsFq = kLdsCtl + 1024;           // attention phase: per wave 6 x 128 bf16 (4 q heads, k, v)
-constexpr int kLds = kLdsFq + kCW * 6 * 256;     // 160,000 B
+// control area: norm partial sums [8] at +0, attention merge statistics [2][4][16] x (m, l) at +64 (1 KiB)
+constexpr int kLdsFq = kLdsCtl + 2048;           // attention phase: per wave 6 x 128 bf16 (4 q heads, k, v)
+constexpr int kLds = kLdsFq + kCW * 6 * 256;     // 161,792 B
 static_assert(kLds <= 160 * 1024, "LDS budget");
 static_assert(2 * 3 * 32 * 64 * 4 <= kD * kXSlot, "attention merge area fits the X ring");
 // GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50), next layer's QKV [50, 58)
