@@ -18,7 +18,10 @@ a first-token timeout only).  Here:
     ``seed=S``                 RNG seed for drop_token
   ``DSSE_FAULTS_RANKS=1,3`` restricts the faults to those ranks (e.g. crash one DP replica of eight).
 * ``Watchdog`` — marks the replica not-ready while it has work but no step completed for ``timeout_s``
-  (default ``DSSE_WATCHDOG_S``=30), and ready again when steps resume.
+  (default ``DSSE_WATCHDOG_S``=30), and ready again when steps resume.  A stall past ``DSSE_STEP_FAIL_S`` (120 s;
+  0 = never) is a device or peer hang the loop cannot leave by itself (a TP peer gone while this rank waits inside
+  an RCCL collective): every live stream gets the reference's [ERROR] token and the process exits with status 3
+  (``DSSE_STEP_FAIL_EXIT=0``: readiness stays down instead, for tests).
 * ``StepTracer`` — ``DSSE_TRACE=/path.jsonl`` writes one JSON line per engine step (wall time, step
   latency, batch, queue, tokens out); ``DSSE_ROCTX=1`` wraps each step in a roctx range (visible in
   ``rocprofv3 --marker-trace`` timelines next to the kernels).
@@ -97,14 +100,30 @@ class FaultPlan:
 class Watchdog(threading.Thread):
     """Readiness follows engine progress: not ready while work is pending and no step finished recently."""
 
-    def __init__(self, loop, set_ready, timeout_s: float | None = None, period_s: float = 0.2):
+    def __init__(self, loop, set_ready, timeout_s: float | None = None, period_s: float = 0.2,
+                 fail_s: float | None = None):
         super().__init__(daemon=True, name="engine-watchdog")
         self.loop, self.set_ready = loop, set_ready
         self.timeout_s = float(os.environ.get("DSSE_WATCHDOG_S", "30")) if timeout_s is None else timeout_s
+        self.fail_s = float(os.environ.get("DSSE_STEP_FAIL_S", "120")) if fail_s is None else fail_s
         self.period_s = period_s
         self.stalled = False
+        self.failed = False
         self.trips = 0
         self._stop = threading.Event()
+
+    def _fail(self, idle_for: float) -> None:
+        """The loop is stuck inside a device or collective wait: end every live stream with [ERROR], then exit."""
+        self.failed = True
+        print(json.dumps({"level": "ERROR", "msg": "engine hung; failing every stream", "seconds": round(idle_for, 3)}),
+              flush=True)
+        try:
+            self.loop.publish(self.loop.engine.fail_all())  # the loop thread is blocked: nothing else mutates it now
+        finally:
+            self.set_ready(False)
+            if os.environ.get("DSSE_STEP_FAIL_EXIT", "1") != "0":
+                time.sleep(0.5)  # the I/O threads write the [ERROR] frames
+                os._exit(3)
 
     def run(self):
         while not self._stop.wait(self.period_s):
@@ -113,6 +132,9 @@ class Watchdog(threading.Thread):
             busy = self.loop.engine.runnable()  # streams paused by flow control are not a stall
             idle_for = time.monotonic() - self.loop.last_progress
             stalled = busy and idle_for > self.timeout_s
+            if stalled and self.fail_s > 0 and idle_for > self.fail_s and not self.failed:
+                self._fail(idle_for)
+                return
             if stalled and not self.stalled:
                 self.trips += 1
                 print(json.dumps({"level": "WARN", "msg": "engine stalled", "seconds": round(idle_for, 3)}), flush=True)

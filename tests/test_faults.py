@@ -126,6 +126,36 @@ def test_device_health_fault_ends_every_stream_with_error(monkeypatch):
         app.stop()
 
 
+def test_hung_engine_step_fails_every_stream_with_error(monkeypatch):
+    """A step that never returns (a TP peer gone while this rank waits inside an RCCL collective, a hung device):
+    past DSSE_STEP_FAIL_S the watchdog ends every live stream with [ERROR] and (in production) exits the process."""
+    monkeypatch.setenv("DSSE_FAULTS", "stall_after_steps=2:4000")
+    monkeypatch.setenv("DSSE_WATCHDOG_S", "0.2")
+    monkeypatch.setenv("DSSE_STEP_FAIL_S", "0.8")
+    monkeypatch.setenv("DSSE_STEP_FAIL_EXIT", "0")
+    app = _app(max_tokens=64)
+    try:
+        port = app.port("edge")
+        out = []
+        ts = [threading.Thread(target=lambda: out.append(request(H, port, "POST", "/chat", {"message": f"h{i}"},
+                                                                 timeout=30)))
+              for i in range(2)]
+        t0 = time.time()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(30)
+        assert len(out) == 2
+        for r in out:
+            toks = [json.loads(e.data) for e in r.events if e.event == "token"]
+            assert toks and toks[-1]["done"] and toks[-1]["token"] == "[ERROR]"
+        assert time.time() - t0 < 4.0  # ended by the watchdog, not by the stall running out
+        assert request(H, port, "GET", "/readyz").status == 503
+        assert app.watchdog.failed
+    finally:
+        app.stop()
+
+
 def _free_port():
     s = socket.socket()
     s.bind((H, 0))
