@@ -7,9 +7,8 @@
 //
 //   workgroup  = one KV head x 64 query tokens; 2G waves (G = Hq/Hkv q heads x 2 halves of 32
 //                queries), so every K/V byte staged in LDS feeds 2G waves (GQA reuse in LDS);
-//   key loop   = 64 keys (two 32-token pages) per iteration, double-buffered LDS (2 x 32 KiB);
-//                the next block's K and V are loaded into registers before the MFMAs of this block
-//                and written to the other buffer after them (one barrier per iteration);
+//   key loop   = 64 keys (two 32-token pages) per block, a 4-block LDS ring (4 x 32 KiB) filled by LDS-DMA
+//                three blocks ahead;
 //   scores     = Sᵀ = K·Qᵀ (keys on MFMA rows, queries on lanes): a query's softmax statistics live
 //                in one lane column, and the exponentiated scores are already the B operand of
 //                Oᵀ = Vᵀ·Pᵀ — the V cache stores each page transposed with the token permutation
@@ -17,14 +16,14 @@
 //   LDS images = K [64 keys][256 B] with the XOR-swizzled 16-byte chunks of gemm_xlds, Vᵀ [128 d]
 //                [128 B] with chunk ^= (d >> 1) & 7: both read with conflict-free ds_read_b128;
 //   softmax    = online, base 2, masked scores contribute exactly 0 (fully masked columns stay 0).
+//
+// Schedule (round 4): two phases per key block, QKᵀ(j) | softmax(j) + PV(j), one barrier before each, and the
+// two query halves staggered by one barrier.  Waves w and w + 4 share a SIMD (G = 4: the same head, the two
+// query halves), so while one runs the 32 MFMAs of its QKᵀ the other runs its softmax VALU work and then its PV
+// MFMAs: the SIMD sees MFMA work from one wave under the other's exp / max / convert chain.  The round-1..3 form
+// (all waves in lockstep, one barrier per two blocks) measured MFMA busy 22 %, 34 % of wave time waiting on
+// dependencies (profiles/pmc_flash_prefill_r1.md): both waves of a SIMD reached their softmax at the same time.
 #include "api.h"
-
-// K/V staging by LDS-DMA (global_load_lds, no VGPRs, no ds_write pass; the round-1 register-staged form measured
-// slower and was removed).
-#ifndef DSSE_PREFILL_GLDS
-#define DSSE_PREFILL_GLDS 1
-#endif
-
 
 namespace dsse {
 
@@ -37,9 +36,10 @@ DEV void glds16(const void* src, char* lds_base) {
 }
 constexpr int kD = 128;
 constexpr int kBQ = 64;    // query tokens per workgroup
-constexpr int kBK = 64;    // keys per iteration (2 pages)
+constexpr int kBK = 64;    // keys per block (2 pages)
 constexpr int kKBytes = kBK * kD * 2;  // 16 KiB
-constexpr int kStage = 2 * kKBytes;    // K + Vᵀ
+constexpr int kStage = 2 * kKBytes;    // K + Vᵀ of one block
+constexpr int kRing = 4;               // LDS blocks
 constexpr float kRescaleThr = 8.f;     // deferred online-softmax rescale threshold (log2 units)
 
 // KV block of page `pg` (clamped to the last page: pages past the context are a harmless, masked re-read).
@@ -54,23 +54,19 @@ DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
 }
 }  // namespace
 
-// K/V staging: two 64-key blocks per LDS stage and per barrier (4 x 32 KiB dynamic LDS); the next stage's loads
-// are issued into registers at the top of an iteration and written to the other LDS stage at its end.  Measured
-// against one block per stage with one or two blocks of register prefetch, and against a software-pipelined
-// variant (QKᵀ of block j+1 in the basic block of block j's softmax): 8k TTFT 115.5 vs 116.1 / 116.6 / 116.8 ms
-// (profiles/experiments_r1.md); those variants were removed in round 2.
 template <int G>
 __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   constexpr int NW = 2 * G;
-  constexpr int NT = 64 * NW;
-  constexpr int PIECES = kStage / 16;  // 16-byte pieces per stage = 2048
-  constexpr int PPT = PIECES / NT;             // pieces per thread
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 4 stages of kStage
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // kRing blocks of kStage
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int r = lane & 15, g = lane >> 4;
   const int wh = w % G, wq = w / G;
-  const int item = blockIdx.x, h = blockIdx.y;
+  // flat grid, head fastest: workgroup b runs on XCD b % 8, so with Hkv = 8 every XCD serves ONE kv head and
+  // its 4 MiB of 8k-context K/V stays in that XCD's L2 for all the head's query tiles (a (tile, head) grid put
+  // consecutive tiles on different XCDs and every XCD streamed all 8 heads); the work list is heaviest-first
+  // globally, not per head
+  const int item = blockIdx.x / p.hkv, h = blockIdx.x % p.hkv;
   const int b = p.work_seq[item];
   const int qlen = p.q_len[b], ctx = p.ctx_len[b];
   const int pos0 = ctx - qlen;                 // absolute position of query 0 of this chunk
@@ -95,52 +91,26 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[qt][s] = ld_bf16x8(qp + 8 * s);
   }
-
-  // ---- staging: pieces [0, 1024) = K (page, token, 16-byte chunk), [1024, 2048) = V (page, d, chunk)
-  auto load_block = [&](int j, bf16x8 (&st)[PPT]) {
-    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
+  // retire the Q loads here, before any DMA is issued: otherwise the compiler's wait for them at the first QKᵀ
+  // MFMA (behind an unknown number of loop-carried DMAs) is a vmcnt(0) inside the loop, draining the prefetch
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = threadIdx.x + i * NT;
-      const int v = pc >> 10, off = pc & 1023;
-      const int page = off >> 9, o2 = off & 511;
-      const int blk = page ? blk1 : blk0;
-      const bf16* src = v == 0 ? p.k_cache + (((size_t)blk * p.hkv + h) * kBS + (o2 >> 4)) * kD + 8 * (o2 & 15)
-                               : p.v_cache + (((size_t)blk * p.hkv + h) * kD + (o2 >> 2)) * kBS + 8 * (o2 & 3);
-      st[i] = ld_bf16x8(src);
-    }
-  };
-  auto store_block = [&](int buf, const bf16x8 (&st)[PPT]) {
-    char* base = smem + buf * kStage;
+  for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = threadIdx.x + i * NT;
-      const int v = pc >> 10, off = pc & 1023;
-      const int page = off >> 9, o2 = off & 511;
-      int dst;
-      if (v == 0) {
-        const int key = page * kBS + (o2 >> 4), c = o2 & 15;
-        dst = key * 256 + ((c ^ swz(key & 15)) << 4);
-      } else {
-        const int d = o2 >> 2, c = page * 4 + (o2 & 3);
-        dst = kKBytes + d * 128 + ((c ^ ((d >> 1) & 7)) << 4);
-      }
-      *reinterpret_cast<bf16x8*>(base + dst) = st[i];
-    }
-  };
+    for (int s = 0; s < 4; ++s) asm volatile("" ::"v"(qf[qt][s]));
 
-  // LDS-DMA form: a stage is 32 x 1 KiB DMA instructions, IPW per wave.  Instruction q < 16 fills keys 4q..4q+3
+  // LDS-DMA: a block is 32 x 1 KiB DMA instructions, IPW per wave.  Instruction q < 16 fills keys 4q..4q+3
   // (lane -> key 4q + lane / 16, LDS slot lane % 16 = chunk ^ swz(key)); q >= 16 fills Vᵀ rows d = 8 (q - 16)
   // + lane / 8 (slot lane % 8 = chunk ^ ((d >> 1) & 7), chunk = page * 4 + 8-token group).  The swizzles sit
-  // on the source address because the DMA writes LDS lane-linearly; the reads are unchanged.
+  // on the source address because the DMA writes LDS lane-linearly; the reads are unchanged.  Blocks past the
+  // last are issued too (pages clamp to the context, nobody reads them): a branch around the DMA made the
+  // compiler's waitcnt placement drain every load in flight.
   constexpr int IPW = 32 / NW;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto issue_block = [&](int j, int buf) {
+  auto issue_block = [&](int j) {
     const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
-    char* base = smem + buf * kStage;
+    char* base = smem + (j % kRing) * kStage;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const int q = wu * IPW + i;  // wave-uniform
+      const int q = w * IPW + i;  // wave-uniform
       const bf16* src;
       if (q < 16) {
         const int key = 4 * q + (lane >> 4), c = (lane & 15) ^ swz(key & 15);
@@ -160,142 +130,136 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
     for (int qt = 0; qt < 2; ++qt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
   const float sc = p.scale_log2;
+  f32x4 s4[4][2];  // Sᵀ[key tile kt][query tile qt] of the current block, live across the mid-block barrier
 
-#if !DSSE_PREFILL_GLDS
-  bf16x8 st0[PPT], st1[PPT];
-  load_block(0, st0);
-  store_block(0, st0);
-#else
-  (void)load_block;
-  (void)store_block;
-#endif
-  // softmax + PV of key block j staged in LDS buffer `buf`
-  auto compute_block = [&](int j, int buf) {
-    const int key0 = j * kBK;
-    if (key0 <= w_last_pos) {  // this wave sees at least one key of the block
-      const char* kb = smem + buf * kStage;
-      const char* vb = kb + kKBytes;
-      // Sᵀ[key tile kt][query tile qt]
-      f32x4 s4[4][2];
+  // phase 1: Sᵀ = K·Qᵀ of the block in LDS slot `buf`
+  auto qk = [&](int buf) {
+    const char* kb = smem + buf * kStage;
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
+    for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int row = 16 * kt + r;
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 256 + (((4 * g + s) ^ swz(r)) << 4));
+      for (int s = 0; s < 4; ++s) {
+        const int row = 16 * kt + r;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 256 + (((4 * g + s) ^ swz(r)) << 4));
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
-        }
+        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
       }
-      const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
-      bf16x8 pf[2][2];  // [qt][page t]
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // phase 2: online softmax of block j and Oᵀ += Vᵀ·Pᵀ
+  auto sm_pv = [&](int j, int buf) {
+    const int key0 = j * kBK;
+    const char* vb = smem + buf * kStage + kKBytes;
+    const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
+    bf16x8 pf[2][2];  // [qt][page t]
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const int qpos = pos0 + q0 + 16 * qt + r;
-        const bool qvalid = q0 + 16 * qt + r < qlen;
-        // max over the RAW scores (scale_log2 > 0 commutes with max); masked scores become -1e30
-        float mx = -1e30f;
-        if (need_mask) {
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int key = key0 + 16 * kt + 4 * g + i;
-              const float v = (qvalid && key <= qpos) ? s4[kt][qt][i] : -1e30f;
-              s4[kt][qt][i] = v;
-              mx = fmaxf(mx, v);
-            }
-        } else {
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s4[kt][qt][i]);
-        }
-        mx = rows4_max(mx);
-        // Deferred rescale: the running max (log2 units) only moves when a query's block max exceeds it by
-        // more than kRescaleThr, so after the first blocks O and l are not rescaled at all (P <= 2^thr stays
-        // well inside bf16 / fp32 range; the final O / l is unchanged).  Decided per wave (any lane).
-        const float m_blk = mx * sc;
-        if (__any(m_blk > m_run[qt] + kRescaleThr)) {
-          const float m_new = fmaxf(m_run[qt], m_blk);
-          // a column with no visible key yet keeps m = -1e30 and must produce p = 0, not exp2(0)
-          const float alpha = __builtin_amdgcn_exp2f(m_run[qt] - (m_new < -1e29f ? 0.f : m_new));
-          l_run[qt] *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < 8; ++dt) {
-            o[dt][qt][0] *= alpha;
-            o[dt][qt][1] *= alpha;
-            o[dt][qt][2] *= alpha;
-            o[dt][qt][3] *= alpha;
-          }
-          m_run[qt] = m_new;
-        }
-        const float m_use = m_run[qt] < -1e29f ? 0.f : m_run[qt];
-        // raw v_exp_f32 (no denormal range reduction: arguments are <= thr and underflow to 0 is wanted);
-        // the scale is folded into one FMA per score
-        float sum = 0.f;
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qpos = pos0 + q0 + 16 * qt + r;
+      const bool qvalid = q0 + 16 * qt + r < qlen;
+      // max over the RAW scores (scale_log2 > 0 commutes with max); masked scores become -1e30
+      float mx = -1e30f;
+      if (need_mask) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(s4[kt][qt][i], sc, -m_use));
-            s4[kt][qt][i] = e;
-            sum += e;
+            const int key = key0 + 16 * kt + 4 * g + i;
+            const float v = (qvalid && key <= qpos) ? s4[kt][qt][i] : -1e30f;
+            s4[kt][qt][i] = v;
+            mx = fmaxf(mx, v);
           }
-        l_run[qt] += rows4_sum(sum);
-        // Pᵀ fragments: page t = key tiles 2t (keys 4g+i) and 2t+1 (keys 16+4g+i)
+      } else {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            pf[qt][t][i] = f2bf(s4[2 * t][qt][i]);
-            pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
-          }
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s4[kt][qt][i]);
       }
-      // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
+      mx = rows4_max(mx);
+      // Deferred rescale: the running max (log2 units) only moves when a query's block max exceeds it by
+      // more than kRescaleThr, so after the first blocks O and l are not rescaled at all (P <= 2^thr stays
+      // well inside bf16 / fp32 range; the final O / l is unchanged).  Decided per wave (any lane).
+      const float m_blk = mx * sc;
+      if (__any(m_blk > m_run[qt] + kRescaleThr)) {
+        const float m_new = fmaxf(m_run[qt], m_blk);
+        // a column with no visible key yet keeps m = -1e30 and must produce p = 0, not exp2(0)
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qt] - (m_new < -1e29f ? 0.f : m_new));
+        l_run[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+          o[dt][qt][0] *= alpha;
+          o[dt][qt][1] *= alpha;
+          o[dt][qt][2] *= alpha;
+          o[dt][qt][3] *= alpha;
+        }
+        m_run[qt] = m_new;
+      }
+      const float m_use = m_run[qt] < -1e29f ? 0.f : m_run[qt];
+      // raw v_exp_f32 (no denormal range reduction: arguments are <= thr and underflow to 0 is wanted);
+      // the scale is folded into one FMA per score
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(s4[kt][qt][i], sc, -m_use));
+          s4[kt][qt][i] = e;
+          sum += e;
+        }
+      l_run[qt] += rows4_sum(sum);
+      // Pᵀ fragments: page t = key tiles 2t (keys 4g+i) and 2t+1 (keys 16+4g+i)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-          const int d = 16 * dt + r;
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vb + d * 128 + (((t * 4 + g) ^ ((d >> 1) & 7)) << 4));
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
+        for (int i = 0; i < 4; ++i) {
+          pf[qt][t][i] = f2bf(s4[2 * t][qt][i]);
+          pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
         }
     }
+    // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const int d = 16 * dt + r;
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vb + d * 128 + (((t * 4 + g) ^ ((d >> 1) & 7)) << 4));
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
+      }
+    __builtin_amdgcn_s_setprio(0);
   };
-  // stage s = blocks 2s, 2s + 1 in buffers 2 (s & 1) + {0, 1}.  Loads and stores are unconditional (pages clamp
-  // to the context; blocks past the last are never read): a branch around them made the compiler's waitcnt
-  // placement drain every load in flight (vmcnt(0)).
-#if DSSE_PREFILL_GLDS
-  // the barrier's fence waits vmcnt(0): the pair's DMA (issued an iteration earlier) has landed everywhere, and
-  // every wave is done reading the other pair, which this iteration's DMA then overwrites
-  issue_block(0, 0);
-  issue_block(1, 1);
-  for (int j = 0; j < nblk; j += 2) {
-    __syncthreads();
-    const int nb = ((j >> 1) + 1) & 1;
-    issue_block(j + 2, 2 * nb);
-    issue_block(j + 3, 2 * nb + 1);
-    compute_block(j, 2 * (nb ^ 1));
-    compute_block(j + 1, 2 * (nb ^ 1) + 1);
+
+  // Barrier accounting (absolute barriers, counted from the loop entry of the leading half; the lagging half,
+  // wq = 1, passes one extra barrier first and one fewer at the end).  Leading half: QKᵀ(j) in interval 2j,
+  // softmax/PV(j) in 2j + 1; lagging half one interval later.  So block j is read in intervals 2j .. 2j + 2:
+  //   RAW  every wave's DMA of block j has retired (its own counted vmcnt) before barrier 2j;
+  //   WAR  block j + 4 reuses j's slot; its DMA is issued at the start of softmax/PV(j + 1), i.e. in interval
+  //        2j + 3 (leading) or 2j + 4 (lagging), after every read of block j (the last in interval 2j + 2).
+  // Each wave issues block j + 3 at the start of its softmax/PV(j) phase, so at the barrier before QKᵀ(j) the
+  // leading half has blocks up to j + 2 issued (wait: all but the 2 youngest blocks), and at the barrier before
+  // softmax/PV(j), which for the lagging half is absolute barrier 2(j + 1), the lagging half needs block j + 1
+  // with blocks up to j + 2 issued (wait: all but the youngest).
+  const bool lag = wq == 1;
+  issue_block(0);
+  issue_block(1);
+  issue_block(2);
+  if (lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
+  for (int j = 0; j < nblk; ++j) {
+    const bool vis = j * kBK <= w_last_pos;  // this wave sees at least one key of the block
+    if (!lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
+    else asm volatile("s_barrier" ::: "memory");
+    if (vis) qk(j % kRing);
+    if (!lag) asm volatile("s_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(IPW) : "memory");
+    issue_block(j + 3);
+    if (vis) sm_pv(j, j % kRing);
   }
-#else
-  load_block(1, st1);
-  store_block(1, st1);
-  for (int j = 0; j < nblk; j += 2) {
-    __syncthreads();
-    const int nb = ((j >> 1) + 1) & 1;
-    load_block(j + 2, st0);
-    load_block(j + 3, st1);
-    compute_block(j, 2 * (nb ^ 1));
-    compute_block(j + 1, 2 * (nb ^ 1) + 1);
-    store_block(2 * nb, st0);
-    store_block(2 * nb + 1, st1);
-  }
-#endif
+  if (!lag) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may still write this workgroup's LDS after it exits
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
 #pragma unroll
@@ -318,25 +282,26 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
 
 }  // namespace dsse
 
-// Work items: (sequence, 64-query tile) pairs; grid = (num_work, Hkv).  Requires G = Hq/Hkv in {1, 2, 4}.
+// Work items: (sequence, 64-query tile) pairs; grid = num_work x Hkv workgroups, head fastest.  Requires G = Hq/Hkv in {1, 2, 4}.
 extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
   using namespace dsse;
   if (num_work <= 0) return hipSuccess;
-  const dim3 grid(num_work, p->hkv);
+  const dim3 grid(num_work * p->hkv);
+  constexpr int lds = kRing * kStage;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<4>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
   switch (p->group) {
-    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1>), grid, dim3(128), 4 * kStage, st, *p); break;
-    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2>), grid, dim3(256), 4 * kStage, st, *p); break;
-    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4>), grid, dim3(512), 4 * kStage, st, *p); break;
+    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1>), grid, dim3(128), lds, st, *p); break;
+    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2>), grid, dim3(256), lds, st, *p); break;
+    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4>), grid, dim3(512), lds, st, *p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -8,6 +8,9 @@
 #   bench64       bench.py (driver form, 64 streams)     bench64_off   the same with DSSE_MEGA=0
 #   bench256      bench.py --streams 256                 prof64        rocprofv3 kernel trace of bench.py
 #   ttft8k        tools/bench_ttft.py --prompt-len 8192  c3stub        8 paced stub replicas x 256 streams (CPU only)
+#   attn_bench    tools/bench_prefill_attn.py (8k / 512 causal, + SDPA arm)
+#   gemm_bench    tools/bench_gemm_tiled.py at M = 8192 and 256 (engine dispatch vs library)
+#   attn_test     tests/test_kernels_gpu.py -k prefill     pmc_attn / pmc_gemm  two rocprofv3 --pmc passes each
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/$1; shift
@@ -38,6 +41,17 @@ for s in "$@"; do
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     c3stub) HIP_VISIBLE_DEVICES= DSSE_DIST_BACKEND=gloo step c3stub 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 8 --streams 256 --steps 64 --warmup 8 --stub-step-ms 9.7 ;;
+    attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill" ;;
+    attn_bench) step attn_bench 300 python -u tools/bench_prefill_attn.py --T 8192,2048,512 --sdpa ;;
+    gemm_bench) step gemm_bench 300 python -u tools/bench_gemm_tiled.py --M 8192,256 --cfg auto ;;
+    pmc_attn)
+      step pmc_attn_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_attn_a" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
+      step pmc_attn_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_attn_b" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
+      python3 tools/pmc_sum.py "$out/pmc_attn_a" "$out/pmc_attn_b" --kernel flash_prefill --title "flash prefill, 8k causal, 32/8 heads" > "$out/pmc_attn.md" 2>&1 ;;
+    pmc_gemm)
+      step pmc_gemm_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_gemm_a" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
+      step pmc_gemm_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_gemm_b" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
+      python3 tools/pmc_sum.py "$out/pmc_gemm_a" "$out/pmc_gemm_b" --kernel gemm --title "gate_up GEMM (N 28672, K 4096) at M = 8192 and 256" > "$out/pmc_gemm.md" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
