@@ -97,6 +97,8 @@ struct MegaMlpParams {
   const int* slots;      // [M]
   const float2* rope;    // [rope_len, 64]
   float scale_log2;
+  unsigned long long* stamps;  // optional [256][16] s_memrealtime (100 MHz) phase stamps, decode_mega.hip
+  int pf_steps;                // seam prefetch steps per compute wave (0 .. mega::kPF), decode_mega.hip
   unsigned* sync;      // dsse_mega_sync_words() words, zeroed once at allocation, never reset
   unsigned* err;       // set to 1 when a bounded wait timed out (the engine's health word, read at drain time)
   int M;

@@ -219,7 +219,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 4) {
+  if (cfg < 0 || cfg > 5) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
     // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
     // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
@@ -234,6 +234,10 @@ TCfg pick_tiled(int M, int N, int K) {
     // change measured 9.81 vs 9.71 ms per step (twice the split-K slabs for the consuming norm / attention),
     // so 128x128 stays there
     if (N <= 8192 && M > 128 && M <= 256) cfg = (M <= 192 && !(N <= 4096 && K <= 4096)) ? 0 : 1;
+    // round 4 (profiles/r4/gemm_wide_r4.md): the 128x256 tile (cfg 5: twice the weight bytes in flight per CU)
+    // for the weight-heavy 129-256-row shapes: gate_up 68.1 vs 73.9 us (256 rows) / 64.4 vs 66.2 (192), down
+    // (K 14336) 42.9 vs 50.5 / 41.0 vs 42.0
+    if (M > 128 && M <= 256 && (N > 8192 || K > 8192)) cfg = 5;
     // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: per shape from the
     // tools/bench_gemm_tiled.py sweep over every config (profiles/r3/prefill_chunk_gemm.md): 257-512 rows down
     // (K 14336) on the phased 256x256 tile split 8 ways (69 vs 92 us), qkv / o on 256x128 (46 / 33 vs 49 / 35
@@ -243,8 +247,8 @@ TCfg pick_tiled(int M, int N, int K) {
   }
   constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
   // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
-  static constexpr int kBM[5] = {256, 128, 256, 256, 256};
-  static constexpr int kBN[5] = {128, 128, 64, 256, 256};
+  static constexpr int kBM[6] = {256, 128, 256, 256, 256, 128};
+  static constexpr int kBN[6] = {128, 128, 64, 256, 256, 256};
   const int BM = kBM[cfg], BN = kBN[cfg];
   c.cfg = cfg;
   c.S = 1;
@@ -899,7 +903,7 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
               const c10::optional<Tensor>& v_cache, const c10::optional<Tensor>& block_tables,
               const c10::optional<Tensor>& q_len, const c10::optional<Tensor>& ctx_len,
               const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
-              const c10::optional<Tensor>& rope) {
+              const c10::optional<Tensor>& rope, const c10::optional<Tensor>& stamps, int64_t pf_steps) {
   for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
                           (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
                           (const Tensor*)&err})
@@ -985,12 +989,19 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
     p.rope_len = (int)rope->size(0);
     p.scale_log2 = 1.4426950408889634f / std::sqrt(128.f);
   }
+  if (stamps.has_value() && stamps->defined()) {
+    check_gpu(*stamps, "stamps");
+    check_dtype(*stamps, at::kLong, "stamps");
+    TORCH_CHECK(stamps->numel() >= 256 * 16, "mega_mlp: stamps hold 256 x 16 int64");
+    p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
+  p.pf_steps = pf_steps < 0 ? 4 : (int)std::min<int64_t>(pf_steps, 4);  // seam prefetch steps (decode_mega.hip kPF)
   p.M = M;
   p.eps = (float)eps;
   DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 12; }
+int64_t kernels_abi_version() { return 13; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -1061,7 +1072,8 @@ TORCH_LIBRARY(dsse, m) {
         "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps, "
         "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None, Tensor? qkv_in=None, int qkv_in_S=0, "
         "Tensor(i!)? k_cache=None, Tensor(j!)? v_cache=None, Tensor? block_tables=None, Tensor? q_len=None, "
-        "Tensor? ctx_len=None, Tensor? positions=None, Tensor? slots=None, Tensor? rope=None) -> ()");
+        "Tensor? ctx_len=None, Tensor? positions=None, Tensor? slots=None, Tensor? rope=None, "
+        "Tensor(k!)? stamps=None, int pf_steps=-1) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);

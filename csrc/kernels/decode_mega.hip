@@ -38,7 +38,9 @@
 // Hand-offs (cdna_hip_programming.md Guideline 16, the "sc1 payload + agent atomic" row of MI355X_MICROARCH.md's
 // valid forms): every handed-off byte (slabs, h, xm, resid, x) is stored write-through (sc1) by buffer stores; each
 // storing wave drains its stores (counted vmcnt, below), the workgroup meets at an s_barrier, and ONE lane adds 1 to
-// the item's counter (agent scope, relaxed; O / D counters sharded by XCD label b & 7 on their own 128-B lines).
+// the item's counter (agent scope, relaxed; the O / D / attention counters sharded by XCD label b & 7 and the norm
+// counters by row & 7, each shard on its own 128-B line: 64 arrivals on one word took 3.4-4.8 us to become visible to
+// the pollers, profiles/r4/mega_r4.md).
 // Consumers poll relaxed (one lane per shard, s_sleep, bounded) and then either load with sc1 buffer loads to
 // registers (norm rows: acquire-free) or, for the X ring's LDS-DMA, take ONE agent acquire first.
 // Counters are monotonic (never zeroed): a workgroup reads every counter it will poll at its start, before it has
@@ -72,8 +74,15 @@ constexpr int kLdsW = kD * kXSlot;           // weight rings after the X ring
 constexpr int kLdsCtl = kLdsW + kCW * kD * kWSlot;
 // control area: norm partial sums [8] at +0, attention merge statistics [2][4][16] x (m, l) at +64 (1 KiB)
 constexpr int kLdsFq = kLdsCtl + 2048;           // attention phase: per wave 6 x 128 bf16 (4 q heads, k, v)
-constexpr int kLds = kLdsFq + kCW * 6 * 256;     // 161,792 B
+constexpr int kLdsTrash = kLdsFq + kCW * 6 * 256;  // 1 KiB sink of the seam prefetch DMAs (contents never read)
+constexpr int kLds = kLdsTrash + 1024;               // 162,816 B
 static_assert(kLds <= 160 * 1024, "LDS budget");
+// Seam prefetch: at the start of an item with a dependency, each compute wave issues kPF more steps of its weight
+// stream (steps 2 .. 2 + kPF - 1 of the item; 0 and 1 are already in its ring) as default-policy loads whose data
+// lands in the trash slot: they run while the workgroup waits at the seam and leave the lines in L2 / MALL, so the
+// ring's own (nt) loads of those steps hit there.  p.pf_steps (<= kPF) of them are real, the rest dummies (0-byte
+// descriptor: the vmcnt accounting is the same either way).
+constexpr int kPF = 4;
 static_assert(2 * 3 * 32 * 64 * 4 <= kD * kXSlot, "attention merge area fits the X ring");
 // GEMM steps of one workgroup: O [0, 4), gate_up [4, 36), down [36, 50), next layer's QKV [50, 58)
 constexpr int kOSteps = 4, kGUSteps = kKCH, kDSteps = kKCF / 8;
@@ -175,6 +184,17 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
           16, 1024 * s + lane * 16, 0, 0, kAuxNT);
   };
 
+  auto issue_pf = [&](int gs, bool real) {
+    uint32_t bytes;
+    const bf16* src = w_src(gs, bytes);
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src, real ? bytes : 0u);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(smem + kLdsTrash)),
+          16, 1024 * s + lane * 16, 0, 0, 0);
+  };
+
   // ---- loader: X(gs) = 64 rows x 128 columns of the step's activation into X slot gs % 3 ----
   auto issue_x = [&](int gs) {
     const bf16* X;
@@ -197,21 +217,34 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
     auto rd = [&](int k, int s) { return __hip_atomic_load(p.sync + sync_word(k, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     unsigned vo = lane < 8 ? rd(kCntO, lane) : 0u, vd = lane < 8 ? rd(kCntD, lane) : 0u;
     unsigned va = lane < 8 ? rd(kCntA, lane) : 0u;
+    unsigned vn1 = lane < 8 ? rd(kCntN1, lane) : 0u, vn2 = lane < 8 ? rd(kCntN2, lane) : 0u;
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) { vo += __shfl_xor(vo, o); vd += __shfl_xor(vd, o); va += __shfl_xor(va, o); }
+    for (int o = 1; o < 8; o <<= 1) {
+      vo += __shfl_xor(vo, o);
+      vd += __shfl_xor(vd, o);
+      va += __shfl_xor(va, o);
+      vn1 += __shfl_xor(vn1, o);
+      vn2 += __shfl_xor(vn2, o);
+    }
     vo = __builtin_amdgcn_readfirstlane(vo);
     vd = __builtin_amdgcn_readfirstlane(vd);
     va = __builtin_amdgcn_readfirstlane(va);
+    vn1 = __builtin_amdgcn_readfirstlane(vn1);
+    vn2 = __builtin_amdgcn_readfirstlane(vn2);
     base_a = va - va % 256u;
-    const unsigned vn1 = __builtin_amdgcn_readfirstlane(rd(kCntN1, 0));
     const unsigned vgu = __builtin_amdgcn_readfirstlane(rd(kCntGU + ks, 0));
-    const unsigned vn2 = __builtin_amdgcn_readfirstlane(rd(kCntN2, 0));
     base_n2 = vn2 - vn2 % 64u;
     base_o = vo - vo % 256u;
     base_d = vd - vd % 256u;
     base_n1 = vn1 - vn1 % 64u;
     base_gu = vgu - vgu % 32u;
   }
+
+  // optional phase stamps (bench_mega.py --stamps): the loader wave's lane 0, 100 MHz wall clock, slot i of 16
+  auto stamp = [&](int i) {
+    if (p.stamps != nullptr && loader && lane == 0) p.stamps[b * 16 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   f32x4 acc[4];
 #pragma unroll
@@ -225,11 +258,13 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   // kind 0 = O / D (fp32 slab ks), 1 = gate_up (SiLU·mul -> h), 2 = next layer's QKV (fp32 slab b & 3 of
   // qkv_slabs).  dep: counter polled before the first X load; sig_k < 0: no completion counter.
   auto gemm_item = [&](int gs0, int nc, int kind, int active, int dep_k, int dep_shards, unsigned dep_base,
-                       unsigned dep_exp, int sig_k, int sig_shard) {
+                       unsigned dep_exp, int sig_k, int sig_shard, int st) {
     if (loader) {
       if (dep_k >= 0) {
         wait_counter(p.sync, p.err, dep_k, dep_shards, dep_base, dep_exp, lane);
+        if (st == 6) stamp(15);  // gate_up: dependency seen, before the acquire
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // X arrives by LDS-DMA: drop this CU's stale lines
+        stamp(st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       int issued = gs0;
@@ -242,12 +277,21 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
         if (issued < gs0 + nc) issue_x(issued++);
       }
       __builtin_amdgcn_s_barrier();  // end of item
+      stamp(st + 1);
       return;
     }
     const bool on = w < active;
+    const bool pf = dep_k >= 0;  // seam prefetch (kPF steps, see kPF)
+    if (pf) {
+#pragma unroll
+      for (int i = 0; i < kPF; ++i) issue_pf(gs0 + 2 + i, i < p.pf_steps && 2 + i < nc);
+    }
     for (int c = 0; c < nc; ++c) {
       const int gs = gs0 + c;
-      vm_barrier<4>();  // own W(gs) landed; X(gs) published by the loader
+      // own W(gs) landed; X(gs) published by the loader.  In the first two steps after a prefetch the kPF
+      // prefetch steps (and W(gs + 1)) are younger than W(gs) and may stay in flight.
+      if (pf && c < 2) vm_barrier<4 + 4 * kPF>();
+      else vm_barrier<4>();
       if (on) {
         const char* xb = smem + (gs % kD) * kXSlot;
         const char* wb = smem + kLdsW + (w * kD + gs % kD) * kWSlot + lane * 16;
@@ -313,12 +357,15 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
   };
 
   // ---- one norm row: resid[m] += sum of the 8 slabs; y[m] = rmsnorm(resid[m]) * wn (sc1 loads / stores) ----
-  auto norm_item = [&](int m, const bf16* wn, bf16* y, int dep_k, int dep_shards, unsigned dep_base, int sig_k) {
+  auto norm_item = [&](int m, const bf16* wn, bf16* y, int dep_k, int dep_shards, unsigned dep_base, int sig_k,
+                       int st) {
     if (loader) {
       wait_counter(p.sync, p.err, dep_k, dep_shards, dep_base, 256u, lane);
+      stamp(st);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_s_barrier();
+      stamp(st + 1);
       return;
     }
     __builtin_amdgcn_s_barrier();  // the loader's poll matched: the slabs are complete (sc1 loads below)
@@ -374,7 +421,7 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
                                                    __float_as_uint(v[7])}, rr, c0 * 4 + 16, 0, kAuxSc1);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (sig_k >= 0 && w == 0 && lane == 0) signal_counter(p.sync, sig_k, 0);
+    if (sig_k >= 0 && w == 0 && lane == 0) signal_counter(p.sync, sig_k, m & 7);  // 64 arrivals over 8 shards
   };
 
   // ---- attention phase (optional): units (sequence, kv head) = (u >> 3, u & 7), u = 2b + (w >> 2), four key-split
@@ -572,15 +619,19 @@ __global__ void __launch_bounds__(mega::kThreads) mega_mlp_kernel(MegaMlpParams 
 
   // ---- this workgroup's schedule ----
   const bool fused_attn = p.qkv_in != nullptr;
+  // stamp slots: 0 start, 1 attention done, 2/3 O dependency met / done, 4/5 N1, 6/7 gate_up, 8/9 down, 10/11 N2,
+  // 12/13 next QKV, 14 end, 15 gate_up dependency seen before its acquire fence
   if (fused_attn) attn_item();
-  gemm_item(0, kOSteps, 0, 8, fused_attn ? kCntA : -1, 8, base_a, 256u, kCntO, ks);
-  if (b < kRows) norm_item(b, p.w_ffn, p.xm, kCntO, 8, base_o, kCntN1);
-  gemm_item(kGU0, kGUSteps, 1, 7, kCntN1, 1, base_n1, 64u, kCntGU + (b >> 5), 0);
-  gemm_item(kD0, kDSteps, 0, 8, kCntGU + ks, 1, base_gu, 32u, kCntD, ks);
-  if (b >= kRows && b < 2 * kRows) norm_item(b - kRows, p.w_next, p.x, kCntD, 8, base_d, kCntN2);
-  if (p.wqkv != nullptr) gemm_item(kQ0, kQSteps, 2, kQTiles, kCntN2, 1, base_n2, 64u, -1, 0);
+  stamp(1);
+  gemm_item(0, kOSteps, 0, 8, fused_attn ? kCntA : -1, 8, base_a, 256u, kCntO, ks, 2);
+  if (b < kRows) norm_item(b, p.w_ffn, p.xm, kCntO, 8, base_o, kCntN1, 4);
+  gemm_item(kGU0, kGUSteps, 1, 7, kCntN1, 8, base_n1, 64u, kCntGU + (b >> 5), 0, 6);
+  gemm_item(kD0, kDSteps, 0, 8, kCntGU + ks, 1, base_gu, 32u, kCntD, ks, 8);
+  if (b >= kRows && b < 2 * kRows) norm_item(b - kRows, p.w_next, p.x, kCntD, 8, base_d, kCntN2, 10);
+  if (p.wqkv != nullptr) gemm_item(kQ0, kQSteps, 2, kQTiles, kCntN2, 8, base_n2, 64u, -1, 0, 12);
   // the look-ahead weight loads past the last step are range-failed dummies, but they still write the LDS: drain
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(14);
 }
 
 }  // namespace dsse

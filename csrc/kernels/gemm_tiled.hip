@@ -399,6 +399,7 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
     case 2: return launch_t<4, 1, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 waves
     case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
     case 4: return launch_phased<MODE>(X, ldx, M, W, K, N, S, ep, part, st);              // 256 x 256, phased
+    case 5: return launch_t<2, 4, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 256, 8 waves
   }
   return hipErrorInvalidValue;
 }
@@ -406,7 +407,9 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
 }  // namespace dsse
 
 // cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves),
-// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel).
+// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel),
+// 5 = 128 x 256 (8 waves, 3 stages of 16 KiB X + 32 KiB W: twice the weight bytes in flight per CU of cfg 0, for the
+// weight-streaming 129-256-row decode GEMMs; the two row blocks of a column block share an XCD and its L2).
 // (Round 3 also tried 4-stage rings and separate X / W loader rings for the 129-512-row decode buckets: all
 // slower in the 256-stream step, removed; profiles/r3/experiments_r3.md.)
 // Shape contract (checked by the caller): N % BN == 0, K % (64 S) == 0, the tiled weight layout (api.h).

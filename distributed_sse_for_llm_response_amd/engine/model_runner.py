@@ -62,9 +62,10 @@ def mega_reason(runner) -> str:
     It runs the O / gate_up / down projections and both norms of a layer in one launch of 256 workgroups that must all
     be resident at once (one per CU), so it needs the Mistral-7B MLP shapes at TP = 1, a 256-CU device, and a GPU this
     process does not share with other ranks (DSSE_GPU_SHARED=1, or more local ranks than devices, turns it off: two
-    processes' persistent grids on one device could each hold half the CUs).  DSSE_MEGA=0 turns it off."""
-    if os.environ.get("DSSE_MEGA", "1") == "0":
-        return "DSSE_MEGA=0"
+    processes' persistent grids on one device could each hold half the CUs).  Opt-in (DSSE_MEGA=1): it is correct on
+    MI355X (tests/test_mega_gpu.py) but measured slower than the launch-per-op path (profiles/r4/mega_r4.md)."""
+    if os.environ.get("DSSE_MEGA", "0") != "1":
+        return "DSSE_MEGA is not 1"
     if runner.device.type != "cuda":
         return "not on a GPU"
     if runner.comm.size > 1:

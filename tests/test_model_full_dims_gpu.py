@@ -43,6 +43,26 @@ def model():
     return std, r
 
 
+@pytest.fixture(scope="module")
+def model_mega(model):
+    """The same weights on a runner with the opt-in persistent decode layer kernel (DSSE_MEGA=1, decode_mega.hip:
+    folded attention + O / norm / gate_up / down / norm / next QKV in one launch per layer) for the 33-64 buckets."""
+    import os
+    from distributed_sse_for_llm_response_amd import ops
+
+    if not ops.mega_supported():
+        pytest.skip("persistent kernel needs a 256-CU gfx950")
+    std, base = model
+    os.environ["DSSE_MEGA"] = "1"
+    try:
+        r = ModelRunner(base.w, num_blocks=64 * PAGES_PER_SEQ + 8, max_batch=64, max_model_len=512, device=base.device)
+        assert r.mega, r.mega_reason
+        r.capture([48, 64])
+    finally:
+        del os.environ["DSSE_MEGA"]
+    return std, r
+
+
 def _compare(ref_row, got_row, what):
     ref_row, got_row = ref_row.float(), got_row.float()
     cos = torch.nn.functional.cosine_similarity(ref_row, got_row, dim=0).item()
@@ -53,7 +73,16 @@ def _compare(ref_row, got_row, what):
 
 @pytest.mark.parametrize("B", BUCKETS)
 def test_full_dims_decode_logits_match_reference(model, gpu, B):
-    std, r = model
+    _decode_logits_check(*model, gpu, B)
+
+
+@pytest.mark.parametrize("B", [40, 64])
+def test_full_dims_decode_logits_persistent_layer_kernel(model_mega, gpu, B):
+    """B = 40: an eager step of 40 rows (a partial 64-row tile in the persistent kernel); B = 64: the captured graph."""
+    _decode_logits_check(*model_mega, gpu, B)
+
+
+def _decode_logits_check(std, r, gpu, B):
     g = torch.Generator().manual_seed(B)
     prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
                for _ in range(B)]

@@ -5,7 +5,7 @@
 #   mega_test     tests/test_mega_gpu.py                 mega_bench    tools/bench_mega.py --M 64
 #   model_test    tests/test_model_full_dims_gpu.py      ar_test       tests/test_custom_ar_gpu.py
 #   gpu_tests     the whole GPU suite (pytest -m gpu)    smoke         __graft_entry__.smoke()
-#   bench64       bench.py (driver form, 64 streams)     bench64_off   the same with DSSE_MEGA=0
+#   bench64       bench.py (driver form, 64 streams)     bench64_mega  the same with DSSE_MEGA=1
 #   bench256      bench.py --streams 256                 prof64        rocprofv3 kernel trace of bench.py
 #   ttft8k        tools/bench_ttft.py --prompt-len 8192  c3stub        8 paced stub replicas x 256 streams (CPU only)
 #   attn_bench    tools/bench_prefill_attn.py (8k / 512 causal, + SDPA arm)
@@ -31,19 +31,22 @@ for s in "$@"; do
   case $s in
     mega_test) step mega_test 300 $PYT tests/test_mega_gpu.py ;;
     mega_bench) step mega_bench 300 python -u tools/bench_mega.py --M 64 ;;
+    mega_stamps) step mega_stamps 300 python -u tools/bench_mega.py --M 64 --qkv --stamps --pf 0,2,4 ;;
     model_test) step model_test 600 $PYT tests/test_model_full_dims_gpu.py ;;
     ar_test) step ar_test 900 $PYT tests/test_custom_ar_gpu.py ;;
     gpu_tests) step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench64) step bench64 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    bench64_off) DSSE_MEGA=0 step bench64_off 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench64_mega) DSSE_MEGA=1 step bench64_mega 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
+    prof64_mega) DSSE_MEGA=1 step prof64_mega 600 rocprofv3 --kernel-trace --stats -d "$out/prof64_mega" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     c3stub) HIP_VISIBLE_DEVICES= DSSE_DIST_BACKEND=gloo step c3stub 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 8 --streams 256 --steps 64 --warmup 8 --stub-step-ms 9.7 ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill" ;;
     attn_bench) step attn_bench 300 python -u tools/bench_prefill_attn.py --T 8192,2048,512 --sdpa ;;
     gemm_bench) step gemm_bench 300 python -u tools/bench_gemm_tiled.py --M 8192,256 --cfg auto ;;
+    gemm_wide) step gemm_wide 300 python -u tools/bench_gemm_tiled.py --M 256,192 --cfg auto,0,1,5 --no-library ;;
     pmc_attn)
       step pmc_attn_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_attn_a" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
       step pmc_attn_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_attn_b" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
