@@ -57,7 +57,7 @@ def model_mega(model):
     try:
         r = ModelRunner(base.w, num_blocks=64 * PAGES_PER_SEQ + 8, max_batch=64, max_model_len=512, device=base.device)
         assert r.mega, r.mega_reason
-        r.capture([48, 64])
+        r.capture([64])
     finally:
         del os.environ["DSSE_MEGA"]
     return std, r
@@ -78,11 +78,12 @@ def test_full_dims_decode_logits_match_reference(model, gpu, B):
 
 @pytest.mark.parametrize("B", [40, 64])
 def test_full_dims_decode_logits_persistent_layer_kernel(model_mega, gpu, B):
-    """B = 40: an eager step of 40 rows (a partial 64-row tile in the persistent kernel); B = 64: the captured graph."""
-    _decode_logits_check(*model_mega, gpu, B)
+    """The 64-row bucket's captured graph on the persistent kernel, full (B = 64) and with 24 inactive rows."""
+    _decode_logits_check(*model_mega, gpu, B, bucket=64)
 
 
-def _decode_logits_check(std, r, gpu, B):
+def _decode_logits_check(std, r, gpu, B, bucket=None):
+    bucket = bucket or B
     g = torch.Generator().manual_seed(B)
     prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
                for _ in range(B)]
@@ -107,7 +108,7 @@ def _decode_logits_check(std, r, gpu, B):
     gen = [[int(t)] for t in r.ids[:B].cpu()]
     logits = []
     for _ in range(2):
-        r.decode(B)
+        r.decode(bucket)
         torch.cuda.synchronize()
         logits.append(r.logits[:B].clone())
         for i, t in enumerate(r.ids[:B].cpu()):

@@ -31,7 +31,7 @@ for s in "$@"; do
   case $s in
     mega_test) step mega_test 300 $PYT tests/test_mega_gpu.py ;;
     mega_bench) step mega_bench 300 python -u tools/bench_mega.py --M 64 ;;
-    mega_stamps) step mega_stamps 300 python -u tools/bench_mega.py --M 64 --qkv --stamps --pf 0,2,4 ;;
+    mega_stamps) step mega_stamps 300 python -u tools/bench_mega.py --M 64 --qkv --stamps ;;
     model_test) step model_test 600 $PYT tests/test_model_full_dims_gpu.py ;;
     ar_test) step ar_test 900 $PYT tests/test_custom_ar_gpu.py ;;
     gpu_tests) step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -39,6 +39,7 @@ for s in "$@"; do
     bench64) step bench64 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench64_mega) DSSE_MEGA=1 step bench64_mega 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
+    bench256b) step bench256b 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     prof64_mega) DSSE_MEGA=1 step prof64_mega 600 rocprofv3 --kernel-trace --stats -d "$out/prof64_mega" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
