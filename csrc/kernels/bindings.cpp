@@ -899,7 +899,11 @@ int64_t mega_sync_words() { return (int64_t)dsse_mega_sync_words(); }
 void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Tensor& wd, Tensor& resid,
               const Tensor& w_ffn, const Tensor& w_next, Tensor& xm, Tensor& h, Tensor& x, Tensor& slabs, Tensor& sync,
               Tensor& err, double eps, const c10::optional<Tensor>& wqkv, const c10::optional<Tensor>& qkv_slabs,
-              const c10::optional<Tensor>& stamps) {
+              const c10::optional<Tensor>& qkv_in, int64_t qkv_in_S, const c10::optional<Tensor>& k_cache,
+              const c10::optional<Tensor>& v_cache, const c10::optional<Tensor>& block_tables,
+              const c10::optional<Tensor>& q_len, const c10::optional<Tensor>& ctx_len,
+              const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
+              const c10::optional<Tensor>& rope, const c10::optional<Tensor>& stamps, int64_t pf_steps) {
   for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
                           (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
                           (const Tensor*)&err})
@@ -916,8 +920,6 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
   TORCH_CHECK(attn.dim() == 2 && attn.size(1) == H && M >= 1 && M <= 64, "mega_mlp: attn must be [M <= 64, 4096]");
   TORCH_CHECK(wo.size(0) == H && wo.size(1) == H && wgu.size(0) == 2 * F && wgu.size(1) == H && wd.size(0) == H &&
                   wd.size(1) == F, "mega_mlp: weights must be Mistral-7B shaped (tiled layout)");
-  for (const Tensor* t : {&attn, (const Tensor*)&resid, (const Tensor*)&xm, (const Tensor*)&h, (const Tensor*)&x})
-    TORCH_CHECK(t->is_contiguous(), "mega_mlp: activations must be contiguous");
   TORCH_CHECK(resid.dim() == 2 && resid.size(0) >= M && resid.size(1) == H, "mega_mlp: resid [>= M, 4096]");
   TORCH_CHECK(xm.size(0) >= M && xm.size(1) == H && x.size(0) >= M && x.size(1) == H, "mega_mlp: xm / x [>= M, 4096]");
   TORCH_CHECK(h.size(0) >= M && h.size(1) == F, "mega_mlp: h [>= M, 14336]");
@@ -936,7 +938,7 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
     TORCH_CHECK(qkv_slabs->numel() >= (int64_t)4 * M * 6144, "mega_mlp: qkv_slabs hold 4 x M x 6144 floats");
   }
   dsse::MegaMlpParams p{};
-  p.attn = reinterpret_cast<const bf16*>(attn.data_ptr());
+  p.attn = reinterpret_cast<bf16*>(attn.data_ptr());
   p.wo = reinterpret_cast<const bf16*>(wo.data_ptr());
   p.wgu = reinterpret_cast<const bf16*>(wgu.data_ptr());
   p.wd = reinterpret_cast<const bf16*>(wd.data_ptr());
@@ -951,18 +953,55 @@ void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Ten
   p.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
   p.wqkv = q ? reinterpret_cast<const bf16*>(wqkv->data_ptr()) : nullptr;
   p.qkv_slabs = q ? qkv_slabs->data_ptr<float>() : nullptr;
+  if (qkv_in.has_value() && qkv_in->defined()) {
+    // the layer's decode attention as the first phase (GQA 32 / 8 heads, page 32, one query per sequence)
+    for (const c10::optional<Tensor>* t : {&k_cache, &v_cache, &block_tables, &q_len, &ctx_len, &positions, &slots, &rope})
+      TORCH_CHECK(t->has_value() && (*t)->defined(), "mega_mlp: the attention phase needs every attention tensor");
+    for (const Tensor* t : {&*qkv_in, &*k_cache, &*v_cache, &*block_tables, &*q_len, &*ctx_len, &*positions, &*slots,
+                            &*rope})
+      check_gpu(*t, "mega_mlp attention tensor");
+    check_dtype(*qkv_in, at::kFloat, "qkv_in");
+    check_dtype(*rope, at::kFloat, "rope");
+    for (const Tensor* t : {&*block_tables, &*q_len, &*ctx_len, &*positions, &*slots}) check_dtype(*t, at::kInt, "metadata");
+    check_dtype(*k_cache, at::kBFloat16, "k_cache");
+    check_dtype(*v_cache, at::kBFloat16, "v_cache");
+    TORCH_CHECK(qkv_in_S >= 1 && qkv_in->numel() >= qkv_in_S * M * 6144, "mega_mlp: qkv_in holds S x M x 6144 floats");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == 8 && k_cache->size(2) == dsse::kBS && k_cache->size(3) == 128,
+                "mega_mlp: k_cache [blocks, 8, 32, 128]");
+    TORCH_CHECK(v_cache->sizes() == at::IntArrayRef({k_cache->size(0), 8, 128, dsse::kBS}), "mega_mlp: v_cache [blocks, 8, 128, 32]");
+    TORCH_CHECK(block_tables->dim() == 2 && block_tables->size(0) >= M, "mega_mlp: block_tables [>= M, max_blocks]");
+    TORCH_CHECK(q_len->numel() >= M && ctx_len->numel() >= M && positions->numel() >= M && slots->numel() >= M,
+                "mega_mlp: per-row metadata too short");
+    TORCH_CHECK(rope->dim() == 3 && rope->size(1) == 64 && rope->size(2) == 2, "mega_mlp: rope [P, 64, 2]");
+    p.qkv_in = qkv_in->data_ptr<float>();
+    p.qkv_in_S = (int)qkv_in_S;
+    p.k_cache = reinterpret_cast<bf16*>(k_cache->data_ptr());
+    p.v_cache = reinterpret_cast<bf16*>(v_cache->data_ptr());
+    p.block_tables = block_tables->data_ptr<int>();
+    p.max_blocks = (int)block_tables->size(1);
+    p.num_blocks = (int)k_cache->size(0);
+    p.num_slots = (int)(k_cache->size(0) * dsse::kBS);
+    p.q_len = q_len->data_ptr<int>();
+    p.ctx_len = ctx_len->data_ptr<int>();
+    p.positions = positions->data_ptr<int>();
+    p.slots = slots->data_ptr<int>();
+    p.rope = reinterpret_cast<const float2*>(rope->data_ptr<float>());
+    p.rope_len = (int)rope->size(0);
+    p.scale_log2 = 1.4426950408889634f / std::sqrt(128.f);
+  }
   if (stamps.has_value() && stamps->defined()) {
     check_gpu(*stamps, "stamps");
     check_dtype(*stamps, at::kLong, "stamps");
     TORCH_CHECK(stamps->numel() >= 256 * 16, "mega_mlp: stamps hold 256 x 16 int64");
     p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
   }
+  p.pf_steps = pf_steps < 0 ? 4 : (int)std::min<int64_t>(pf_steps, 4);  // seam prefetch steps (decode_mega.hip kPF)
   p.M = M;
   p.eps = (float)eps;
   DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 14; }
+int64_t kernels_abi_version() { return 13; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -1031,7 +1070,10 @@ TORCH_LIBRARY(dsse, m) {
   m.def("mega_sync_words() -> int", &mega_sync_words);
   m.def("mega_mlp(Tensor attn, Tensor wo, Tensor wgu, Tensor wd, Tensor(a!) resid, Tensor w_ffn, Tensor w_next, "
         "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps, "
-        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None, Tensor(i!)? stamps=None) -> ()");
+        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None, Tensor? qkv_in=None, int qkv_in_S=0, "
+        "Tensor(i!)? k_cache=None, Tensor(j!)? v_cache=None, Tensor? block_tables=None, Tensor? q_len=None, "
+        "Tensor? ctx_len=None, Tensor? positions=None, Tensor? slots=None, Tensor? rope=None, "
+        "Tensor(k!)? stamps=None, int pf_steps=-1) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);

@@ -238,15 +238,20 @@ class ModelRunner:
         if self.mega and MEGA_MIN_B <= B <= MEGA_MAX_B:
             # two launches per layer: the folded decode attention (QKV slab sum + RoPE + K/V write + attention), then
             # the persistent block (decode_mega.hip): O -> norm -> gate_up -> down -> norm -> the NEXT layer's QKV
-            # projection as split-K slabs, one launch whose register weight ring streams across the seams.  Layer 0's
-            # QKV is the attention launch's own projection.
+            # projection, one launch whose weight stream runs across every seam.  Layer 0's QKV is its own launch.
+            fused_qkv = os.environ.get("DSSE_MEGA_QKV", "1") != "0"
+            # attention inside the persistent launch measured slower than its own launch (profiles/r4/mega_r4.md)
+            if fused_qkv and os.environ.get("DSSE_MEGA_ATTN", "0") == "1":
+                self._decode_layers_mega(B, resid, x)
+                return
             for li, L in enumerate(w.layers):
-                self._qkv_attention(li, L, B, x, part, nparts, slabs_ready=4 if li > 0 else 0)
+                self._qkv_attention(li, L, B, x, part, nparts, slabs_ready=4 if (fused_qkv and li > 0) else 0)
                 nxt = w.layers[li + 1] if li + 1 < nl else None
                 ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm,
                              nxt.attn_norm if nxt is not None else w.final_norm, self.xm[r], self.h[r], x,
                              self.split_part, self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps,
-                             wqkv=nxt.wqkv_t if nxt is not None else None, qkv_slabs=self.split_part)
+                             wqkv=nxt.wqkv_t if (fused_qkv and nxt is not None) else None,
+                             qkv_slabs=self.split_part)
             ops.gemm_out(x, w.lm_head_t, self.logits[r])
             self._sample_commit(B)
             ops.ring_advance(self.ring_counter)
@@ -267,6 +272,28 @@ class ModelRunner:
             else:
                 ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
                 comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps)
+        ops.gemm_out(x, w.lm_head_t, self.logits[r])
+        self._sample_commit(B)
+        ops.ring_advance(self.ring_counter)
+
+    def _decode_layers_mega(self, B: int, resid, x) -> None:
+        """ONE launch per layer (decode_mega.hip with its attention phase): the layer's decode attention on the QKV slabs
+        the previous launch left (slab sum + RoPE + the step's K / V + paged attention), O -> norm -> gate_up -> down ->
+        norm, and the next layer's QKV projection; layer 0's QKV slabs come from one GEMM launch before the loop."""
+        w, eps = self.w, self.cfg.rms_eps
+        r = slice(0, B)
+        nl = len(w.layers)
+        S = ops.gemm_qkv_slabs(x, w.layers[0].wqkv_t, self.split_part)
+        for li, L in enumerate(w.layers):
+            nxt = w.layers[li + 1] if li + 1 < nl else None
+            att = dict(qkv_in=self.split_part, qkv_in_S=S, k_cache=self.kv.k[li], v_cache=self.kv.v[li],
+                       block_tables=self.block_tables[r], q_len=self.q_len[r], ctx_len=self.ctx_len[r],
+                       positions=self.positions[r], slots=self.slots[r], rope=self.rope)
+            ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm,
+                         nxt.attn_norm if nxt is not None else w.final_norm, self.xm[r], self.h[r], x, self.split_part,
+                         self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps,
+                         wqkv=nxt.wqkv_t if nxt is not None else None, qkv_slabs=self.split_part, attention=att)
+            S = 4
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)

@@ -202,17 +202,21 @@ def gemm_qkv_slabs(x, w, slabs) -> int:
 
 
 def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv=None, qkv_slabs=None,
-             stamps=None):
-    """Decode MLP block in one launch (HIP, <= 64 rows, Mistral-7B shapes): resid += attn·woᵀ; r1 = resid;
-    xm = bf16(r1·w_ffn) (unnormalised); h = silu(inv1·xm·w_gᵀ)·(inv1·xm·w_uᵀ) with inv1 = 1 / rms(r1) per row;
-    resid += h·w_dᵀ; r2 = resid.  With `wqkv` (the next layer's QKV weight): x = bf16(r2·w_next) (unnormalised) and
-    `qkv_slabs` = 4 fp32 split-K slabs whose sum is inv2·x·Wqkvᵀ (= norm(r2)·Wqkvᵀ, for
-    qkv_attention_decode(..., slabs_ready=4)); without: x = norm(r2)·w_next.  `err` [1] int32 is set when a bounded
-    in-kernel wait timed out (the engine's health word).  `stamps` (int64 [256, 16], HIP only) receives
-    per-workgroup phase timestamps (100 MHz) for tools/bench_mega.py --stamps."""
+             attention=None, stamps=None, pf_steps: int = -1):
+    """Decode MLP block in one launch (HIP, <= 64 rows, Mistral-7B shapes): resid += attn·woᵀ; xm = norm(resid)·w_ffn;
+    h = silu(xm·w_gᵀ)·(xm·w_uᵀ); resid += h·w_dᵀ; x = norm(resid)·w_next; with `wqkv` also the next layer's QKV
+    projection of x as 4 fp32 split-K slabs in `qkv_slabs` (for qkv_attention_decode(..., slabs_ready=4)).  With
+    `attention` = dict(qkv_in, qkv_in_S, k_cache, v_cache, block_tables, q_len, ctx_len, positions, slots, rope) the
+    layer's decode attention runs first in the same launch (folded QKV epilogue, writes `attn` and the step's K / V).
+    `err` [1] int32 is set when a bounded in-kernel wait timed out (the engine's health word).  `stamps` (int64
+    [256, 16], HIP only) receives per-workgroup phase timestamps (100 MHz) for tools/bench_mega.py --stamps;
+    `pf_steps` (0-4, -1 = the default 4) weight steps each compute wave prefetches into L2 / MALL at a seam."""
     if _hip(attn):
+        a = attention or {}
         torch.ops.dsse.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv,
-                                qkv_slabs, stamps)
+                                qkv_slabs, a.get("qkv_in"), int(a.get("qkv_in_S", 0)), a.get("k_cache"),
+                                a.get("v_cache"), a.get("block_tables"), a.get("q_len"), a.get("ctx_len"),
+                                a.get("positions"), a.get("slots"), a.get("rope"), stamps, int(pf_steps))
     else:
         ref.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps, wqkv, qkv_slabs)
 

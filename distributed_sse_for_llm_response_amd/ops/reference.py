@@ -150,27 +150,20 @@ def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nspli
 
 
 def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps, wqkv=None, qkv_slabs=None):
-    """The persistent decode MLP block (csrc/kernels/decode_mega.hip): its norms are folded into the consumers, so
-    xm (and x when the next layer's QKV runs) hold bf16(resid · w) unnormalised and the consumers scale by the row's
-    1 / rms; the next layer's QKV projection lands in one fp32 slab followed by three zero slabs (the same sum)."""
+    """The persistent decode MLP block (csrc/kernels/decode_mega.hip) as its five unfused ops (+ the next layer's QKV
+    projection as one fp32 slab followed by three zero slabs: the same sum)."""
     M = attn.shape[0]
     r = resid[:M]
     gemm_resid(attn, wo, r)
-    inv1 = torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + eps)
-    xm[:M] = (r * w_ffn.float()).to(xm.dtype)
-    y = (xm[:M].float() @ untile_weight(wgu).float().t()) * inv1
-    y = y.view(M, -1, 2, 8)
-    h[:M] = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, -1).to(h.dtype)
+    rmsnorm(r, w_ffn, xm[:M], eps)
+    gemm_silu(xm[:M], wgu, h[:M])
     gemm_resid(h[:M], wd, r)
-    inv2 = torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + eps)
-    if wqkv is None:
-        x[:M] = (r * inv2 * w_next.float()).to(x.dtype)
-        return
-    x[:M] = (r * w_next.float()).to(x.dtype)
-    N = wqkv.shape[0]
-    sl = qkv_slabs.view(-1)[: 4 * M * N].view(4, M, N)
-    sl.zero_()
-    sl[0] = (x[:M].float() @ untile_weight(wqkv).float().t()) * inv2
+    rmsnorm(r, w_next, x[:M], eps)
+    if wqkv is not None:
+        N = wqkv.shape[0]
+        sl = qkv_slabs.view(-1)[: 4 * M * N].view(4, M, N)
+        sl.zero_()
+        sl[0] = x[:M].float() @ untile_weight(wqkv).float().t()
 
 
 # ---------------------------------------------------------------- decode metadata

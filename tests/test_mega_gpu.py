@@ -71,15 +71,14 @@ def test_mega_mlp_stages(gpu, block, M):
     _run(d, b)
     torch.cuda.synchronize()
     assert int(d["err"].item()) == 0, "a bounded wait timed out"
-    # stage 1 (O + the N1 strips): resid1 = r0 + attn Woᵀ, xm = bf16(resid1 · w_ffn) unnormalised
+    # stage 1: resid1 = r0 + attn Woᵀ, xm = norm(resid1) w_ffn
     r1 = r0 + b["attn"].float() @ d["Wo"].t()
-    _close(b["xm"], (r1 * d["w_ffn"].float()).bfloat16(), 2e-2, 2e-2, "xm")
-    # stage 2: h = silu(inv1 · gate) (inv1 · up) from the kernel's own xm, inv1 = 1 / rms(resid1)
-    inv1 = torch.rsqrt(r1.pow(2).mean(-1, keepdim=True) + 1e-5)
-    y = ((b["xm"].float() @ d["Wgu"].t()) * inv1).view(M, -1, 2, 8)
+    _close(b["xm"], _norm(r1, d["w_ffn"]), 2e-2, 2e-2, "xm")
+    # stage 2: h = silu(gate) up from the kernel's own xm
+    y = (b["xm"].float() @ d["Wgu"].t()).view(M, -1, 2, 8)
     h_ref = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, F)
     _close(b["h"], h_ref, 2e-2, 2e-2, "h")
-    # stage 3: resid2 = resid1 + h Wdᵀ from the kernel's own h, x = norm(resid2) w_next (last layer: normalised)
+    # stage 3: resid2 = resid1 + h Wdᵀ from the kernel's own h, x = norm(resid2) w_next
     r2 = r1 + b["h"].float() @ d["Wd"].t()
     _close(b["resid"], r2, 2e-3, 2e-3, "resid")
     _close(b["x"], _norm(r2, d["w_next"]), 2e-2, 2e-2, "x")
@@ -134,8 +133,8 @@ def test_mega_mlp_repeated_launches_and_graph_replay(gpu, block):
 
 
 def test_mega_mlp_next_layer_qkv_slabs(gpu, block):
-    """The optional last phase: the next layer's QKV projection as 4 fp32 split-K slabs whose sum is
-    norm(resid2)·Wqkvᵀ (x then holds bf16(resid2 · w_next) unnormalised; the slabs carry the row's 1 / rms)."""
+    """The optional last phase: the next layer's QKV projection of x as 4 fp32 split-K slabs (their sum = x·Wqkvᵀ),
+    and qkv_attention_decode(slabs_ready=4) on them equals the unfused QKV + RoPE + attention."""
     d = block
     M = 64
     g = torch.Generator().manual_seed(21)
@@ -146,28 +145,6 @@ def test_mega_mlp_next_layer_qkv_slabs(gpu, block):
                  slabs, d["sync"], d["err"], 1e-5, wqkv=wq, qkv_slabs=slabs)
     torch.cuda.synchronize()
     assert int(d["err"].item()) == 0
-    r2 = b["resid"].float()
-    _close(b["x"], (r2 * d["w_next"].float()).bfloat16(), 2e-2, 2e-2, "x (unnormalised)")
-    inv2 = torch.rsqrt(r2.pow(2).mean(-1, keepdim=True) + 1e-5)
     got = slabs[: 4 * M * 6144].view(4, M, 6144).sum(0)
-    ref = (b["x"].float() @ R.untile_weight(wq).float().t()) * inv2
+    ref = b["x"].float() @ R.untile_weight(wq).float().t()
     _close(got, ref, 2e-3, 2e-3, "qkv slabs")
-    # the same slabs through the engine's reference semantics (one slab + zeros) give the same sum
-    cpu = {k: v.cpu().clone() for k, v in _bufs(M, gpu, 13).items()}
-    sl = torch.zeros(8 * M * H)
-    R.mega_mlp(cpu["attn"], d["wo"].cpu(), d["wgu"].cpu(), d["wd"].cpu(), cpu["resid"], d["w_ffn"].cpu(),
-               d["w_next"].cpu(), cpu["xm"], cpu["h"], cpu["x"], 1e-5, wq.cpu(), sl)
-    _close(got, sl[: 4 * M * 6144].view(4, M, 6144).sum(0), 5e-2, 4e-2, "qkv slabs vs reference block")
-
-
-def test_mega_mlp_phase_stamps(gpu, block):
-    """The optional per-workgroup phase stamps (tools/bench_mega.py --stamps) are monotonic per workgroup."""
-    d = block
-    b = _bufs(64, gpu, 3)
-    st = torch.zeros(256, 16, dtype=torch.int64, device=gpu)
-    ops.mega_mlp(b["attn"], d["wo"], d["wgu"], d["wd"], b["resid"], d["w_ffn"], d["w_next"], b["xm"], b["h"], b["x"],
-                 d["slabs"], d["sync"], d["err"], 1e-5, stamps=st)
-    torch.cuda.synchronize()
-    s = st.cpu()[:, :13]
-    assert bool((s > 0).all()), "every workgroup records slots 0-12"
-    assert bool((s[:, 1:] >= s[:, :-1]).all()), "stamps go forward"

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=32)
     ap.add_argument("--qkv", action="store_true")
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--pf", default="4", help="seam prefetch steps to A/B (comma list, each a persistent arm)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ops.load_library(required=True)
@@ -65,15 +66,17 @@ def main():
             if a.qkv:
                 ops.gemm_qkv_slabs(x, s["wqkv"], qkv_slabs)
 
-    def fused(stamps=None, i0=0, n=None):
+    pfs = [int(v) for v in a.pf.split(",")]
+
+    def fused(stamps=None, i0=0, n=None, pf=pfs[0]):
         for i in range(i0, i0 + (n or a.blocks)):
             s = sets[i % a.sets]
             ops.mega_mlp(attn, s["wo"], s["wgu"], s["wd"], resid, s["w_ffn"], s["w_next"], xm, h, x, part, sync, err,
                          1e-5, wqkv=s["wqkv"], qkv_slabs=qkv_slabs,
-                         stamps=None if stamps is None else stamps[i - i0])
+                         stamps=None if stamps is None else stamps[i - i0], pf_steps=pf)
 
     graphs = {}
-    arms = [("unfused", unfused), ("mega", fused)]
+    arms = [("unfused", unfused)] + [(f"mega_pf{v}", (lambda v=v: fused(pf=v))) for v in pfs]
     for name, fn in arms:
         st = torch.cuda.Stream()
         st.wait_stream(torch.cuda.current_stream())
@@ -104,11 +107,11 @@ def main():
     if a.stamps:
         n = 6
         st = torch.zeros(n, 256, 16, dtype=torch.int64, device=dev)
-        fused(st, 0, n)
+        fused(st, 0, n, pf=pfs[-1])
         torch.cuda.synchronize()
         assert int(err.item()) == 0, "mega kernel: a bounded wait timed out"
-        names = ["start", "O done", "N1 strip dep met", "N1 strip done", "gate_up dep met", "gate_up done",
-                 "h published", "down dep met", "down done", "N2 strip dep met", "N2 strip done", "N2 all met", "end"]
+        names = ["start", "attention done", "O dep met", "O done", "N1 dep met", "N1 done", "gate_up dep met",
+                 "gate_up done", "down dep met", "down done", "N2 dep met", "N2 done", "QKV dep met", "QKV done", "end", "gate_up pre-fence"]
         for k in (3, 4, 5):  # launches whose weight sets are cold (rotating 8 sets)
             s = st[k].cpu().double()
             t0 = s[:, 0].min()
