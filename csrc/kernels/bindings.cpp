@@ -219,7 +219,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 5) {
+  if (cfg < 0 || cfg > 7) {
     // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
     // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
     // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
@@ -247,8 +247,8 @@ TCfg pick_tiled(int M, int N, int K) {
   }
   constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
   // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
-  static constexpr int kBM[6] = {256, 128, 256, 256, 256, 128};
-  static constexpr int kBN[6] = {128, 128, 64, 256, 256, 256};
+  static constexpr int kBM[8] = {256, 128, 256, 256, 256, 128, 256, 256};
+  static constexpr int kBN[8] = {128, 128, 64, 256, 256, 256, 256, 256};
   const int BM = kBM[cfg], BN = kBN[cfg];
   c.cfg = cfg;
   c.S = 1;

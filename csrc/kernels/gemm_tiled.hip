@@ -400,6 +400,8 @@ static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf
     case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
     case 4: return launch_phased<MODE>(X, ldx, M, W, K, N, S, ep, part, st);              // 256 x 256, phased
     case 5: return launch_t<2, 4, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 256, 8 waves
+    case 6: return launch_t<2, 2, 8, 8, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 4 waves
+    case 7: return launch_t<2, 2, 8, 8, 2, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 4 waves, FB 2
   }
   return hipErrorInvalidValue;
 }

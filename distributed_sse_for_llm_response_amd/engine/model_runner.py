@@ -35,7 +35,7 @@ from .. import ops
 from ..ops.reference import rope_table
 from ..parallel.comm import TPComm
 from .kv_cache import PAGE, KVCache
-from .weights import EngineWeights
+from .weights import EngineWeights, attach_library
 
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
@@ -93,6 +93,18 @@ def prefill_row_chunks(T: int, tp: int) -> list:
     n = int(os.environ.get("DSSE_TP_PREFILL_CHUNKS", "4")) if tp > 1 and T >= lo else 1
     step = max(64, -(-T // max(1, n) // 64) * 64)
     return [(a, min(T, a + step)) for a in range(0, T, step)]
+
+
+# Rows from which a projection runs on the library GEMM (hipBLASLt through torch.matmul on the row-major weight copies,
+# weights.attach_library) instead of the tiled-layout kernels, per projection, from interleaved A/Bs on MI355X
+# (profiles/r4/prefill_lib_r4.md): 512 rows qkv 34 vs 46 us, o 27 vs 33, gate_up 89 (+ ~8 silu_mul) vs 114, down 87 vs
+# 73 (tiled wins); 1024 rows all four (down 118 vs 171); 256 rows only gate_up (57 vs 68-71).  8k TTFT 112.5 vs 121.9 ms.
+LIB_MIN_ROWS = {"qkv": 512, "o": 512, "gate_up": 256, "down": 1024}
+
+
+def prefill_lib_enabled(dev) -> bool:
+    """DSSE_PREFILL_LIB=0: every projection on the tiled kernels (and no 14.5 GB of row-major copies)."""
+    return torch.device(dev).type == "cuda" and os.environ.get("DSSE_PREFILL_LIB", "1") != "0"
 
 
 # decode buckets run on the persistent MLP kernel (rows <= 64; smaller buckets keep the launch-per-op path unless
@@ -213,6 +225,14 @@ class ModelRunner:
         if self.comm.size > 1 and self.comm.rank == 0:
             print(f"[engine] TP={self.comm.size} decode all-reduce: "
                   f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
+        # wide projections on the library GEMMs (row-major weight copies, weights.attach_library): LIB_MIN_ROWS
+        self.lib = prefill_lib_enabled(dev)
+        self._gu = None
+        if self.lib:
+            attach_library(w)
+            # [rows, 2F] gate / up product of the library path, allocated once (captured graphs hold its address):
+            # a pass with more rows than this runs gate_up on the tiled kernel instead
+            self._gu = torch.empty(max(max_prefill_tokens, Bm + 2048), 2 * F, **bf)
         self.graphs = {}
         self.graph_pool = None
         self.pf_graphs = {}   # row bucket -> captured prefill graph
@@ -315,7 +335,7 @@ class ModelRunner:
         for li, L in enumerate(w.layers):
             self._qkv_attention(li, L, B, x, part, nparts)
             self._resid_proj(self.attn[r], L.wo_t, resid, L.ffn_norm, x, self.tmp[r])
-            ops.gemm_silu(x, L.wgu_t, self.h[r])
+            self._gate_up(x, L, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             self._resid_proj(self.h[r], L.wd_t, resid, w_next, x, self.tmp[r])
         step = 256 if DECODE_GEMM_MAX_M > 2 else DECODE_GEMM_MAX_M  # one 256-row call streams the head once
@@ -551,6 +571,25 @@ class ModelRunner:
         done.record(self._side)
         return done
 
+    def _proj(self, a, wt, ws, out, kind: str) -> None:
+        """out = a·wᵀ in bf16: the library GEMM on the row-major copy from LIB_MIN_ROWS[kind] rows, else the tiled
+        kernels."""
+        if self.lib and ws is not None and a.shape[0] >= LIB_MIN_ROWS[kind]:
+            torch.matmul(a, ws.t(), out=out)
+        else:
+            ops.gemm_out(a, wt, out)
+
+    def _gate_up(self, x, L, h) -> None:
+        """h = SiLU(x·W_gateᵀ)·(x·W_upᵀ): fused epilogue on the tiled kernels, or the library GEMM into a [rows, 2F]
+        product (gate / up interleaved in 8-column blocks, as the tiled rows) + the vectorised silu_mul pass."""
+        rows = x.shape[0]
+        if self.lib and L.wgu_s is not None and LIB_MIN_ROWS["gate_up"] <= rows <= self._gu.shape[0]:
+            gu = self._gu[:rows]
+            torch.matmul(x, L.wgu_s.t(), out=gu)
+            ops.silu_mul(gu, h)
+        else:
+            ops.gemm_silu(x, L.wgu_t, h)
+
     def _prefill_post_attention(self, T: int, attn, L, w_next, resid, x, h, tmp) -> None:
         """resid += all_reduce(attn·Woᵀ); x = norm(resid); resid += all_reduce(silu-mlp(x)); x = norm(resid)·w_next.
 
@@ -562,33 +601,33 @@ class ModelRunner:
         eps = self.cfg.rms_eps
         chunks = prefill_row_chunks(T, self.comm.size)
         if len(chunks) == 1:
-            self._prefill_resid(attn, L.wo_t, resid, L.ffn_norm, x, tmp)
-            ops.gemm_silu(x, L.wgu_t, h)
-            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
+            self._prefill_resid(attn, L.wo_t, resid, L.ffn_norm, x, tmp, L.wo_s, "o")
+            self._gate_up(x, L, h)
+            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp, L.wd_s, "down")
             return
         main = torch.cuda.current_stream(self.device) if tmp.is_cuda else None
         ar1 = []
         for a, b in chunks:
-            ops.gemm_out(attn[a:b], L.wo_t, tmp[a:b])
+            self._proj(attn[a:b], L.wo_t, L.wo_s, tmp[a:b], "o")
             ar1.append(self._comm_async(tmp[a:b]))
         ar2 = []
         for (a, b), ev in zip(chunks, ar1):
             if ev is not None:
                 main.wait_event(ev)
             ops.rmsnorm(resid[a:b], L.ffn_norm, x[a:b], eps, delta=tmp[a:b])
-            ops.gemm_silu(x[a:b], L.wgu_t, h[a:b])
-            ops.gemm_out(h[a:b], L.wd_t, tmp[a:b])  # tmp rows [a, b) are free: their O all-reduce was consumed
+            self._gate_up(x[a:b], L, h[a:b])
+            self._proj(h[a:b], L.wd_t, L.wd_s, tmp[a:b], "down")  # tmp rows [a, b) are free: their O all-reduce was consumed
             ar2.append(self._comm_async(tmp[a:b]))
         for (a, b), ev in zip(chunks, ar2):
             if ev is not None:
                 main.wait_event(ev)
             ops.rmsnorm(resid[a:b], w_next, x[a:b], eps, delta=tmp[a:b])
 
-    def _prefill_resid(self, a, wt, resid, norm_w, x, tmp) -> None:
+    def _prefill_resid(self, a, wt, resid, norm_w, x, tmp, ws=None, kind: str = "o") -> None:
         """resid += a·wᵀ, x = RMSNorm(resid).  Thousands of rows: the product goes out as a bf16 tile (row-contiguous
         stores) and the norm kernel adds it -- the fused fp32 read-modify-write epilogue measured +120 us per
         8192-row projection (profiles/r2/prefill_kernels_8k.md)."""
-        ops.gemm_out(a, wt, tmp)
+        self._proj(a, wt, ws, tmp, kind)
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 
@@ -699,12 +738,12 @@ class ModelRunner:
         resid, x, q, attn, h, tmp, qkv = (d[k] for k in ("resid", "x", "q", "attn", "h", "tmp", "qkv"))
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d["ids"])
         nl = len(w.layers)
-        # every projection on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows);
-        # gate_up with its fused SiLU·mul epilogue (no [T, 2F] intermediate)
+        # projections on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows; gate_up with its
+        # fused SiLU·mul epilogue) below lib_min rows, on the library GEMM above (_proj / _gate_up)
         for li, L in enumerate(w.layers):
             # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
             # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
-            ops.gemm_out(x, L.wqkv_t, qkv)
+            self._proj(x, L.wqkv_t, L.wqkv_s, qkv, "qkv")
             ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
                                 d["wt"], attn, self.part_o, self.part_ml, d["part"], 1)
@@ -777,7 +816,7 @@ class ModelRunner:
         nl = len(w.layers)
         for li, L in enumerate(w.layers):
             kc, vc = self.kv.k[li], self.kv.v[li]
-            ops.gemm_out(x, L.wqkv_t, qkv)
+            self._proj(x, L.wqkv_t, L.wqkv_s, qkv, "qkv")
             ops.rope_kv_write(qkv, pos, slots, self.rope, q, kc, vc, nh, nkv)
             ops.paged_attention(0, q[r], kc, vc, self.block_tables[r], self.q_start[r], self.q_len[r],
                                 self.ctx_len[r], self.work_seq[r], self.work_tile[r], attn[r], self.part_o,
@@ -785,7 +824,7 @@ class ModelRunner:
             ops.paged_attention(2, q, kc, vc, d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"], d["wt"], attn,
                                 self.part_o, self.part_ml, d["part"], 1)
             self._resid_proj(attn.view(M, nh * 128), L.wo_t, resid, L.ffn_norm, x, tmp)
-            ops.gemm_silu(x, L.wgu_t, h)
+            self._gate_up(x, L, h)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             self._resid_proj(h, L.wd_t, resid, w_next, x, tmp)
         ops.gemm_out(x[r], w.lm_head_t, self.logits[r])

@@ -43,10 +43,13 @@ for s in "$@"; do
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     prof64_mega) DSSE_MEGA=1 step prof64_mega 600 rocprofv3 --kernel-trace --stats -d "$out/prof64_mega" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
+    ttft8k_nolib) DSSE_PREFILL_LIB=0 step ttft8k_nolib 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
+    ttft512) step ttft512 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
     c3stub) HIP_VISIBLE_DEVICES= DSSE_DIST_BACKEND=gloo step c3stub 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 8 --streams 256 --steps 64 --warmup 8 --stub-step-ms 9.7 ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill" ;;
     attn_bench) step attn_bench 300 python -u tools/bench_prefill_attn.py --T 8192,2048,512 --sdpa ;;
     gemm_bench) step gemm_bench 300 python -u tools/bench_gemm_tiled.py --M 8192,256 --cfg auto ;;
+    gemm_mid) step gemm_mid 300 python -u tools/bench_gemm_tiled.py --M 1024,512 --cfg auto ;;
     gemm_wide) step gemm_wide 300 python -u tools/bench_gemm_tiled.py --M 256,192 --cfg auto,0,1,5 --no-library ;;
     pmc_attn)
       step pmc_attn_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_attn_a" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
