@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--decode-steps", type=int, default=16)
+    ap.add_argument("--profile-marker", action="store_true",
+                    help="launch one bitwise_not kernel after the warm-up iteration: tools/trace_sum.py --after-kernel "
+                         "bitwise_not then keeps only the timed iterations of a rocprofv3 kernel trace")
     args = ap.parse_args()
 
     import numpy as np
@@ -87,6 +90,9 @@ def main():
         return ttft, itl, first
 
     one_iter()  # warm-up (allocator, first launches)
+    if args.profile_marker:
+        torch.ones(1, dtype=torch.int32, device=device).bitwise_not_()
+        torch.cuda.synchronize()
     ttfts, itls = [], []
     for _ in range(args.iters):
         a, b, _ = one_iter()
