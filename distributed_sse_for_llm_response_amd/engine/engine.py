@@ -160,6 +160,64 @@ class _Drain:
         return (self.pf_host if first else self.host)[row]
 
 
+class PassCost:
+    """Measured GPU cost of the engine's step kinds, for the adaptive prefill budget (pick the
+    chunk from measured pass cost, not a fixed size).  Timing events bracket every separate prefill pass and every
+    decode step; they are read once they have completed (no host wait).  Decode: an EMA of the step per bucket.
+    Prefill passes: an exponentially weighted least-squares line ms = a + b * tokens.
+
+    budget(B) = the largest multiple of 64 prompt tokens whose pass costs at most (ratio - 1) x step(B): a stream
+    whose token gap spans a decode step AND a prefill pass then waits at most `ratio` x the steady step.  Until both
+    costs are measured it returns None (the caller keeps its configured budget)."""
+
+    def __init__(self, ratio: float, decay: float = 0.9):
+        self.ratio = ratio
+        self.decay = decay
+        self.step_ms: dict = {}
+        self._fit = [0.0] * 5  # weighted sums: w, w t, w t^2, w y, w t y
+        self._pending: deque = deque()
+
+    def record(self, kind: str, key: int):
+        """(start event, end-record callable) around one enqueued pass; kind 'decode' (key = bucket) or 'prefill'
+        (key = tokens)."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return lambda: (e1.record(), self._pending.append((kind, key, e0, e1)))
+
+    def observe(self, kind: str, key: int, ms: float) -> None:
+        if kind == "decode":
+            old = self.step_ms.get(key)
+            self.step_ms[key] = ms if old is None else 0.8 * old + 0.2 * ms
+            return
+        f, d, t = self._fit, self.decay, float(key)
+        for i, v in enumerate((1.0, t, t * t, ms, t * ms)):
+            f[i] = d * f[i] + v
+
+    def poll(self) -> None:
+        while self._pending and self._pending[0][3].query():
+            kind, key, e0, e1 = self._pending.popleft()
+            self.observe(kind, key, e0.elapsed_time(e1))
+
+    def line(self):
+        """(a, b) of the pass-cost line, or None before two passes of different sizes were seen."""
+        w, st, stt, sy, sty = self._fit
+        den = w * stt - st * st
+        if w <= 0 or den <= 1e-6 * max(1.0, w * stt):
+            return None
+        b = (w * sty - st * sy) / den
+        a = (sy - b * st) / w
+        return (max(0.0, a), b) if b > 0 else None
+
+    def budget(self, B: int, cap: int):
+        step = self.step_ms.get(B)
+        line = self.line()
+        if step is None or line is None:
+            return None
+        a, b = line
+        room = (self.ratio - 1.0) * step - a
+        return max(64, min(cap, int(room / b) // 64 * 64)) if room > 0 else 64
+
+
 class LLMEngine:
     def __init__(self, runner: ModelRunner, eos_id: int = 2, prefill_budget: int = 512,
                  idle_prefill_budget: int | None = None, default_params: SamplingParams | None = None,
@@ -208,6 +266,13 @@ class LLMEngine:
         self.mixed_min_b = mixed_min_b()  # "auto": mixed steps only from this decode bucket up
         self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
         self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
+        # adaptive prefill budget (separate passes while streams decode): DSSE_PREFILL_ITL_RATIO = r > 1 sizes each
+        # pass so that a token gap spanning a decode step and a pass stays <= r x the occupied bucket's step
+        # (PassCost), up to prefill_budget; a prompt that has waited DSSE_PREFILL_BOOST_STEPS steps gets the full
+        # budget (TTFT guard).  Unset / 0: the fixed prefill_budget.
+        ratio = float(os.environ.get("DSSE_PREFILL_ITL_RATIO", "0") or 0)
+        self.cost = PassCost(ratio) if ratio > 1.0 and runner.device.type == "cuda" else None
+        self.boost_steps = int(os.environ.get("DSSE_PREFILL_BOOST_STEPS", "8"))
 
     # ------------------------------------------------------------------ requests
     def next_rid(self) -> int:
@@ -446,9 +511,24 @@ class LLMEngine:
         entry = graphs.get(B)
         return entry is not None and sum(len(c.tokens) for c in chunks) <= entry[0] and len(chunks) <= PREFILL_GRAPH_SEQS
 
+    def set_itl_ratio(self, ratio: float) -> None:
+        """Adaptive prefill budget on (ratio > 1) or off (bench_serving sweeps both in one process)."""
+        self.cost = PassCost(ratio) if ratio > 1.0 and self.r.device.type == "cuda" else None
+
+    def _oldest_prefill_step(self) -> int:
+        oldest = min((s.enq_step for s in self.slots if s is not None and s.state == "prefill"), default=self.step_no)
+        if self.waiting:
+            oldest = min(oldest, self.waiting[0].enq_step)
+        return oldest
+
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
         budget = self.prefill_budget if running_decode else self.idle_prefill_budget
+        if running_decode and self.cost is not None and not self.mixed:
+            self.cost.poll()
+            adaptive = self.cost.budget(self._decode_bucket(), self.prefill_budget)
+            if adaptive is not None and self.step_no - self._oldest_prefill_step() <= self.boost_steps:
+                budget = adaptive
         if running_decode and self.mixed and self._decode_bucket() >= self.mixed_min_b:
             # the chunk rides in the decode step: keep B + chunk near the next row bucket, unless a prompt has
             # waited too long (counted in steps: identical on every TP rank)
@@ -521,7 +601,10 @@ class LLMEngine:
         mixed = bool(chunks) and bool(dec) and self.mixed and B >= self.mixed_min_b and self._mixed_fits(B, chunks)
         if chunks:
             if not mixed:
+                done = self.cost.record("prefill", sum(len(c.tokens) for c in chunks)) if self.cost else None
                 r.prefill(chunks, ring_row=row)
+                if done:
+                    done()
             self.stats["prefill_tokens"] += sum(len(c.tokens) for c in chunks)
             if not mixed and dec and prefill_done:
                 # a decode step follows on the stream: drain the first tokens now (TTFT minus one decode step)
@@ -535,7 +618,10 @@ class LLMEngine:
                 r.mixed(B, chunks, ring_row=row)
                 self.stats["mixed_steps"] += 1
             else:
+                done = self.cost.record("decode", B) if self.cost else None
                 r.decode(B)
+                if done:
+                    done()
             for s in dec:
                 s.decode_enqueued += 1
                 producers.append((s.slot, s))

@@ -1,0 +1,56 @@
+"""Adaptive prefill budget (engine.PassCost): the pass-cost line fit and the budget it gives per decode bucket."""
+import pytest
+
+from distributed_sse_for_llm_response_amd.engine.engine import PassCost
+
+
+def _feed(pc, a=1.5, b=0.016, sizes=(128, 256, 512, 384, 256, 512)):
+    for t in sizes:
+        pc.observe("prefill", t, a + b * t)
+
+
+def test_line_recovers_a_linear_pass_cost():
+    pc = PassCost(2.0)
+    assert pc.line() is None
+    pc.observe("prefill", 512, 9.7)
+    assert pc.line() is None  # one size: no slope yet
+    _feed(pc)
+    a, b = pc.line()
+    assert a == pytest.approx(1.5, abs=0.05) and b == pytest.approx(0.016, rel=0.02)
+
+
+def test_budget_keeps_a_step_plus_pass_within_the_ratio():
+    pc = PassCost(2.0)
+    _feed(pc)
+    assert pc.budget(64, 512) is None  # no decode step measured for the bucket yet
+    for ms in (4.3, 4.3, 4.3):
+        pc.observe("decode", 64, ms)
+    for ms in (6.1, 6.1):
+        pc.observe("decode", 128, ms)
+    b64, b128 = pc.budget(64, 512), pc.budget(128, 512)
+    assert b64 % 64 == 0 and b128 % 64 == 0 and 64 <= b64 < b128 <= 512
+    for B, bud in ((64, b64), (128, b128)):
+        step = pc.step_ms[B]
+        assert 1.5 + 0.016 * bud <= (2.0 - 1.0) * step + 1e-6  # the pass fits in one step's time
+        assert 1.5 + 0.016 * (bud + 64) > step                 # and is the largest multiple of 64 that does
+    # a generous ratio is capped by the configured budget; a step too short for any pass still moves 64 tokens
+    assert PassCost(10.0).budget(64, 512) is None
+    big = PassCost(10.0)
+    _feed(big)
+    big.observe("decode", 64, 4.3)
+    assert big.budget(64, 512) == 512
+    tiny = PassCost(1.1)
+    _feed(tiny)
+    tiny.observe("decode", 64, 4.3)
+    assert tiny.budget(64, 512) == 64
+
+
+def test_decode_step_ema_and_bad_fits():
+    pc = PassCost(2.0)
+    pc.observe("decode", 64, 4.0)
+    pc.observe("decode", 64, 5.0)
+    assert pc.step_ms[64] == pytest.approx(4.2)
+    # a falling cost line (noise) is not used
+    for t, ms in ((128, 5.0), (512, 3.0), (256, 4.5)):
+        pc.observe("prefill", t, ms)
+    assert pc.line() is None and pc.budget(64, 512) is None

@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--long-every", type=int, default=0)
     ap.add_argument("--long-words", type=int, default=8000)
     ap.add_argument("--prefill-budget", default="2048", help="comma list of PREFILL_BUDGET values")
+    ap.add_argument("--itl-ratios", default="0",
+                    help="comma list of DSSE_PREFILL_ITL_RATIO values (0 = fixed budget; r > 1 = adaptive budget "
+                         "capped by PREFILL_BUDGET: a step plus a pass <= r x the bucket's step)")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=8448)
     ap.add_argument("--skip-s", type=float, default=2.0)
@@ -100,8 +103,9 @@ def main():
     message = " ".join(f"w{i % 997}" for i in range(a.prompt_words))
     try:
         runs = 0
-        for budget in [int(b) for b in a.prefill_budget.split(",")]:
+        for budget, ratio in [(int(b), float(q)) for b in a.prefill_budget.split(",") for q in a.itl_ratios.split(",")]:
             app.engine.prefill_budget = budget
+            app.engine.set_itl_ratio(ratio)
             for rate in [float(r) for r in a.rates.split(",")]:
                 for warm, n in ((True, a.warmup_requests), (False, a.requests)):
                     if warm and runs > 0:
@@ -118,6 +122,7 @@ def main():
                     if warm:
                         continue
                     out = {"metric": "serving under Poisson arrivals", "rate_req_s": rate, "prefill_budget": budget,
+                           "itl_ratio": ratio,
                            "max_tokens": a.max_tokens, "prompt_tokens": a.prompt_words + 6,
                            "long_prompt_every": a.long_every, "long_prompt_tokens": a.long_words + 6 if a.long_every else 0,
                            **analyse(res["arrivals"], n, a.long_every, a.skip_s, a.max_tokens),
