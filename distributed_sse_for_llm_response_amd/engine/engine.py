@@ -601,7 +601,8 @@ class LLMEngine:
         mixed = bool(chunks) and bool(dec) and self.mixed and B >= self.mixed_min_b and self._mixed_fits(B, chunks)
         if chunks:
             if not mixed:
-                done = self.cost.record("prefill", sum(len(c.tokens) for c in chunks)) if self.cost else None
+                done = (self.cost.record("prefill", sum(len(c.tokens) for c in chunks))
+                        if self.cost is not None and r.device.type == "cuda" else None)
                 r.prefill(chunks, ring_row=row)
                 if done:
                     done()
@@ -618,7 +619,7 @@ class LLMEngine:
                 r.mixed(B, chunks, ring_row=row)
                 self.stats["mixed_steps"] += 1
             else:
-                done = self.cost.record("decode", B) if self.cost else None
+                done = self.cost.record("decode", B) if self.cost is not None and r.device.type == "cuda" else None
                 r.decode(B)
                 if done:
                     done()

@@ -54,3 +54,56 @@ def test_decode_step_ema_and_bad_fits():
     for t, ms in ((128, 5.0), (512, 3.0), (256, 4.5)):
         pc.observe("prefill", t, ms)
     assert pc.line() is None and pc.budget(64, 512) is None
+
+
+def test_engine_sizes_prefill_chunks_from_the_cost_model():
+    """With a PassCost attached (as DSSE_PREFILL_ITL_RATIO does on a GPU), a prompt arriving while streams decode is
+    prefilled in chunks of the model's budget for the occupied bucket; a prompt starved past boost_steps gets the full
+    PREFILL_BUDGET; the token streams equal the fixed-budget engine's (greedy)."""
+    import torch
+
+    from distributed_sse_for_llm_response_amd.engine.engine import LLMEngine, SamplingParams
+    from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner
+    from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+    from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights
+
+    w = convert_standard(TINY, init_standard_weights(TINY, seed=11))
+
+    def run(cost):
+        r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device="cpu", use_graphs=False)
+        e = LLMEngine(r, eos_id=-1, prefill_budget=256)
+        e.cost = cost
+        e.boost_steps = 3
+        chunks = []
+        orig = r.prefill
+
+        def spy(seqs, ring_row):
+            chunks.append(sum(len(s.tokens) for s in seqs))
+            return orig(seqs, ring_row=ring_row)
+
+        r.prefill = spy
+        g = torch.Generator().manual_seed(3)
+        out = {}
+        e.add_request("a", torch.randint(3, TINY.vocab_size, (20,), generator=g).tolist(),
+                      SamplingParams(temperature=0.0, max_tokens=12))
+        long_prompt = torch.randint(3, TINY.vocab_size, (300,), generator=g).tolist()
+        for step in range(400):
+            if step == 2:
+                e.add_request("b", long_prompt, SamplingParams(temperature=0.0, max_tokens=4))
+            for ev in e.step():
+                out.setdefault(ev.conversation_id, []).append(ev.token_id)
+            if step > 2 and not e.has_work():
+                break
+        return chunks, out
+
+    fixed_chunks, fixed_out = run(None)
+    pc = PassCost(2.0)
+    for t in (64, 128, 256, 128):
+        pc.observe("prefill", t, 1.0 + 0.02 * t)
+    pc.observe("decode", 1, 2.3)  # bucket 1 (one decoding stream): budget = (2.3 - 1.0) / 0.02 -> 64
+    assert pc.budget(1, 256) == 64
+    ad_chunks, ad_out = run(pc)
+    assert fixed_out == ad_out
+    assert 256 in fixed_chunks  # the long prompt's first pass at the fixed budget
+    # adaptive: 64-token passes while "a" decodes, until the starvation guard hands the rest the full budget
+    assert ad_chunks[1] == 64 and max(ad_chunks) <= 256 and len(ad_chunks) > len(fixed_chunks)
