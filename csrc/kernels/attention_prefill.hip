@@ -54,19 +54,24 @@ DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
 }
 }  // namespace
 
-template <int G>
-__global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
-  constexpr int NW = 2 * G;
+// G = q heads per kv head; HG = the q heads one workgroup takes (HG < G splits a kv head's q heads over G / HG
+// workgroups: short prompts, where one workgroup per (tile, kv head) leaves most CUs idle -- a 512-token prompt is 64
+// workgroups; each then stages its K/V itself, which the L2 serves)
+template <int G, int HG>
+__global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
+  constexpr int NW = 2 * HG;
+  constexpr int NSPLIT = G / HG;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // kRing blocks of kStage
 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int r = lane & 15, g = lane >> 4;
-  const int wh = w % G, wq = w / G;
+  const int wh = w % HG, wq = w / HG;
   // flat grid, head fastest: workgroup b runs on XCD b % 8, so with Hkv = 8 every XCD serves ONE kv head and
   // its 4 MiB of 8k-context K/V stays in that XCD's L2 for all the head's query tiles (a (tile, head) grid put
   // consecutive tiles on different XCDs and every XCD streamed all 8 heads); the work list is heaviest-first
   // globally, not per head
-  const int item = blockIdx.x / p.hkv, h = blockIdx.x % p.hkv;
+  const int h = blockIdx.x % p.hkv, rest = blockIdx.x / p.hkv;
+  const int hs = rest % NSPLIT, item = rest / NSPLIT;
   const int b = p.work_seq[item];
   const int qlen = p.q_len[b], ctx = p.ctx_len[b];
   const int pos0 = ctx - qlen;                 // absolute position of query 0 of this chunk
@@ -78,7 +83,7 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   const int nblk = (kmax + kBK - 1) / kBK;
   const int w_last_pos = pos0 + min(qlen, q0 + 32) - 1;  // last visible key of this wave
   const int w_first_pos = pos0 + q0;
-  const int head = h * G + wh;
+  const int head = h * G + hs * HG + wh;
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   const int npages = (kmax + kBS - 1) / kBS;
 
@@ -105,9 +110,9 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   // last are issued too (pages clamp to the context, nobody reads them): a branch around the DMA made the
   // compiler's waitcnt placement drain every load in flight.
   constexpr int IPW = 32 / NW;
-  auto issue_block = [&](int j) {
+  auto issue_block = [&](int j, int slot) {
     const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
-    char* base = smem + (j % kRing) * kStage;
+    char* base = smem + slot * kStage;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const int q = w * IPW + i;  // wave-uniform
@@ -128,32 +133,48 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+  float m_run[2] = {-1e30f, -1e30f};
+  // per-lane partial row sums (packed pairs): reduced over the 4 lane groups of a query once, after the last block
+  f32x2 l_part[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
   const float sc = p.scale_log2;
   f32x4 s4[4][2];  // Sᵀ[key tile kt][query tile qt] of the current block, live across the mid-block barrier
 
-  // phase 1: Sᵀ = K·Qᵀ of the block in LDS slot `buf`
+  // Lane-constant parts of the fragment addresses: K row 16 kt + r, chunk (4g + s) ^ swz(r) = kt * 4096 + kofs[s];
+  // Vᵀ row d = 16 dt + r, chunk (4t + g) ^ ((d >> 1) & 7) = (4t + g) ^ ((r >> 1) & 7) = dt * 2048 + vofs[t].  With the
+  // slot a compile-time constant (the block loop is unrolled by the ring) every read is one base VGPR + an immediate.
+  int kofs[4], vofs[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) kofs[s2] = r * 256 + (((4 * g + s2) ^ swz(r)) << 4);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) vofs[t] = kKBytes + r * 128 + (((4 * t + g) ^ ((r >> 1) & 7)) << 4);
+
+  // phase 1: Sᵀ = K·Qᵀ of the block in LDS slot `buf`; a key tile's 4 fragments are read one tile ahead
   auto qk = [&](int buf) {
     const char* kb = smem + buf * kStage;
+    bf16x8 kf[2][4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) kf[0][s2] = *reinterpret_cast<const bf16x8*>(kb + kofs[s2]);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
+      if (kt < 3) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+          kf[(kt + 1) & 1][s2] = *reinterpret_cast<const bf16x8*>(kb + (kt + 1) * 4096 + kofs[s2]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int row = 16 * kt + r;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 256 + (((4 * g + s) ^ swz(r)) << 4));
+      for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf, qf[qt][s], s4[kt][qt]);
-      }
+        for (int qt = 0; qt < 2; ++qt) s4[kt][qt] = mfma16x16x32(kf[kt & 1][s2], qf[qt][s2], s4[kt][qt]);
     }
     __builtin_amdgcn_s_setprio(0);
   };
   // phase 2: online softmax of block j and Oᵀ += Vᵀ·Pᵀ
   auto sm_pv = [&](int j, int buf) {
     const int key0 = j * kBK;
-    const char* vb = smem + buf * kStage + kKBytes;
     const bool need_mask = key0 + kBK - 1 > w_first_pos;  // some key of the block is after some query
     bf16x8 pf[2][2];  // [qt][page t]
 #pragma unroll
@@ -187,7 +208,7 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
         const float m_new = fmaxf(m_run[qt], m_blk);
         // a column with no visible key yet keeps m = -1e30 and must produce p = 0, not exp2(0)
         const float alpha = __builtin_amdgcn_exp2f(m_run[qt] - (m_new < -1e29f ? 0.f : m_new));
-        l_run[qt] *= alpha;
+        l_part[qt] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) {
           o[dt][qt][0] *= alpha;
@@ -198,18 +219,22 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
         m_run[qt] = m_new;
       }
       const float m_use = m_run[qt] < -1e29f ? 0.f : m_run[qt];
-      // raw v_exp_f32 (no denormal range reduction: arguments are <= thr and underflow to 0 is wanted);
-      // the scale is folded into one FMA per score
-      float sum = 0.f;
+      // raw v_exp_f32 (no denormal range reduction: arguments are <= thr and underflow to 0 is wanted); the scale
+      // is folded into one packed FMA per score pair and the row sum is a packed add (VALU is this loop's bound:
+      // profiles/r4/pmc_flash_prefill_r4.md)
+      const f32x2 scv = {sc, sc}, mv = {-m_use, -m_use};
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(s4[kt][qt][i], sc, -m_use));
-          s4[kt][qt][i] = e;
-          sum += e;
+        for (int i = 0; i < 4; i += 2) {
+          f32x2 v = {s4[kt][qt][i], s4[kt][qt][i + 1]};
+          v = __builtin_elementwise_fma(v, scv, mv);
+          v[0] = __builtin_amdgcn_exp2f(v[0]);
+          v[1] = __builtin_amdgcn_exp2f(v[1]);
+          s4[kt][qt][i] = v[0];
+          s4[kt][qt][i + 1] = v[1];
+          l_part[qt] += v;
         }
-      l_run[qt] += rows4_sum(sum);
       // Pᵀ fragments: page t = key tiles 2t (keys 4g+i) and 2t+1 (keys 16+4g+i)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -219,17 +244,21 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
           pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
         }
     }
-    // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ
+    // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ: the 8 fragments of a page read before its 16 MFMAs
+    const char* vb0 = smem + buf * kStage;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 vf[8];
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const int d = 16 * dt + r;
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vb + d * 128 + (((t * 4 + g) ^ ((d >> 1) & 7)) << 4));
+      for (int dt = 0; dt < 8; ++dt) vf[dt] = *reinterpret_cast<const bf16x8*>(vb0 + dt * 2048 + vofs[t]);
+      // keep the 8 reads ahead of the MFMAs (the scheduler otherwise pairs 2 reads with a full lgkmcnt wait)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf, pf[qt][t], o[dt][qt]);
-      }
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] = mfma16x16x32(vf[dt], pf[qt][t], o[dt][qt]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -244,19 +273,26 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   // softmax/PV(j), which for the lagging half is absolute barrier 2(j + 1), the lagging half needs block j + 1
   // with blocks up to j + 2 issued (wait: all but the youngest).
   const bool lag = wq == 1;
-  issue_block(0);
-  issue_block(1);
-  issue_block(2);
+  issue_block(0, 0);
+  issue_block(1, 1);
+  issue_block(2, 2);
   if (lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
-  for (int j = 0; j < nblk; ++j) {
-    const bool vis = j * kBK <= w_last_pos;  // this wave sees at least one key of the block
-    if (!lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
-    else asm volatile("s_barrier" ::: "memory");
-    if (vis) qk(j % kRing);
-    if (!lag) asm volatile("s_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(IPW) : "memory");
-    issue_block(j + 3);
-    if (vis) sm_pv(j, j % kRing);
+  // unrolled by the ring size: each block's LDS slot is a compile-time offset (no per-read address arithmetic)
+  for (int j0 = 0; j0 < nblk; j0 += kRing) {
+#pragma unroll
+    for (int k = 0; k < kRing; ++k) {
+      const int j = j0 + k;
+      if (j < nblk) {
+        const bool vis = j * kBK <= w_last_pos;  // this wave sees at least one key of the block
+        if (!lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
+        else asm volatile("s_barrier" ::: "memory");
+        if (vis) qk(k);
+        if (!lag) asm volatile("s_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(IPW) : "memory");
+        issue_block(j + 3, (k + 3) % kRing);
+        if (vis) sm_pv(j, k);
+      }
+    }
   }
   if (!lag) asm volatile("s_barrier" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may still write this workgroup's LDS after it exits
@@ -266,7 +302,8 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
   for (int qt = 0; qt < 2; ++qt) {
     const int qi = q0 + 16 * qt + r;
     if (qi >= qlen) continue;
-    const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
+    const float l = rows4_sum(l_part[qt][0] + l_part[qt][1]);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + head) * kD + 4 * g;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
@@ -282,29 +319,33 @@ __global__ void __launch_bounds__(128 * G) flash_prefill_kernel(AttnParams p) {
 
 }  // namespace dsse
 
-// Work items: (sequence, 64-query tile) pairs; grid = num_work x Hkv workgroups, head fastest.  Requires G = Hq/Hkv in {1, 2, 4}.
-extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
+namespace {
+template <int G, int HG>
+hipError_t launch_flash(int num_work, const dsse::AttnParams* p, hipStream_t st) {
   using namespace dsse;
-  if (num_work <= 0) return hipSuccess;
-  const dim3 grid(num_work * p->hkv);
   constexpr int lds = kRing * kStage;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<G, HG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
+  hipLaunchKernelGGL((flash_prefill_kernel<G, HG>), dim3(num_work * p->hkv * (G / HG)), dim3(128 * HG), lds, st, *p);
+  return hipGetLastError();
+}
+}  // namespace
+
+// Work items: (sequence, 64-query tile) pairs; grid = num_work x Hkv workgroups, kv head fastest.  Requires
+// G = Hq/Hkv in {1, 2, 4}.  (Splitting a kv head's q heads over G workgroups for short prompts -- 256 workgroups of
+// 2 waves instead of 64 of 8 at 512 tokens -- measured 38.9 vs 28.8 us and was dropped; profiles/r4.)
+extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
+  if (num_work <= 0) return hipSuccess;
   switch (p->group) {
-    case 1: hipLaunchKernelGGL((flash_prefill_kernel<1>), grid, dim3(128), lds, st, *p); break;
-    case 2: hipLaunchKernelGGL((flash_prefill_kernel<2>), grid, dim3(256), lds, st, *p); break;
-    case 4: hipLaunchKernelGGL((flash_prefill_kernel<4>), grid, dim3(512), lds, st, *p); break;
+    case 1: return launch_flash<1, 1>(num_work, p, st);
+    case 2: return launch_flash<2, 2>(num_work, p, st);
+    case 4: return launch_flash<4, 4>(num_work, p, st);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 DSSE_CHECK_READER(dsse_check_attention_prefill)

@@ -110,7 +110,7 @@ rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* _
   const int pos = DSSE_IDX(positions[t], rope_len, 0);
   const int slot = slots[t] < 0 ? -1 : DSSE_IDX(slots[t], num_slots, -1);
   const int blk = slot >= 0 ? slot / kPageTok : 0, off = slot >= 0 ? slot % kPageTok : 0;
-  const int nrot = (hq + hkv) * 8, nv = slot >= 0 ? hkv * 16 : 0;
+  const int nrot = (hq + hkv) * 8, nv = 0;  // V: v_page_write_kernel
   for (int idx = threadIdx.x; idx < nrot + nv; idx += blockDim.x) {
     if (idx < nrot) {
       const int u = idx >> 3, j = idx & 7;
@@ -139,6 +139,45 @@ rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* _
 #pragma unroll
       for (int e = 0; e < 8; ++e) vp[(size_t)e * kPageTok] = v[e];
     }
+  }
+}
+
+// ---- V into the transposed, token-permuted pages, a page row at a time -----------------------------------------
+// The per-token form (rope_kv_write_kernel's V branch) writes 2 bytes per (token, d): 128 scattered stores per head
+// per token.  Here a workgroup takes 32 consecutive rows x one kv head; thread d gathers its 32 values (coalesced
+// over d) and, when the 32 rows fill one whole page in order (prefill of a page-aligned run), writes the page's row
+// d as 4 x 16-byte stores in the vperm token order.  Other groups (page boundaries, padding, scattered slots) fall
+// back to per-element stores.
+__global__ void __launch_bounds__(128)
+v_page_write_kernel(const bf16* __restrict__ qkv, int T, int hq, int hkv, const int* __restrict__ slots,
+                    bf16* __restrict__ v_cache, int num_slots) {
+  const int t0 = blockIdx.x * kPageTok, h = blockIdx.y, d = threadIdx.x;
+  const int ncols = (hq + 2 * hkv) * 128;
+  const int lane = threadIdx.x & 63;
+  const int tl = t0 + (lane & 31);
+  const int my_slot = tl < T ? (slots[tl] < 0 ? -1 : DSSE_IDX(slots[tl], num_slots, -1)) : -1;
+  const int s0 = __shfl(my_slot, 0);
+  const bool whole = __all(s0 >= 0 && s0 % kPageTok == 0 && my_slot == s0 + (lane & 31));
+  // qkv columns are in the engine's permuted order: inside 16-column tile j, columns 0-7 = dims 8j..8j+7 and columns
+  // 8-15 = dims 64 + 8j .. 64 + 8j + 7
+  const int col = d < 64 ? 16 * (d >> 3) + (d & 7) : 16 * ((d - 64) >> 3) + 8 + (d & 7);
+  const bf16* src = qkv + (size_t)t0 * ncols + (hq + hkv + h) * 128 + col;
+  if (whole) {
+    bf16 v[kPageTok];
+#pragma unroll
+    for (int i = 0; i < kPageTok; ++i) v[i] = src[(size_t)i * ncols];
+    bf16x8 o[4];
+#pragma unroll
+    for (int i = 0; i < kPageTok; ++i) o[vperm_tok(i) >> 3][vperm_tok(i) & 7] = v[i];
+    bf16* dst = v_cache + (((size_t)(s0 / kPageTok) * hkv + h) * 128 + d) * kPageTok;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(dst + 8 * q) = o[q];
+    return;
+  }
+  for (int i = 0; i < kPageTok && t0 + i < T; ++i) {
+    const int sl = __shfl(my_slot, i);
+    if (sl < 0) continue;
+    v_cache[(((size_t)(sl / kPageTok) * hkv + h) * 128 + d) * kPageTok + vperm_tok(sl % kPageTok)] = src[(size_t)i * ncols];
   }
 }
 
@@ -217,6 +256,8 @@ extern "C" hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv
                      reinterpret_cast<const bf16*>(qkv), hq, hkv, positions, slots, rope,
                      reinterpret_cast<bf16*>(q_out), reinterpret_cast<bf16*>(k_cache),
                      reinterpret_cast<bf16*>(v_cache), num_slots, rope_len);
+  hipLaunchKernelGGL(v_page_write_kernel, dim3((T + kPageTok - 1) / kPageTok, hkv), dim3(128), 0, st,
+                     reinterpret_cast<const bf16*>(qkv), T, hq, hkv, slots, reinterpret_cast<bf16*>(v_cache), num_slots);
   return hipGetLastError();
 }
 

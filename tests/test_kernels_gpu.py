@@ -358,12 +358,19 @@ def test_rmsnorm_back_to_back_modes(gpu):
         _close(y, yr, 2e-2, 1e-2, f"y it={it} M={M} mode={mode}")
 
 
-def test_rope_kv_write_and_silu_mul(gpu):
-    nh, nkv, T = 8, 2, 45
+@pytest.mark.parametrize("layout", ["scattered", "pages"])
+def test_rope_kv_write_and_silu_mul(gpu, layout):
+    """layout 'pages': rows 0-63 fill pages 1 and 2 in order (the page-row V path), rows 64-76 start page 0 and the
+    last row is padding (slot -1); 'scattered': random slots (the per-element V path)."""
+    nh, nkv = 8, 2
+    T = 45 if layout == "scattered" else 78
     g = torch.Generator().manual_seed(5)
     qkv = torch.randn(T, (nh + 2 * nkv) * 128, generator=g).bfloat16()
     positions = torch.arange(100, 100 + T, dtype=torch.int32)
-    slots = torch.randperm(4 * 32, generator=g)[:T].to(torch.int32)
+    if layout == "scattered":
+        slots = torch.randperm(4 * 32, generator=g)[:T].to(torch.int32)
+    else:
+        slots = torch.cat([torch.arange(32, 96), torch.arange(0, 13), torch.tensor([-1])]).to(torch.int32)
     rope = R.rope_table(1024, 1e6)
     q, kc, vc = (torch.zeros(T, nh, 128, dtype=torch.bfloat16), torch.zeros(4, nkv, 32, 128, dtype=torch.bfloat16),
                  torch.zeros(4, nkv, 128, 32, dtype=torch.bfloat16))
@@ -472,9 +479,10 @@ def test_qkv_attention_decode_folded_epilogue(gpu, monkeypatch, cfg, M, part):
 
 @pytest.mark.parametrize("mode,hq", [(1, 32), (2, 32), (2, 16), (2, 8)])
 @pytest.mark.parametrize("case", [([45], [45]), ([300, 17], [300, 17]), ([700, 64], [100, 64]), ([4096], [1000]),
-                                  ([129, 1], [65, 1])])
+                                  ([129, 1], [65, 1]), ([2048], [2048])])
 def test_paged_attention_prefill(gpu, case, mode, hq):
-    """mode 1: decode-style kernel on 16-query tiles; mode 2: flash prefill on 64-query tiles (G = hq / 8)."""
+    """mode 1: decode-style kernel on 16-query tiles; mode 2: flash prefill on 64-query tiles (G = hq / 8; the
+    small cases split a kv head's q heads over workgroups (HG < G), [2048] keeps them in one (256 workgroups))."""
     ctxs, qlens = case
     g = torch.Generator().manual_seed(sum(ctxs) + hq)
     B = len(ctxs)

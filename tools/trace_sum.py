@@ -21,7 +21,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--div", type=float, default=1.0)
     ap.add_argument("--top", type=int, default=30)
-    ap.add_argument("--skip", default=r"normal_|uniform_|random_|fill_|distribution")
+    ap.add_argument("--skip", default=r"normal_kernel|uniform_kernel|random_|FillFunctor|distribution_")
     ap.add_argument("--after-kernel", default="")
     ap.add_argument("--title", default="")
     args = ap.parse_args()
