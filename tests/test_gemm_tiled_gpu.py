@@ -40,7 +40,7 @@ def _ref(x, wt):
     return x.float() @ R.untile_weight(wt).float().t()
 
 
-@pytest.mark.parametrize("M", [192, 256, 2048, 8192, 1000])
+@pytest.mark.parametrize("M", [129, 192, 200, 256, 512, 2048, 8192, 1000])
 def test_tiled_store_and_resid(gpu, M):
     g = torch.Generator().manual_seed(M)
     x = _rand((M, H), g, gpu)
@@ -60,7 +60,7 @@ def test_tiled_store_and_resid(gpu, M):
     _check(r, r0 + _ref(h, wd), f"down resid M={M}", rel=2e-3)
 
 
-@pytest.mark.parametrize("M", [256, 2048, 4100])
+@pytest.mark.parametrize("M", [129, 192, 200, 256, 2048, 4100])
 def test_tiled_silu_gate_up(gpu, M):
     g = torch.Generator().manual_seed(M + 1)
     x = _rand((M, H), g, gpu)
@@ -94,7 +94,8 @@ def test_tiled_qkv_rope_kv_write(gpu, M):
     _check(vc.cpu(), vr, "v cache", rel=2e-2)
 
 
-@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("2", "4"), ("4", "1"), ("4", "2")])
+@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("2", "4"), ("4", "1"), ("4", "2"), ("5", "1"), ("5", "2"),
+                                       ("6", "1"), ("7", "2")])
 def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     monkeypatch.setenv("DSSE_T_CFG", cfg)
     monkeypatch.setenv("DSSE_T_SPLIT", split)
@@ -102,7 +103,7 @@ def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     g = torch.Generator().manual_seed(int(cfg) * 10 + int(split))
     for M in (1, 70, 256, 600):
         x = _rand((M, 2048), g, gpu)
-        w = R.tile_weight(_rand((1024 if cfg != "4" else 1536, 2048), g, gpu, 1 / 45))
+        w = R.tile_weight(_rand((1024 if cfg not in ("4", "6", "7") else 1536, 2048), g, gpu, 1 / 45))
         out = torch.empty(M, w.shape[0], device=gpu)
         ops.gemm_out(x, w, out)
         _check(out, _ref(x, w), f"cfg {cfg} split {split} M={M}", rel=2e-3)
