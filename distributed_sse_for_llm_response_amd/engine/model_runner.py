@@ -107,6 +107,27 @@ def prefill_lib_enabled(dev) -> bool:
     return torch.device(dev).type == "cuda" and os.environ.get("DSSE_PREFILL_LIB", "1") != "0"
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "tunableop_gfx950.csv")
+
+
+def load_tuned_gemms() -> bool:
+    """The library projections' best solution per shape (PyTorch TunableOp results, tuned on MI355X with this image's
+    torch / hipBLASLt / rocBLAS by tools/bench_tunable.py: 3-17 % faster than the default heuristic for most prefill
+    shapes, entries that tuned slower dropped; profiles/r4/prefill_lib_r4.md).  Tuning itself stays off: a shape not in
+    the file uses the library default, and nothing is benchmarked at serving time.  Process-wide; the file's
+    validators (torch / HIP / library versions, gfx arch) must match or it is ignored.  DSSE_TUNABLEOP=0 disables."""
+    path = os.environ.get("DSSE_TUNABLEOP_FILE", TUNED_GEMMS)
+    if os.environ.get("DSSE_TUNABLEOP", "1") == "0" or not os.path.exists(path):
+        return False
+    tun = torch.cuda.tunable
+    tun.tuning_enable(False)
+    tun.set_filename(path)
+    if not tun.read_file(path):
+        return False
+    tun.enable(True)
+    return True
+
+
 # decode buckets run on the persistent MLP kernel (rows <= 64; smaller buckets keep the launch-per-op path unless
 # DSSE_MEGA_MIN_B lowers the bound)
 MEGA_MIN_B = int(os.environ.get("DSSE_MEGA_MIN_B", "33"))
@@ -230,6 +251,7 @@ class ModelRunner:
         self._gu = None
         if self.lib:
             attach_library(w)
+            load_tuned_gemms()
             # [rows, 2F] gate / up product of the library path, allocated once (captured graphs hold its address):
             # a pass with more rows than this runs gate_up on the tiled kernel instead
             self._gu = torch.empty(max(max_prefill_tokens, Bm + 2048), 2 * F, **bf)
