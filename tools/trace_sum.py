@@ -1,12 +1,13 @@
 """Per-kernel totals from a rocprofv3 `--kernel-trace --output-format csv` run (run_kernel_trace.csv).
 
     python tools/trace_sum.py gpurun_out/x/prof/run_kernel_trace.csv --div 3 [--after-kernel flash_prefill]
-        [--skip 'normal_|uniform_|fill_'] [--top 30]
+        [--skip 'normal_|uniform_|fill_'] [--top 30] [--unit-kernel decode_prep --last 6 [--skip-last 20]]
 
 Groups dispatches by (kernel, grid), divides by --div (e.g. the number of timed prefills) and prints a markdown
 table, heaviest first.  --skip drops kernels by regex (the random weight initialisation of a benchmark's setup, torch
 fills); --after-kernel drops every dispatch before the first one whose name matches (the setup and warm-up), so the
-table is the steady-state work only.
+table is the steady-state work only; --unit-kernel R --last N keeps the last N units (each starting at a dispatch
+matching R, e.g. the last 6 decode steps) and divides by N.
 """
 from __future__ import annotations
 
@@ -24,12 +25,23 @@ def main():
     ap.add_argument("--skip", default=r"normal_kernel|uniform_kernel|random_|FillFunctor|distribution_")
     ap.add_argument("--after-kernel", default="")
     ap.add_argument("--title", default="")
+    ap.add_argument("--unit-kernel", default="",
+                    help="with --last: a unit starts at each dispatch matching this regex (e.g. decode_prep)")
+    ap.add_argument("--last", type=int, default=0, help="keep only the last N complete units (sets --div to N)")
+    ap.add_argument("--skip-last", type=int, default=0, help="with --last: ... that end this many units before the end")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.csv, newline="")), key=lambda r: int(r["Start_Timestamp"]))
     if args.after_kernel:
         pat = re.compile(args.after_kernel)
         first = next((i for i, r in enumerate(rows) if pat.search(r["Kernel_Name"])), 0)
         rows = rows[first:]
+    if args.unit_kernel and args.last:
+        pat = re.compile(args.unit_kernel)
+        starts = [i for i, r in enumerate(rows) if pat.search(r["Kernel_Name"])]
+        k = args.skip_last
+        if len(starts) > args.last + k:
+            rows = rows[starts[-args.last - 1 - k]:starts[-1 - k]]
+            args.div = float(args.last)
     skip = re.compile(args.skip) if args.skip else None
     per = collections.defaultdict(lambda: [0, 0.0])
     total = 0.0
