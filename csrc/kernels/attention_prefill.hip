@@ -110,21 +110,51 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
   // last are issued too (pages clamp to the context, nobody reads them): a branch around the DMA made the
   // compiler's waitcnt placement drain every load in flight.
   constexpr int IPW = 32 / NW;
-  auto issue_block = [&](int j, int slot) {
-    const int blk0 = page_block(bt, 2 * j, npages, p), blk1 = page_block(bt, 2 * j + 1, npages, p);
+  // Lane-constant parts of the DMA sources (element offsets inside a page block of this kv head) and, for the Vᵀ
+  // pieces, which of the block's two pages the lane's chunk comes from: per block only the two page bases change
+  // (scalar), so a piece costs a select and one 64-bit add instead of a per-lane 64-bit multiply-add.
+  uint32_t loff[IPW];
+  bool vhi[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int q = w * IPW + i;  // wave-uniform
+    if (q < 16) {
+      const int key = 4 * q + (lane >> 4), c = (lane & 15) ^ swz(key & 15);
+      loff[i] = (key & 31) * kD + 8 * c;
+      vhi[i] = false;
+    } else {
+      const int d = 8 * (q - 16) + (lane >> 3), c = (lane & 7) ^ ((d >> 1) & 7);
+      loff[i] = d * kBS + 8 * (c & 3);
+      vhi[i] = c >= 4;
+    }
+  }
+  const size_t pstride = (size_t)p.hkv * kBS * kD;  // elements per page block (all kv heads)
+  const bf16* kh = p.k_cache + (size_t)h * kBS * kD;
+  const bf16* vh = p.v_cache + (size_t)h * kD * kBS;
+  // Page-table entries are read one block ahead: the scalar load of block j + 1's pages is in flight while block j
+  // is issued and retired by the next LDS wait, not by a dependent wait in front of this block's DMA.
+  int pg0 = page_block(bt, 0, npages, p), pg1 = page_block(bt, 1, npages, p);
+  int jn = 0;  // next block to issue (blocks are issued in order)
+  // (the page bases are pinned in SGPR pairs: left to itself the compiler folds the per-lane select of two bases into
+  // a per-lane select of the page index followed by a per-lane 64-bit multiply)
+  auto sbase = [&](const bf16* head, int blk) {
+    uint64_t u = reinterpret_cast<uint64_t>(head + (size_t)blk * pstride);
+    asm volatile("" : "+s"(u));
+    return u;
+  };
+  auto issue_block = [&](int slot) {
+    const int blk0 = pg0, blk1 = pg1;
+    ++jn;
+    pg0 = page_block(bt, 2 * jn, npages, p);
+    pg1 = page_block(bt, 2 * jn + 1, npages, p);
     char* base = smem + slot * kStage;
+    const bool kpiece = w * IPW < 16;  // wave-uniform: a wave's pieces are all K or all Vᵀ (IPW divides 16)
+    const uint64_t b0 = sbase(kpiece ? kh : vh, blk0), b1 = sbase(kpiece ? kh : vh, blk1);
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const int q = w * IPW + i;  // wave-uniform
-      const bf16* src;
-      if (q < 16) {
-        const int key = 4 * q + (lane >> 4), c = (lane & 15) ^ swz(key & 15);
-        src = p.k_cache + (((size_t)(q >= 8 ? blk1 : blk0) * p.hkv + h) * kBS + (key & 31)) * kD + 8 * c;
-      } else {
-        const int d = 8 * (q - 16) + (lane >> 3), c = (lane & 7) ^ ((d >> 1) & 7);
-        src = p.v_cache + (((size_t)(c >= 4 ? blk1 : blk0) * p.hkv + h) * kD + d) * kBS + 8 * (c & 3);
-      }
-      glds16(src, base + q * 1024);
+      const uint64_t b = kpiece ? (q >= 8 ? b1 : b0) : (vhi[i] ? b1 : b0);
+      glds16(reinterpret_cast<const bf16*>(b + 2ull * loff[i]), base + q * 1024);
     }
   };
 
@@ -273,9 +303,9 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
   // softmax/PV(j), which for the lagging half is absolute barrier 2(j + 1), the lagging half needs block j + 1
   // with blocks up to j + 2 issued (wait: all but the youngest).
   const bool lag = wq == 1;
-  issue_block(0, 0);
-  issue_block(1, 1);
-  issue_block(2, 2);
+  issue_block(0);
+  issue_block(1);
+  issue_block(2);
   if (lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
   // unrolled by the ring size: each block's LDS slot is a compile-time offset (no per-read address arithmetic)
   for (int j0 = 0; j0 < nblk; j0 += kRing) {
@@ -289,7 +319,7 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
         if (vis) qk(k);
         if (!lag) asm volatile("s_barrier" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(IPW) : "memory");
-        issue_block(j + 3, (k + 3) % kRing);
+        issue_block((k + 3) % kRing);  // block j + 3
         if (vis) sm_pv(j, k);
       }
     }
