@@ -97,61 +97,48 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
 // ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
 // qkv: [T, (hq + 2 hkv) * 128] bf16 in the engine's permuted column order (inside each 16-column
 // tile j of a head: columns 0..7 = dims 8j..8j+7, columns 8..15 = dims 64+8j..64+8j+7).
-// One workgroup per token; a thread rotates 8 pairs of one (unit, tile j) with 16-byte loads and stores,
-// or moves 8 V columns into the transposed, token-permuted V page.
-__global__ void __launch_bounds__(256)
-rope_kv_write_kernel(const bf16* __restrict__ qkv, int hq, int hkv, const int* __restrict__ positions,
-                     const int* __restrict__ slots, const float2* __restrict__ rope,
-                     bf16* __restrict__ q_out, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
-                     int num_slots, int rope_len) {
-  const int t = blockIdx.x;
+// A token's rows: each thread rotates 8 pairs of one (unit, tile j) with 16-byte loads and stores.
+DEV void rope_kv_rows(const bf16* __restrict__ qkv, int hq, int hkv, const int* __restrict__ positions,
+                      const int* __restrict__ slots, const float2* __restrict__ rope, bf16* __restrict__ q_out,
+                      bf16* __restrict__ k_cache, int num_slots, int rope_len, int t) {
   const int ncols = (hq + 2 * hkv) * 128;
   const bf16* row = qkv + (size_t)t * ncols;
   const int pos = DSSE_IDX(positions[t], rope_len, 0);
   const int slot = slots[t] < 0 ? -1 : DSSE_IDX(slots[t], num_slots, -1);
   const int blk = slot >= 0 ? slot / kPageTok : 0, off = slot >= 0 ? slot % kPageTok : 0;
-  const int nrot = (hq + hkv) * 8, nv = 0;  // V: v_page_write_kernel
-  for (int idx = threadIdx.x; idx < nrot + nv; idx += blockDim.x) {
-    if (idx < nrot) {
-      const int u = idx >> 3, j = idx & 7;
-      bf16* dst = u < hq ? q_out + ((size_t)t * hq + u) * 128
-                         : (slot >= 0 ? k_cache + (((size_t)blk * hkv + (u - hq)) * kPageTok + off) * 128 : nullptr);
-      if (dst == nullptr) continue;
-      const bf16x8 x1 = ld_bf16x8(row + u * 128 + 16 * j);
-      const bf16x8 x2 = ld_bf16x8(row + u * 128 + 16 * j + 8);
-      const float4* cs4 = reinterpret_cast<const float4*>(rope + (size_t)pos * 64 + 8 * j);
-      bf16x8 o1, o2;
+  const int nrot = (hq + hkv) * 8;  // q and k heads x 8 column tiles (V: v_page_write)
+  for (int idx = threadIdx.x; idx < nrot; idx += blockDim.x) {
+    const int u = idx >> 3, j = idx & 7;
+    bf16* dst = u < hq ? q_out + ((size_t)t * hq + u) * 128
+                       : (slot >= 0 ? k_cache + (((size_t)blk * hkv + (u - hq)) * kPageTok + off) * 128 : nullptr);
+    if (dst == nullptr) continue;
+    const bf16x8 x1 = ld_bf16x8(row + u * 128 + 16 * j);
+    const bf16x8 x2 = ld_bf16x8(row + u * 128 + 16 * j + 8);
+    const float4* cs4 = reinterpret_cast<const float4*>(rope + (size_t)pos * 64 + 8 * j);
+    bf16x8 o1, o2;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float4 cs = cs4[e];  // (cos, sin) of pairs 2e and 2e + 1
-        const float a0 = bf2f(x1[2 * e]), b0 = bf2f(x2[2 * e]), a1 = bf2f(x1[2 * e + 1]), b1 = bf2f(x2[2 * e + 1]);
-        o1[2 * e] = f2bf(a0 * cs.x - b0 * cs.y);
-        o2[2 * e] = f2bf(b0 * cs.x + a0 * cs.y);
-        o1[2 * e + 1] = f2bf(a1 * cs.z - b1 * cs.w);
-        o2[2 * e + 1] = f2bf(b1 * cs.z + a1 * cs.w);
-      }
-      *reinterpret_cast<bf16x8*>(dst + 8 * j) = o1;
-      *reinterpret_cast<bf16x8*>(dst + 64 + 8 * j) = o2;
-    } else {
-      const int vi = idx - nrot, h = vi >> 4, j = (vi >> 1) & 7, half = vi & 1;
-      const bf16x8 v = ld_bf16x8(row + (hq + hkv + h) * 128 + 16 * j + 8 * half);
-      bf16* vp = v_cache + (((size_t)blk * hkv + h) * 128 + (half ? 64 : 0) + 8 * j) * kPageTok + vperm_tok(off);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vp[(size_t)e * kPageTok] = v[e];
+    for (int e = 0; e < 4; ++e) {
+      const float4 cs = cs4[e];  // (cos, sin) of pairs 2e and 2e + 1
+      const float a0 = bf2f(x1[2 * e]), b0 = bf2f(x2[2 * e]), a1 = bf2f(x1[2 * e + 1]), b1 = bf2f(x2[2 * e + 1]);
+      o1[2 * e] = f2bf(a0 * cs.x - b0 * cs.y);
+      o2[2 * e] = f2bf(b0 * cs.x + a0 * cs.y);
+      o1[2 * e + 1] = f2bf(a1 * cs.z - b1 * cs.w);
+      o2[2 * e + 1] = f2bf(b1 * cs.z + a1 * cs.w);
     }
+    *reinterpret_cast<bf16x8*>(dst + 8 * j) = o1;
+    *reinterpret_cast<bf16x8*>(dst + 64 + 8 * j) = o2;
   }
 }
 
 // ---- V into the transposed, token-permuted pages, a page row at a time -----------------------------------------
-// The per-token form (rope_kv_write_kernel's V branch) writes 2 bytes per (token, d): 128 scattered stores per head
-// per token.  Here a workgroup takes 32 consecutive rows x one kv head; thread d gathers its 32 values (coalesced
+// A per-token form writes 2 bytes per (token, d): 128 scattered stores per head per token.  Here 128 threads take
+// 32 consecutive rows x one kv head; thread d gathers its 32 values (coalesced
 // over d) and, when the 32 rows fill one whole page in order (prefill of a page-aligned run), writes the page's row
 // d as 4 x 16-byte stores in the vperm token order.  Other groups (page boundaries, padding, scattered slots) fall
 // back to per-element stores.
-__global__ void __launch_bounds__(128)
-v_page_write_kernel(const bf16* __restrict__ qkv, int T, int hq, int hkv, const int* __restrict__ slots,
-                    bf16* __restrict__ v_cache, int num_slots) {
-  const int t0 = blockIdx.x * kPageTok, h = blockIdx.y, d = threadIdx.x;
+// (rows t0 .. t0 + 31, kv head h, dim d = the thread's index in its 128-thread half; a wave never spans two heads)
+DEV void v_page_write(const bf16* __restrict__ qkv, int T, int hq, int hkv, const int* __restrict__ slots,
+                      bf16* __restrict__ v_cache, int num_slots, int t0, int h, int d) {
   const int ncols = (hq + 2 * hkv) * 128;
   const int lane = threadIdx.x & 63;
   const int tl = t0 + (lane & 31);
@@ -179,6 +166,22 @@ v_page_write_kernel(const bf16* __restrict__ qkv, int T, int hq, int hkv, const 
     if (sl < 0) continue;
     v_cache[(((size_t)(sl / kPageTok) * hkv + h) * 128 + d) * kPageTok + vperm_tok(sl % kPageTok)] = src[(size_t)i * ncols];
   }
+}
+
+// One launch for both: blocks [0, T) rotate q / k of one token each (rope_kv_rows), the blocks after
+// them write V page rows, two kv heads per 256-thread block.
+__global__ void __launch_bounds__(256)
+rope_kv_v_kernel(const bf16* __restrict__ qkv, int T, int hq, int hkv, const int* __restrict__ positions,
+                 const int* __restrict__ slots, const float2* __restrict__ rope, bf16* __restrict__ q_out,
+                 bf16* __restrict__ k_cache, bf16* __restrict__ v_cache, int num_slots, int rope_len) {
+  if ((int)blockIdx.x < T) {
+    rope_kv_rows(qkv, hq, hkv, positions, slots, rope, q_out, k_cache, num_slots, rope_len, blockIdx.x);
+    return;
+  }
+  const int vb = blockIdx.x - T, hpairs = (hkv + 1) / 2;
+  const int h = 2 * (vb % hpairs) + (threadIdx.x >> 7);
+  if (h >= hkv) return;  // wave-uniform (128-thread halves)
+  v_page_write(qkv, T, hq, hkv, slots, v_cache, num_slots, (vb / hpairs) * kPageTok, h, threadIdx.x & 127);
 }
 
 // ---- SiLU·mul over the interleaved gate/up output of a library GEMM (prefill) ---------------
@@ -252,12 +255,10 @@ extern "C" hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv
                                          void* k_cache, void* v_cache, int num_slots, int rope_len,
                                          hipStream_t st) {
   if (T <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rope_kv_write_kernel, dim3(T), dim3(256), 0, st,
-                     reinterpret_cast<const bf16*>(qkv), hq, hkv, positions, slots, rope,
-                     reinterpret_cast<bf16*>(q_out), reinterpret_cast<bf16*>(k_cache),
+  const int vblocks = (T + kPageTok - 1) / kPageTok * ((hkv + 1) / 2);
+  hipLaunchKernelGGL(rope_kv_v_kernel, dim3(T + vblocks), dim3(256), 0, st, reinterpret_cast<const bf16*>(qkv), T,
+                     hq, hkv, positions, slots, rope, reinterpret_cast<bf16*>(q_out), reinterpret_cast<bf16*>(k_cache),
                      reinterpret_cast<bf16*>(v_cache), num_slots, rope_len);
-  hipLaunchKernelGGL(v_page_write_kernel, dim3((T + kPageTok - 1) / kPageTok, hkv), dim3(128), 0, st,
-                     reinterpret_cast<const bf16*>(qkv), T, hq, hkv, slots, reinterpret_cast<bf16*>(v_cache), num_slots);
   return hipGetLastError();
 }
 

@@ -102,6 +102,10 @@ def prefill_row_chunks(T: int, tp: int) -> list:
 LIB_MIN_ROWS = {"qkv": 512, "o": 512, "gate_up": 256, "down": 1024}
 
 
+# prompt passes up to this many rows send the residual projections' split-K slabs to the norm (_prefill_resid)
+PREFILL_SLAB_ROWS = 512
+
+
 def prefill_lib_enabled(dev) -> bool:
     """DSSE_PREFILL_LIB=0: every projection on the tiled kernels (and no 14.5 GB of row-major copies)."""
     return torch.device(dev).type == "cuda" and os.environ.get("DSSE_PREFILL_LIB", "1") != "0"
@@ -222,7 +226,11 @@ class ModelRunner:
         self.h = torch.zeros(Bm, F, **bf)
         self.tmp = torch.zeros(Bm, H, **bf)
         # fp32 split-K slabs of the residual projections (reduced inside the next RMSNorm)
-        self.split_part = torch.zeros(32 * Bm * H, device=dev, dtype=torch.float32)
+        # (on a GPU also large enough for the 8 slabs of a PREFILL_SLAB_ROWS-row prompt pass: _prefill_resid)
+        slab_floats = 32 * Bm * H
+        if torch.device(dev).type == "cuda":
+            slab_floats = max(slab_floats, 8 * min(PREFILL_SLAB_ROWS, max_prefill_tokens) * H)
+        self.split_part = torch.zeros(slab_floats, device=dev, dtype=torch.float32)
         self.health = torch.zeros(4, device=dev, dtype=torch.int32)
         self.mega_reason = mega_reason(self)
         self.mega = not self.mega_reason and Bm >= MEGA_MIN_B
@@ -648,7 +656,14 @@ class ModelRunner:
     def _prefill_resid(self, a, wt, resid, norm_w, x, tmp, ws=None, kind: str = "o") -> None:
         """resid += a·wᵀ, x = RMSNorm(resid).  Thousands of rows: the product goes out as a bf16 tile (row-contiguous
         stores) and the norm kernel adds it -- the fused fp32 read-modify-write epilogue measured +120 us per
-        8192-row projection (profiles/r2/prefill_kernels_8k.md)."""
+        8192-row projection (profiles/r2/prefill_kernels_8k.md).  Up to PREFILL_SLAB_ROWS rows on the tiled kernels
+        (split K) the norm reduces the fp32 split-K slabs itself, as in decode: no reduce launch, no bf16 round trip."""
+        rows = a.shape[0]
+        lib = self.lib and ws is not None and rows >= LIB_MIN_ROWS[kind]
+        if self.comm.size == 1 and not lib and rows <= PREFILL_SLAB_ROWS and self.split_part.numel() >= 8 * rows * wt.shape[0]:
+            ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
+            ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, part=self.split_part, nsplit=ns)
+            return
         self._proj(a, wt, ws, tmp, kind)
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
