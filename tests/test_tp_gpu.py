@@ -16,6 +16,9 @@ pytestmark = pytest.mark.gpu
 
 PROMPTS = [[5, 17, 99, 3, 8, 1000, 42], list(range(100, 150)), [7] * 33]
 BTS = [[0, 1, 2], [10, 4, 5, 6], [20, 21, 22]]
+# longer prompts (217 prefill rows) for the chunked, overlapped TP prefill (DSSE_TP_PREFILL_OVERLAP_MIN lowered)
+PROMPTS_LONG = [list(range(3, 93)), list(range(200, 290)), [7] * 37]
+BTS_LONG = [[0, 1, 2, 3], [10, 4, 5, 6], [20, 21]]
 STEPS = 6
 
 
@@ -29,7 +32,7 @@ def _cfg(name):
                          num_layers=2, num_heads=16, num_kv_heads=8, max_position=4096)
 
 
-def _generate(rank, world, device, cfg=SMALL):
+def _generate(rank, world, device, cfg=SMALL, prompts=PROMPTS, bts=BTS):
     from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner, PrefillSeq
     from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
     from distributed_sse_for_llm_response_amd.parallel.comm import TPComm
@@ -38,10 +41,10 @@ def _generate(rank, world, device, cfg=SMALL):
     comm = TPComm(rank=rank, size=world, group=None) if world > 1 else TPComm()
     w = convert_standard(cfg, std, tp_rank=rank, tp_size=world, device=device)
     r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device=device, comm=comm, use_graphs=False)
-    for i, bt in enumerate(BTS):
+    for i, bt in enumerate(bts):
         r.block_tables[i, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
     r.temperature[:3] = 0.0
-    r.prefill([PrefillSeq(i, p, 0, BTS[i], True) for i, p in enumerate(PROMPTS)], ring_row=0)
+    r.prefill([PrefillSeq(i, p, 0, bts[i], True) for i, p in enumerate(prompts)], ring_row=0)
     r.active[:3] = 1
     gen = [[int(r.ids[i])] for i in range(3)]
     for _ in range(STEPS):
@@ -51,19 +54,19 @@ def _generate(rank, world, device, cfg=SMALL):
     return gen
 
 
-def _worker(rank, world, port, out, cfg_name="small"):
+def _worker(rank, world, port, out, cfg_name="small", long=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if long:
+        os.environ.update(DSSE_TP_PREFILL_OVERLAP_MIN="64", DSSE_TP_PREFILL_CHUNKS="4")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out[rank] = _generate(rank, world, torch.device("cuda", 0), _cfg(cfg_name))
+        prompts, bts = (PROMPTS_LONG, BTS_LONG) if long else (PROMPTS, BTS)
+        out[rank] = _generate(rank, world, torch.device("cuda", 0), _cfg(cfg_name), prompts, bts)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,cfg_name", [(2, "small"), (4, "small"), (8, "tp8")])
-def test_tp_on_gpu_kernels_matches_reference(world, cfg_name):
-    """TP = 2 / 4 / 8 ranks time-sharing the one GPU (8 ranks: one KV head and a 1/8 vocab shard each)."""
+def _run(world, cfg_name, long=False):
     import socket
 
     s = socket.socket()
@@ -73,16 +76,34 @@ def test_tp_on_gpu_kernels_matches_reference(world, cfg_name):
     ctx = mp.get_context("spawn")
     with ctx.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, port, out, cfg_name), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, out, cfg_name, long), nprocs=world, join=True)
         res = [out[r] for r in range(world)]
     assert all(r == res[0] for r in res), "TP ranks disagree on the sampled tokens"
     cfg = _cfg(cfg_name)
     std = init_standard_weights(cfg, seed=3)
+    prompts = PROMPTS_LONG if long else PROMPTS
     worst = 0.0
     for i in range(3):
-        logits, _ = reference_forward(cfg, std, torch.tensor(PROMPTS[i] + res[0][i]))
-        L = len(PROMPTS[i])
+        logits, _ = reference_forward(cfg, std, torch.tensor(prompts[i] + res[0][i]))
+        L = len(prompts[i])
         for j, g in enumerate(res[0][i]):
             row = logits[L - 1 + j]
             worst = max(worst, float(row.max() - row[g]))
     assert worst < 0.15, worst
+    return res[0]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,cfg_name", [(2, "small"), (4, "small"), (8, "tp8")])
+def test_tp_on_gpu_kernels_matches_reference(world, cfg_name):
+    """TP = 2 / 4 / 8 ranks time-sharing the one GPU (8 ranks: one KV head and a 1/8 vocab shard each)."""
+    _run(world, cfg_name)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_chunked_prefill_on_gpu_kernels_matches_reference(world):
+    """The row-chunked TP prefill (prefill_row_chunks: 4 chunks, each chunk's all-reduces issued as soon as its GEMM
+    is done) over 2 / 4 ranks on the GPU kernels: ranks agree and every greedy token stays within bf16 tolerance of
+    the fp32 reference (TP-vs-TP1 bit equality of the chunked path: tests/test_tp_cpu.py, fp32 on the CPU)."""
+    _run(world, "small", long=True)

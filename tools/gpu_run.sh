@@ -32,6 +32,7 @@ for s in "$@"; do
     mega_test) step mega_test 300 $PYT tests/test_mega_gpu.py ;;
     mega_bench) step mega_bench 300 python -u tools/bench_mega.py --M 64 ;;
     mega_stamps) step mega_stamps 300 python -u tools/bench_mega.py --M 64 --qkv --stamps ;;
+    tp_test) step tp_test 600 $PYT tests/test_tp_gpu.py ;;
     model_test) step model_test 600 $PYT tests/test_model_full_dims_gpu.py ;;
     ar_test) step ar_test 900 $PYT tests/test_custom_ar_gpu.py ;;
     gpu_tests) step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
