@@ -57,6 +57,7 @@ for s in "$@"; do
     c3stub) HIP_VISIBLE_DEVICES= DSSE_DIST_BACKEND=gloo step c3stub 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 8 --streams 256 --steps 64 --warmup 8 --stub-step-ms 9.7 ;;
     serving13) step serving13 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0,2 ;;
     serving13b) step serving13b 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 256,512 --itl-ratios 0 ;;
+    overlap) step overlap 600 python3 tools/bench_overlap.py --streams 128 --ctx 512 --prompt 512 && step overlap64 600 python3 tools/bench_overlap.py --streams 64 --ctx 512 --prompt 512 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
     tunable) step tunable 900 python -u tools/bench_tunable.py --M 8192,4096,2048,1024,512,256,320 --out "$out/tunableop_results.csv" ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
