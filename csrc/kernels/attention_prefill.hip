@@ -23,6 +23,10 @@
 // MFMAs: the SIMD sees MFMA work from one wave under the other's exp / max / convert chain.  The round-1..3 form
 // (all waves in lockstep, one barrier per two blocks) measured MFMA busy 22 %, 34 % of wave time waiting on
 // dependencies (profiles/pmc_flash_prefill_r1.md): both waves of a SIMD reached their softmax at the same time.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "api.h"
 
 namespace dsse {
@@ -57,8 +61,12 @@ DEV int page_block(const int* bt, int pg, int npages, const AttnParams& p) {
 // G = q heads per kv head; HG = the q heads one workgroup takes (HG < G splits a kv head's q heads over G / HG
 // workgroups: short prompts, where one workgroup per (tile, kv head) leaves most CUs idle -- a 512-token prompt is 64
 // workgroups; each then stages its K/V itself, which the L2 serves)
-template <int G, int HG>
-__global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
+// STAMP (diagnostic build, DSSE_FLASH_STAMPS): every wave of the first kStampWgs workgroups records the shader clock at
+// six points of each key block (before / after the barrier in front of QKᵀ, before / after the barrier in front of
+// softmax + PV, after the DMA issue, after the softmax) into 24 KiB of LDS past the ring, copied to `stamps` at the end; tools/flash_stamps.py reads them.
+constexpr int kStampBlocks = 128, kStampWgs = 32, kStampsPerBlock = 6;
+template <int G, int HG, bool STAMP>
+__global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, unsigned* stamps) {
   constexpr int NW = 2 * HG;
   constexpr int NSPLIT = G / HG;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // kRing blocks of kStage
@@ -178,6 +186,12 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) vofs[t] = kKBytes + r * 128 + (((4 * t + g) ^ ((r >> 1) & 7)) << 4);
 
+  unsigned* st_lds = reinterpret_cast<unsigned*>(smem + kRing * kStage) + w * kStampsPerBlock * kStampBlocks;
+  auto stamp = [&](int j, int i) {
+    if constexpr (STAMP) {
+      if (lane == 0 && j < kStampBlocks) st_lds[kStampsPerBlock * j + i] = (unsigned)__builtin_amdgcn_s_memtime();
+    }
+  };
   // phase 1: Sᵀ = K·Qᵀ of the block in LDS slot `buf`; a key tile's 4 fragments are read one tile ahead
   auto qk = [&](int buf) {
     const char* kb = smem + buf * kStage;
@@ -274,6 +288,7 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
           pf[qt][t][4 + i] = f2bf(s4[2 * t + 1][qt][i]);
         }
     }
+    stamp(j, 5);
     // Oᵀ[d tile][query tile] += Vᵀ · Pᵀ: the 8 fragments of a page read before its 16 MFMAs
     const char* vb0 = smem + buf * kStage;
     __builtin_amdgcn_s_setprio(1);
@@ -314,18 +329,30 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
       const int j = j0 + k;
       if (j < nblk) {
         const bool vis = j * kBK <= w_last_pos;  // this wave sees at least one key of the block
+        stamp(j, 0);
         if (!lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
         else asm volatile("s_barrier" ::: "memory");
+        stamp(j, 1);
         if (vis) qk(k);
+        stamp(j, 2);
         if (!lag) asm volatile("s_barrier" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(IPW) : "memory");
+        stamp(j, 3);
         issue_block((k + 3) % kRing);  // block j + 3
+        stamp(j, 4);
         if (vis) sm_pv(j, k);
       }
     }
   }
   if (!lag) asm volatile("s_barrier" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may still write this workgroup's LDS after it exits
+  if constexpr (STAMP) {
+    if (blockIdx.x < kStampWgs) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stamp writes have landed
+      unsigned* dst = stamps + ((size_t)blockIdx.x * NW + w) * kStampsPerBlock * kStampBlocks;
+      for (int i = lane; i < kStampsPerBlock * kStampBlocks; i += 64) dst[i] = i < kStampsPerBlock * nblk ? st_lds[i] : 0u;
+    }
+  }
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
 #pragma unroll
@@ -350,18 +377,41 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p) {
 }  // namespace dsse
 
 namespace {
-template <int G, int HG>
-hipError_t launch_flash(int num_work, const dsse::AttnParams* p, hipStream_t st) {
+template <int G, int HG, bool STAMP>
+hipError_t launch_flash(int num_work, const dsse::AttnParams* p, hipStream_t st, unsigned* stamps) {
   using namespace dsse;
-  constexpr int lds = kRing * kStage;
+  constexpr int lds = kRing * kStage + (STAMP ? 2 * HG * kStampsPerBlock * kStampBlocks * 4 : 0);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<G, HG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_prefill_kernel<G, HG, STAMP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((flash_prefill_kernel<G, HG>), dim3(num_work * p->hkv * (G / HG)), dim3(128 * HG), lds, st, *p);
+  hipLaunchKernelGGL((flash_prefill_kernel<G, HG, STAMP>), dim3(num_work * p->hkv * (G / HG)), dim3(128 * HG), lds, st,
+                     *p, stamps);
   return hipGetLastError();
+}
+
+// DSSE_FLASH_STAMPS=<file>: the diagnostic build of the kernel; after each call the stamps of the first kStampWgs
+// workgroups ([wg][wave][block][6] u32 shader-clock values) overwrite <file> (synchronises the device: never set it in
+// serving)
+hipError_t launch_stamped(int num_work, const dsse::AttnParams* p, hipStream_t st, const char* path) {
+  using namespace dsse;
+  if (p->group != 4) return hipErrorInvalidValue;
+  const size_t n = (size_t)kStampWgs * 8 * kStampsPerBlock * kStampBlocks;
+  static unsigned* buf = nullptr;
+  if (buf == nullptr && hipMalloc(&buf, n * sizeof(unsigned)) != hipSuccess) return hipErrorOutOfMemory;
+  (void)hipMemsetAsync(buf, 0, n * sizeof(unsigned), st);
+  hipError_t e = launch_flash<4, 4, true>(num_work, p, st, buf);
+  if (e != hipSuccess) return e;
+  std::vector<unsigned> host(n);
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  if ((e = hipMemcpy(host.data(), buf, n * sizeof(unsigned), hipMemcpyDeviceToHost)) != hipSuccess) return e;
+  if (FILE* f = fopen(path, "wb")) {
+    fwrite(host.data(), sizeof(unsigned), n, f);
+    fclose(f);
+  }
+  return hipSuccess;
 }
 }  // namespace
 
@@ -370,10 +420,12 @@ hipError_t launch_flash(int num_work, const dsse::AttnParams* p, hipStream_t st)
 // 2 waves instead of 64 of 8 at 512 tokens -- measured 38.9 vs 28.8 us and was dropped; profiles/r4.)
 extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
   if (num_work <= 0) return hipSuccess;
+  static const char* stamps = getenv("DSSE_FLASH_STAMPS");
+  if (stamps != nullptr && stamps[0] != '\0') return launch_stamped(num_work, p, st, stamps);
   switch (p->group) {
-    case 1: return launch_flash<1, 1>(num_work, p, st);
-    case 2: return launch_flash<2, 2>(num_work, p, st);
-    case 4: return launch_flash<4, 4>(num_work, p, st);
+    case 1: return launch_flash<1, 1, false>(num_work, p, st, nullptr);
+    case 2: return launch_flash<2, 2, false>(num_work, p, st, nullptr);
+    case 4: return launch_flash<4, 4, false>(num_work, p, st, nullptr);
     default: return hipErrorInvalidValue;
   }
 }

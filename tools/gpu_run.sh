@@ -66,6 +66,8 @@ for s in "$@"; do
     tunable) step tunable 900 python -u tools/bench_tunable.py --M 8192,4096,2048,1024,512,256,320 --out "$out/tunableop_results.csv" ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill or rope_kv" ;;
+    flash_stamps) DSSE_FLASH_STAMPS="$out/fs.bin" step flash_stamps 300 python -u tools/bench_prefill_attn.py --T 8192
+      python3 tools/flash_stamps.py "$out/fs.bin" > "$out/flash_stamps.md" 2>&1 ;;
     attn_bench) step attn_bench 300 python -u tools/bench_prefill_attn.py --T 8192,2048,512 --sdpa ;;
     gemm_bench) step gemm_bench 300 python -u tools/bench_gemm_tiled.py --M 8192,256 --cfg auto ;;
     gemm_mid) step gemm_mid 300 python -u tools/bench_gemm_tiled.py --M 1024,512 --cfg auto ;;
