@@ -186,17 +186,35 @@ rope_kv_v_kernel(const bf16* __restrict__ qkv, int T, int hq, int hkv, const int
 
 // ---- SiLU·mul over the interleaved gate/up output of a library GEMM (prefill) ---------------
 // gu: [T, 2F] with 16-column tiles (0..7 gate[8t..8t+7], 8..15 up[8t..8t+7]) -> h: [T, F]
+// Block (x, y) takes 1024 tiles of row y (grid-strided over rows past 65535): each thread loads its four tiles'
+// gate and up halves (8 x 16 B in flight) before it computes -- the one-tile-per-iteration form with a 64-bit
+// division per tile ran the 8k-row pass at 5.9 TB/s.
 __global__ void __launch_bounds__(256)
 silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ h, int F, int T) {
-  const size_t n = (size_t)T * (F / 8);
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t t = i / (F / 8), tile = i % (F / 8);
-    const bf16x8 gv = *reinterpret_cast<const bf16x8*>(gu + t * 2 * F + tile * 16);
-    const bf16x8 uv = *reinterpret_cast<const bf16x8*>(gu + t * 2 * F + tile * 16 + 8);
-    bf16x8 o;
+  const int tiles = F / 8;
+  for (int t = blockIdx.y; t < T; t += gridDim.y) {
+    const bf16* src = gu + (size_t)t * 2 * F;
+    bf16* dst = h + (size_t)t * F;
+    const int tile0 = blockIdx.x * 1024 + threadIdx.x;
+    bf16x8 gv[4], uv[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(silu(bf2f(gv[j])) * bf2f(uv[j]));
-    *reinterpret_cast<bf16x8*>(h + t * F + tile * 8) = o;
+    for (int u = 0; u < 4; ++u) {
+      const int tile = tile0 + 256 * u;
+      if (tile < tiles) {
+        gv[u] = *reinterpret_cast<const bf16x8*>(src + tile * 16);
+        uv[u] = *reinterpret_cast<const bf16x8*>(src + tile * 16 + 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int tile = tile0 + 256 * u;
+      if (tile < tiles) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(silu(bf2f(gv[u][j])) * bf2f(uv[u][j]));
+        *reinterpret_cast<bf16x8*>(dst + tile * 8) = o;
+      }
+    }
   }
 }
 
@@ -264,9 +282,8 @@ extern "C" hipError_t dsse_rope_kv_write(int T, const void* qkv, int hq, int hkv
 
 extern "C" hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st) {
   if (T <= 0) return hipSuccess;
-  const size_t n = (size_t)T * (F / 8);
-  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, st,
+  const dim3 grid((F / 8 + 1023) / 1024, std::min(T, 65535));
+  hipLaunchKernelGGL(silu_mul_kernel, grid, dim3(256), 0, st,
                      reinterpret_cast<const bf16*>(gu), reinterpret_cast<bf16*>(h), F, T);
   return hipGetLastError();
 }
