@@ -62,6 +62,7 @@ for s in "$@"; do
     serving13_mx256) DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
     serving40_mx512) DSSE_MIXED=1 DSSE_MIXED_CHUNK=512 step serving40_mx512 900 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 512 --itl-ratios 0 ;;
     serving40_mx256) DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving40_mx256 900 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 512 --itl-ratios 0 ;;
+    serving13_mx256_d0) DSSE_PIPELINE_DEPTH=0 DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256_d0 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
     tunable) step tunable 900 python -u tools/bench_tunable.py --M 8192,4096,2048,1024,512,256,320 --out "$out/tunableop_results.csv" ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
