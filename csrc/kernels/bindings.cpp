@@ -208,6 +208,13 @@ WCfg pick_wide(int M, int N, int K) {
   return c;
 }
 
+// cfg 8 = the pipelined 256 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's configurations
+hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W, int K,
+                      int N, const dsse::GemmEpi* ep, float* part) {
+  if (cfg == 8) return dsse_gemm_pipe(mode, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
+  return dsse_gemm_tiled(mode, cfg, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
+}
+
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
 // Tiled LDS-DMA GEMM (gemm_tiled.hip; prefill and wide batches).  Env overrides: DSSE_T_CFG (0 = 256x128,
@@ -219,13 +226,12 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("DSSE_T_CFG", -1);
-  if (cfg < 0 || cfg > 7) {
-    // measured on MI355X (profiles/r2/gemm_tiled_*.log): the 256x256 tile in the phased schedule (cfg 4: 8 waves
-    // of 128x64, two wave rows one barrier apart) is the fastest once it yields >= ~160 workgroups (1.28-1.34
-    // PFLOP/s at 8192 rows, cfg 3's one-barrier loop 1.16-1.22); below that the 256x128 tile (3-stage ring)
-    // fills more CUs; 128x128 for tiny M
+  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8) {
+    // round 5 (profiles/r5/gemm_pipe_r5.md): the 256x256 tile of gemm_pipe.hip (cfg 8: 8 waves, every LDS-DMA
+    // half-tile five phases ahead of its wait) once it yields >= ~160 workgroups -- 1.35-1.40 PFLOP/s at 8192 rows,
+    // +5-7 % over round 4's phased cfg 4; below that the 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
     const int big_tiles = ((M + 255) / 256) * (N / 256);
-    cfg = (N % 256 == 0 && big_tiles >= 160) ? 4 : (M > 128 ? 0 : 1);
+    cfg = (N % 256 == 0 && big_tiles >= 160) ? 8 : (M > 128 ? 0 : 1);
     // narrow projections of the wide decode buckets (N <= 8192, 128 < M <= 512: qkv / o / down at 192-256
     // streams): 128x128 tiles (4 waves) split 2-4 ways -- 256-stream step 9.88 vs 9.93 ms with 256x128
     // (same box, alternating; profiles/experiments_r2.md).
@@ -238,27 +244,26 @@ TCfg pick_tiled(int M, int N, int K) {
     // for the weight-heavy 129-256-row shapes: gate_up 68.1 vs 73.9 us (256 rows) / 64.4 vs 66.2 (192), down
     // (K 14336) 42.9 vs 50.5 / 41.0 vs 42.0
     if (M > 128 && M <= 256 && (N > 8192 || K > 8192)) cfg = 5;
-    // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: per shape from the
-    // tools/bench_gemm_tiled.py sweep over every config (profiles/r3/prefill_chunk_gemm.md): 257-512 rows down
-    // (K 14336) on the phased 256x256 tile split 8 ways (69 vs 92 us), qkv / o on 256x128 (46 / 33 vs 49 / 35
-    // us); 513-1024 rows N <= 4096 (o, down) on 128x128 (50 / 153 vs 65 / 205 us)
-    if (N <= 8192 && M > 256 && M <= 512) cfg = K > 8192 ? 4 : 0;
+    // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: 257-512 rows down
+    // (K 14336) on the 256x256 tile split 8 ways (cfg 8: 69 vs 72 us on round 4's phased tile, vs 92 us on
+    // 256x128), o on 256x128 (33 vs 38 us), qkv on cfg 8 (43 vs 46 us); 513-1024 rows N <= 4096 (o, down) on
+    // 128x128 (50 / 153 vs 65 / 205 us; profiles/r3/prefill_chunk_gemm.md)
+    if (N <= 8192 && M > 256 && M <= 512) cfg = (K > 8192 || N > 4096) ? 8 : 0;
     if (N <= 4096 && M > 512 && M <= 1024) cfg = 1;
   }
   constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
-  // tile shapes of gemm_tiled.hip launch_t_mode, by cfg
-  static constexpr int kBM[8] = {256, 128, 256, 256, 256, 128, 256, 256};
-  static constexpr int kBN[8] = {128, 128, 64, 256, 256, 256, 256, 256};
-  const int BM = kBM[cfg], BN = kBN[cfg];
+  // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8)
+  const int BM = cfg == 1 || cfg == 5 ? 128 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
   c.cfg = cfg;
   c.S = 1;
-  c.ok = N % BN == 0 && K % 64 == 0;
+  c.ok = N % BN == 0 && K % (cfg == 8 ? 128 : 64) == 0;
   if (!c.ok) return c;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   int S = env_int("DSSE_T_SPLIT", 0);
-  if (S <= 0 || K % (64 * S) != 0) {
+  const int kq = cfg == 8 ? 128 : 64;  // K granule of a slice (gemm_pipe: >= 2 steps of 64)
+  if (S <= 0 || K % (kq * S) != 0) {
     S = 1;  // split K only for the few-tile wide-decode shapes (slabs cost M x N x 4 B each)
-    while (M <= kMaxDecodeM && tiles * S < min_wgs && K % (64 * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
+    while (M <= kMaxDecodeM && tiles * S < min_wgs && K % (kq * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
   }
   c.S = S;
   return c;
@@ -321,8 +326,8 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
     const TCfg c = pick_tiled(M, N, K);
     at::Tensor part;
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
-    DSSE_CHECK_HIP(dsse_gemm_tiled(mode, c.cfg, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
-                                   c.S > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+    DSSE_CHECK_HIP(tiled_call(mode, c.cfg, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                              c.S > 1 ? part.data_ptr<float>() : nullptr));
     return;
   }
   TORCH_CHECK(M <= 64 || impl >= 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
@@ -390,8 +395,8 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
       check_dtype(x, at::kBFloat16, "x");
       check_dtype(w, at::kBFloat16, "w");
       dsse::GemmEpi ep{};
-      DSSE_CHECK_HIP(dsse_gemm_tiled(dsse::kResidAdd, c.cfg, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
-                                     part.data_ptr<float>(), cur_stream()));
+      DSSE_CHECK_HIP(tiled_call(dsse::kResidAdd, c.cfg, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                part.data_ptr<float>()));
       return c.S;
     }
   } else if (impl == 3) {
@@ -716,7 +721,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
     // slabs written by an earlier kernel on this stream
   } else if (impl == 4) {
     const TCfg c = pick_tiled(M, N, K);
-    DSSE_CHECK_HIP(dsse_gemm_tiled(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));
+    DSSE_CHECK_HIP(tiled_call(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl));
   } else if (impl == 3) {
     const WCfg c = pick_wide(M, N, K);
     DSSE_CHECK_HIP(dsse_gemm_wide(dsse::kQkvRope, c.mb, c.rd, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl, cur_stream()));

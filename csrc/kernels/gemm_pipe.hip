@@ -1,0 +1,297 @@
+// Prefill / wide GEMM, 256 x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
+// weight layout (api.h kTileChunk), M >= 256 (smaller M: split K, grid.z-style slices in the tile index).
+//
+// Why a new schedule (profiles/r4/pmc_gemm_r4.md): gemm_phased (gemm_tiled.hip cfg 4) issued the last A half of step
+// t+1 one phase before the counted wait that needed it, so every K step waited ~a full L2/HBM round trip -- 44 %
+// MFMA-busy, 42 % of wave time waiting on a dependency at 8192 rows.  Here every half-tile is in flight for five
+// phases (~2,500 cycles) before any wave waits for it:
+//
+//   * 8 waves = 2 wave rows (128 rows each) x 4 wave columns (64 columns each); a wave's 128 x 64 tile is four
+//     64 x 32 quadrants; a K step of 64 runs as four phases, one quadrant (16 MFMAs 16x16x32) per phase:
+//         phase 0  quadrant (0, 0)   reads A rows q0 + B cols q0   issue  A-half 1 of step t+1
+//         phase 1  quadrant (0, 1)   reads B cols q1
+//         phase 2  quadrant (1, 1)   reads A rows q1                issue  A-half 0, B-half 0 of step t+2
+//         phase 3  quadrant (1, 0)   (operands in registers)        issue  B-half 1 of step t+2
+//     each phase = [fragment reads, DMA issue, counted vmcnt] s_barrier lgkmcnt(0) [16 MFMAs, prio 1] s_barrier,
+//     with the two wave rows one barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other's LDS
+//     reads (the 8-phase template of the CDNA HIP guide, §5; the half-tile order is this kernel's own);
+//   * a "half-tile" is what one phase's quadrant reads across the workgroup: A-half q = the 64-row quadrant q of
+//     BOTH wave rows (128 rows x 128 B = 16 KiB), B-half q = the 32-column quadrant q of all four wave columns
+//     (8 column tiles x 2 KiB); each is 16 one-KiB LDS-DMA instructions, two per wave;
+//   * WAR: a half of buffer t & 1 is re-staged (for step t+2) only in a phase after the one whose reads retired it
+//     (A0 / B0 read in phase 0, re-staged in phase 2; B1 read in 1, re-staged in 3; A1 read in 2, re-staged in
+//     phase 0 of step t+1) -- with the lagging wave row that is still >= 1 barrier after its lgkmcnt(0);
+//   * RAW: counted waits -- phase 0 retires B-half 1 of step t (vmcnt 10), phase 1 A-half 1 of step t (vmcnt 8),
+//     phase 3 A0 / B0 of step t+1 (vmcnt 10) -- each in the phase before the first read, so the lagging row has
+//     passed it one barrier before the leading row reads (never vmcnt(0) in the steady loop);
+//   * buffer-load LDS-DMA: one SGPR offset per K step, per-lane offsets fixed for the whole loop (no per-step VALU
+//     address arithmetic); rows past M read as zeros (out-of-range offsets, no memory traffic); the last two steps
+//     issue nothing past the end and count their waits exactly;
+//   * XCD-aware tile order (bijective remap, groups of 8 row blocks swept by column) as gemm_tiled.hip;
+//   * epilogues: bf16 store staged through LDS (16-byte row stores), SiLU·mul, fp32 / residual / QKV+RoPE /
+//     split-K partial slabs through gemm_epilogue.h.
+#include "gemm_epilogue.h"
+
+namespace dsse {
+namespace gp {
+
+constexpr int kA = 256 * 128;     // A image of one K step: 256 rows x 64 bf16, swizzled 16-byte pieces
+constexpr int kB = 16 * 2048;     // B image: 16 column tiles x two 1 KiB k-step blocks
+constexpr int kBuf = kA + kB;     // 64 KiB per K step
+constexpr size_t kLDS = 2 * (size_t)kBuf;
+constexpr uint32_t kOOB = 0x80000000u;  // buffer offset past every range: the load returns zeros, no traffic
+
+typedef __attribute__((address_space(3))) void* lds_t;
+
+DEV void dma(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_t)(reinterpret_cast<uintptr_t>(lds)), 16, voff, soff, 0, 0);
+}
+
+// A-image swizzle (as gemm_tiled.hip a_swz): piece q of LDS row `row` holds piece q ^ swz(row) of the X row;
+// conflict-free ds_read_b128 for the A-fragment pattern (lane (r, g) reads row r, piece 2g + s).
+DEV int a_swz(int row) { return (row >> 1) & 5; }
+
+}  // namespace gp
+
+template <int MODE>
+__global__ void __launch_bounds__(512)
+gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
+                 GemmEpi ep, float* __restrict__ part) {
+  using namespace gp;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int wm = w >> 2, wn = w & 3;
+
+  // ---- tile order: bijective XCD remap, then groups of 8 row blocks swept column by column (L2 panel reuse)
+  const int nbm = (M + 255) / 256, nbn = N / 256, ntile = nbm * nbn;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
+  const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
+  const int ks = lid / ntile, tl = lid % ntile;
+  constexpr int GM = 8;
+  const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
+  const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int k0 = ks * Kr, nk = Kr >> 6;
+  const int KC = K >> 7;
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(X, (uint32_t)(((size_t)(M - 1) * ldx + K) * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(W, (uint32_t)((size_t)N * K * 2));
+
+  // ---- per-lane DMA offsets (bytes), fixed for the whole K loop: [half q][instruction i] of this wave
+  uint32_t a_vo[2][2], b_vo[2][2];
+  int a_lo[2][2], b_lo[2][2];  // LDS byte offsets inside a buffer
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 2 * w + i;                                     // instruction j of the 16 of this half
+      const int rb = (j >> 3) * 128 + q * 64 + (j & 7) * 8;        // first of its 8 rows
+      const int row = rb + (lane >> 3);
+      const int pc = (lane & 7) ^ a_swz(row);
+      a_lo[q][i] = rb * 128;
+      a_vo[q][i] = m0 + row < M ? (uint32_t)(((size_t)(m0 + row) * ldx + 32 * (pc >> 1) + 8 * (pc & 1)) * 2) : kOOB;
+      const int tb = (j >> 2) * 4 + q * 2 + ((j >> 1) & 1), sub = j & 1;  // column tile of the block, k sub-step
+      b_lo[q][i] = kA + tb * 2048 + sub * 1024;
+      b_vo[q][i] = (uint32_t)((((size_t)(n0 / 16 + tb) * KC) * kTileChunk + sub * 512 + lane * 8) * 2);
+    }
+  // K step t: X columns 128c + 16h + (piece offsets), W chunk c, k sub-steps 2h, 2h+1
+  auto a_so = [&](int t) {
+    const int kk = k0 + 64 * t;
+    return (uint32_t)(((kk >> 7) * 128 + 16 * ((kk >> 6) & 1)) * 2);
+  };
+  auto b_so = [&](int t) {
+    const int kk = k0 + 64 * t;
+    return (uint32_t)(((kk >> 7) * kTileChunk + ((kk >> 6) & 1) * 1024) * 2);
+  };
+  auto issue_a = [&](int q, int t) {
+    char* base = smem + (t & 1) * kBuf;
+    const uint32_t so = __builtin_amdgcn_readfirstlane(a_so(t));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(xr, base + a_lo[q][i], a_vo[q][i], so);
+  };
+  auto issue_b = [&](int q, int t) {
+    char* base = smem + (t & 1) * kBuf;
+    const uint32_t so = __builtin_amdgcn_readfirstlane(b_so(t));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma(wr, base + b_lo[q][i], b_vo[q][i], so);
+  };
+
+  // ---- fragment reads: A rows wm*128 + 64 qm + 16 i + r (the swizzle is the same for every i), B column tiles
+  // wn*4 + 2 qn + i, k sub-step sp of the step
+  int a_rd[2];
+#pragma unroll
+  for (int sp = 0; sp < 2; ++sp) {
+    const int row = wm * 128 + r;
+    a_rd[sp] = row * 128 + (((2 * g + sp) ^ a_swz(row)) << 4);
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4][2], b[4][2];
+  auto read_a = [&](const char* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+        a[i][sp] = *reinterpret_cast<const bf16x8*>(buf + a_rd[sp] + (64 * qm + 16 * i) * 128);
+  };
+  auto read_b = [&](const char* buf, int qn) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+        b[2 * qn + i][sp] =
+            *reinterpret_cast<const bf16x8*>(buf + kA + (wn * 4 + 2 * qn + i) * 2048 + sp * 1024 + lane * 16);
+  };
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = mfma16x16x32(a[i][sp], b[2 * qn + j][sp], acc[4 * qm + i][2 * qn + j]);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_barrier" ::: "memory");
+  };
+
+  // ---- prologue: step 0 whole, step 1 without its A-half 1 (issued in phase 0 of step 0, as in the loop)
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  issue_a(0, 1);
+  issue_b(0, 1);
+  issue_b(1, 1);
+  asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");  // A0 / B0 of step 0 landed everywhere
+  if (wm == 1) asm volatile("s_barrier" ::: "memory");  // wave row 1 runs one barrier behind row 0
+
+  // one K step; TAIL 0 = steady, 1 = step t+1 exists but t+2 does not, 2 = last step
+  auto step = [&](int t, auto tail_tag) {
+    constexpr int TAIL = decltype(tail_tag)::value;
+    const char* buf = smem + (t & 1) * kBuf;
+    // LDS-DMA issued in the fragment-read sections (counts: file header)
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if constexpr (TAIL < 2) issue_a(1, t + 1);
+    if constexpr (TAIL < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B-half 1 of step t
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    mma(0, 0);
+    read_b(buf, 1);
+    if constexpr (TAIL < 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-half 1 of step t
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mma(0, 1);
+    read_a(buf, 1);
+    if constexpr (TAIL == 0) {
+      issue_a(0, t + 2);
+      issue_b(0, t + 2);
+    }
+    mma(1, 1);
+    if constexpr (TAIL == 0) {
+      issue_b(1, t + 2);
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0 / B0 of step t+1
+    } else if constexpr (TAIL == 1) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    mma(1, 0);
+  };
+  int t = 0;
+  for (; t < nk - 2; ++t) step(t, std::integral_constant<int, 0>{});
+  step(t++, std::integral_constant<int, 1>{});  // nk >= 2 (host contract)
+  step(t, std::integral_constant<int, 2>{});
+  // balance the barrier count of the two rows
+  if (wm == 0) asm volatile("s_barrier" ::: "memory");
+
+  const int row0 = m0 + wm * 128, tile0 = n0 / 16 + wn * 4;
+  if constexpr (MODE == kStoreBf16) {
+    // stage the wave's 128 x 64 bf16 tile in LDS (all DMA retired, everyone past its last fragment read), then
+    // 16-byte row stores: 8 lanes per 128-byte row, 8 rows per instruction
+    __syncthreads();
+    bf16* st = reinterpret_cast<bf16*>(smem + w * (128 * 64 * 2));
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rr = 16 * mt + 4 * g + i, cc = 16 * nt + r;
+          // 16-byte chunk (cc >> 3) of row rr at chunk slot (cc >> 3) ^ (rr & 7): conflict-spread writes and reads
+          st[rr * 64 + ((((cc >> 3) ^ (rr & 7)) << 3) | (cc & 7))] = f2bf(acc[mt][nt][i]);
+        }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's own LDS image is complete
+    bf16* out = reinterpret_cast<bf16*>(ep.out);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int rr = 8 * it + (lane >> 3), ch = lane & 7;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + rr * 64 + ((ch ^ (rr & 7)) << 3));
+      const int m = row0 + rr;
+      if (m < M) *reinterpret_cast<bf16x8*>(out + (size_t)m * ep.ldo + n0 + wn * 64 + ch * 8) = v;
+    }
+    return;
+  }
+  if constexpr (MODE == kSiluMul) {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) silu_epilogue4(ep, M, row0 + 16 * mt + 4 * g, tile0 + nt, r, acc[mt][nt]);
+    return;
+  }
+  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = acc[mt][nt][i];
+        const float partner = (MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
+        epilogue<MODE>(ep, part_ks, M, N, row0 + 16 * mt + 4 * g + i, tile0 + nt, r, v, partner);
+      }
+}
+
+template <int MODE>
+static hipError_t launch_pipe(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
+                              float* part, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)gp::kLDS);
+    attr_set = true;
+  }
+  const int nbm = (M + 255) / 256, nbn = N / 256;
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE>), dim3(nbm * nbn * S), dim3(512), gp::kLDS, st, X, ldx, M, W, K, N,
+                     K / S, ep, part);
+  return hipGetLastError();
+}
+
+}  // namespace dsse
+
+// Shape contract (checked here): N % 256 == 0, K % (128 S) == 0 (>= 2 K steps of 64 per slice), the tiled weight
+// layout (api.h), X rows of ldx >= K elements.  S > 1: fp32 slabs [S, M, N] into `part`, reduced by
+// launch_splitk_reduce unless partial_only.
+extern "C" hipError_t dsse_gemm_pipe(int mode, int S, int partial_only, const void* X, int ldx, int M, const void* W,
+                                     int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st) {
+  using namespace dsse;
+  if (M < 1 || N % 256 != 0 || S < 1 || K % (128 * S) != 0 || ldx < K) return hipErrorInvalidValue;
+  const bf16* x = reinterpret_cast<const bf16*>(X);
+  const bf16* w = reinterpret_cast<const bf16*>(W);
+  if (S == 1 && !partial_only) {
+    switch (mode) {
+      case kStoreBf16: return launch_pipe<kStoreBf16>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_pipe<kStoreF32>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_pipe<kResidAdd>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_pipe<kSiluMul>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_pipe<kQkvRope>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+    }
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = launch_pipe<kPartial>(x, ldx, M, w, K, N, S, *ep, part, st);
+  if (e != hipSuccess || partial_only) return e;
+  return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
+}

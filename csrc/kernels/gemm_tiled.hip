@@ -210,208 +210,25 @@ static hipError_t launch_t(const bf16* X, int ldx, int M, const bf16* W, int K, 
   return hipGetLastError();
 }
 
-// ---- cfg 4: 256 x 256 tile in a phased schedule (prefill).  8 waves (2 rows x 4 columns of 128 x 64), K steps of
-// 64 in four phases of 16 MFMAs each (one 64 x 32 quadrant of the wave's tile per phase), the two wave rows
-// running one barrier apart: while one row is in its MFMA cluster (s_setprio 1) the other issues its LDS
-// fragment reads and its share of the next steps' LDS-DMA.  Each phase is
-//     [fragment reads + 2 DMA instructions] s_barrier, lgkmcnt(0), 16 MFMAs, s_barrier
-// and one K step's operands arrive as four 16 KiB half-tiles, one per phase, two LDS buffers:
-//     phase 0: read A(rows 0-63 of the wave), B(n-tiles 0-1)   DMA: B half 1 of step t+1
-//     phase 1: read B(n-tiles 2-3)                              DMA: A half 0 of step t+1
-//     phase 2: read A(rows 64-127)                              DMA: A half 1 of step t+1
-//     phase 3: --                                               DMA: B half 0 of step t+2; vmcnt(2)
-// WAR: a half-tile is re-staged >= 2 phases after its last fragment read (B halves are read in phases 0-1,
-// A halves in 0 and 2; the lagging row passed the lgkmcnt(0) of those reads one barrier before).  RAW: the
-// counted vmcnt(2) in phase 3 retires all of step t+1 except the B half of t+2 just issued, and the reads of
-// step t+1 come after the next barrier of either row.  (Schedule after the 256x256 8-phase template of the
-// CDNA HIP guide; the buffer / re-stage order is this kernel's own.)
-constexpr int kPhA = 256 * 128;      // A image: 256 rows x 64 bf16, swizzled 16-byte pieces
-constexpr int kPhB = 16 * 2048;      // B image: 16 column tiles x two 1 KiB k-step blocks
-constexpr int kPhBuf = kPhA + kPhB;  // 64 KiB per K step
-constexpr size_t kPhLDS = 2 * (size_t)kPhBuf;
-
-template <int MODE>
-__global__ void __launch_bounds__(512)
-gemm_phased_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
-                   GemmEpi ep, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int wm = w >> 2, wn = w & 3;
-
-  // tile order: as gemm_tiled_kernel (bijective XCD remap, groups of 8 row blocks swept column by column)
-  const int nbm = (M + 255) / 256, nbn = N / 256, ntile = nbm * nbn;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
-  const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
-  const int ks = lid / ntile, tl = lid % ntile;
-  constexpr int GM = 8;
-  const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
-  const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
-  const int m0 = bm * 256, n0 = bn * 256;
-  const int k0 = ks * Kr, nk = Kr >> 6;
-  const int KC = K >> 7;
-
-  // DMA sources: a half-tile is 16 one-KiB instructions; wave w issues instructions 2w and 2w + 1
-  const bf16* a_src[2][2];
-  int a_koff[2][2];
-  const bf16* b_src[2][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 128 * hf + (2 * w + i) * 8 + (lane >> 3);
-      const int pc = (lane & 7) ^ a_swz(row);
-      a_src[hf][i] = X + (size_t)min(m0 + row, M - 1) * ldx;
-      a_koff[hf][i] = 32 * (pc >> 1) + 8 * (pc & 1);
-      const int j = 2 * w + i;  // block j of B half hf: column tile 8 hf + j / 2, k sub-step j % 2
-      b_src[hf][i] = W + ((size_t)(n0 / 16 + 8 * hf + (j >> 1)) * KC) * kTileChunk + (j & 1) * 512 + lane * 8;
-    }
-  // steps past the end re-load the last step into a buffer nobody reads any more (no branch around the DMA)
-  auto issue_a = [&](int hf, int t) {
-    const int kk = k0 + 64 * min(t, nk - 1), c = kk >> 7, h = (kk >> 6) & 1;
-    char* base = smem + (t & 1) * kPhBuf + hf * (kPhA / 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(a_src[hf][i] + c * 128 + 16 * h + a_koff[hf][i], base + (2 * w + i) * 1024);
-  };
-  auto issue_b = [&](int hf, int t) {
-    const int kk = k0 + 64 * min(t, nk - 1), c = kk >> 7, h = (kk >> 6) & 1;
-    char* base = smem + (t & 1) * kPhBuf + kPhA + hf * (kPhB / 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(b_src[hf][i] + (size_t)c * kTileChunk + h * 1024, base + (2 * w + i) * 1024);
-  };
-
-  int a_off[8][2];  // A-fragment LDS offsets of the wave's 8 m-tiles (row-dependent swizzle), k sub-step sp
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-    const int row = wm * 128 + 16 * mt + r;
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp) a_off[mt][sp] = row * 128 + (((2 * g + sp) ^ a_swz(row)) << 4);
-  }
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 a[4][2], b[4][2];
-  auto read_a = [&](const char* As, int qm) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) a[i][sp] = *reinterpret_cast<const bf16x8*>(As + a_off[4 * qm + i][sp]);
-  };
-  auto read_b = [&](const char* Bs, int qn) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-        b[2 * qn + i][sp] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 4 + 2 * qn + i) * 2048 + sp * 1024 + lane * 16);
-  };
-  auto mma = [&](int qm, int qn) {
-    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * qm + i][2 * qn + j] = mfma16x16x32(a[i][sp], b[2 * qn + j][sp], acc[4 * qm + i][2 * qn + j]);
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_barrier" ::: "memory");
-  };
-
-  // prologue: step 0 and B half 0 of step 1; everyone's step 0 landed before the first reads
-  issue_b(0, 0);
-  issue_b(1, 0);
-  issue_a(0, 0);
-  issue_a(1, 0);
-  issue_b(0, 1);
-  asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
-  if (wm == 1) asm volatile("s_barrier" ::: "memory");  // wave row 1 runs one barrier behind row 0
-  for (int t = 0; t < nk; ++t) {
-    const char* As = smem + (t & 1) * kPhBuf;
-    const char* Bs = As + kPhA;
-    read_a(As, 0);
-    read_b(Bs, 0);
-    issue_b(1, t + 1);
-    mma(0, 0);
-    read_b(Bs, 1);
-    issue_a(0, t + 1);
-    mma(0, 1);
-    read_a(As, 1);
-    issue_a(1, t + 1);
-    mma(1, 0);
-    issue_b(0, t + 2);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // step t+1 landed (this wave's DMA); B half 0 of t+2 in flight
-    mma(1, 1);
-  }
-  // balance the barrier count of the two rows; no DMA may still write this workgroup's LDS after it exits
-  if (wm == 0) asm volatile("s_barrier" ::: "memory");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
-  const int row0 = m0 + wm * 128, tile0 = n0 / 16 + wn * 4;
-  if constexpr (MODE == kSiluMul) {
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) silu_epilogue4(ep, M, row0 + 16 * mt + 4 * g, tile0 + nt, r, acc[mt][nt]);
-    return;
-  }
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = acc[mt][nt][i];
-        const float partner = (MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
-        epilogue<MODE>(ep, part_ks, M, N, row0 + 16 * mt + 4 * g + i, tile0 + nt, r, v, partner);
-      }
-}
-
-template <int MODE>
-static hipError_t launch_phased(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
-                                float* part, hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phased_kernel<MODE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPhLDS);
-    attr_set = true;
-  }
-  const int nbm = (M + 255) / 256, nbn = N / 256;
-  hipLaunchKernelGGL((gemm_phased_kernel<MODE>), dim3(nbm * nbn * S), dim3(512), kPhLDS, st, X, ldx, M, W, K, N,
-                     K / S, ep, part);
-  return hipGetLastError();
-}
-
 template <int MODE>
 static hipError_t launch_t_mode(int cfg, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                                 const GemmEpi& ep, float* part, hipStream_t st) {
   switch (cfg) {
     // measured on MI355X (profiles/r2/gemm_tiled_v*.log); other tile / ring shapes tried and removed are listed
-    // in profiles/experiments_r2.md
+    // in profiles/experiments_r2.md; the 256 x 256 configurations moved to gemm_pipe.hip (cfg 8, round 5)
     case 0: return launch_t<4, 2, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 128, 8 waves
     case 1: return launch_t<2, 2, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 128, 4 waves
-    case 2: return launch_t<4, 1, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 64, 4 waves
-    case 3: return launch_t<2, 4, 8, 4, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 2 stages
-    case 4: return launch_phased<MODE>(X, ldx, M, W, K, N, S, ep, part, st);              // 256 x 256, phased
     case 5: return launch_t<2, 4, 4, 4, 3, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 128 x 256, 8 waves
-    case 6: return launch_t<2, 2, 8, 8, 2, 1, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 4 waves
-    case 7: return launch_t<2, 2, 8, 8, 2, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);  // 256 x 256, 4 waves, FB 2
   }
   return hipErrorInvalidValue;
 }
 
 }  // namespace dsse
 
-// cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 2 = 256 x 64 (4 waves),
-// 3 = 256 x 256 (8 waves of 128 x 64, 2 LDS stages), 4 = 256 x 256 in the phased schedule (gemm_phased_kernel),
-// 5 = 128 x 256 (8 waves, 3 stages of 16 KiB X + 32 KiB W: twice the weight bytes in flight per CU of cfg 0, for the
-// weight-streaming 129-256-row decode GEMMs; the two row blocks of a column block share an XCD and its L2).
+// cfg: 0 = 256 x 128 tile (8 waves, 3 LDS stages), 1 = 128 x 128 (4 waves), 5 = 128 x 256 (8 waves, 3 stages of 16
+// KiB X + 32 KiB W: twice the weight bytes in flight per CU of cfg 0, for the weight-streaming 129-256-row decode
+// GEMMs; the two row blocks of a column block share an XCD and its L2).  (Round 4's 256 x 256 configurations 2, 3, 4,
+// 6 and 7 are gone: gemm_pipe.hip, cfg 8, replaces them.)
 // (Round 3 also tried 4-stage rings and separate X / W loader rings for the 129-512-row decode buckets: all
 // slower in the 256-stream step, removed; profiles/r3/experiments_r3.md.)
 // Shape contract (checked by the caller): N % BN == 0, K % (64 S) == 0, the tiled weight layout (api.h).

@@ -35,7 +35,7 @@ from .. import ops
 from ..ops.reference import rope_table
 from ..parallel.comm import TPComm
 from .kv_cache import PAGE, KVCache
-from .weights import EngineWeights, attach_library
+from .weights import EngineWeights
 
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
@@ -95,41 +95,8 @@ def prefill_row_chunks(T: int, tp: int) -> list:
     return [(a, min(T, a + step)) for a in range(0, T, step)]
 
 
-# Rows from which a projection runs on the library GEMM (hipBLASLt through torch.matmul on the row-major weight copies,
-# weights.attach_library) instead of the tiled-layout kernels, per projection, from interleaved A/Bs on MI355X
-# (profiles/r4/prefill_lib_r4.md): 512 rows qkv 34 vs 46 us, o 27 vs 33, gate_up 89 (+ ~8 silu_mul) vs 114, down 87 vs
-# 73 (tiled wins); 1024 rows all four (down 118 vs 171); 256 rows only gate_up (57 vs 68-71).  8k TTFT 112.5 vs 121.9 ms.
-LIB_MIN_ROWS = {"qkv": 512, "o": 512, "gate_up": 256, "down": 1024}
-
-
 # prompt passes up to this many rows send the residual projections' split-K slabs to the norm (_prefill_resid)
 PREFILL_SLAB_ROWS = 512
-
-
-def prefill_lib_enabled(dev) -> bool:
-    """DSSE_PREFILL_LIB=0: every projection on the tiled kernels (and no 14.5 GB of row-major copies)."""
-    return torch.device(dev).type == "cuda" and os.environ.get("DSSE_PREFILL_LIB", "1") != "0"
-
-
-TUNED_GEMMS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "tunableop_gfx950.csv")
-
-
-def load_tuned_gemms() -> bool:
-    """The library projections' best solution per shape (PyTorch TunableOp results, tuned on MI355X with this image's
-    torch / hipBLASLt / rocBLAS by tools/bench_tunable.py: 3-17 % faster than the default heuristic for most prefill
-    shapes, entries that tuned slower dropped; profiles/r4/prefill_lib_r4.md).  Tuning itself stays off: a shape not in
-    the file uses the library default, and nothing is benchmarked at serving time.  Process-wide; the file's
-    validators (torch / HIP / library versions, gfx arch) must match or it is ignored.  DSSE_TUNABLEOP=0 disables."""
-    path = os.environ.get("DSSE_TUNABLEOP_FILE", TUNED_GEMMS)
-    if os.environ.get("DSSE_TUNABLEOP", "1") == "0" or not os.path.exists(path):
-        return False
-    tun = torch.cuda.tunable
-    tun.tuning_enable(False)
-    tun.set_filename(path)
-    if not tun.read_file(path):
-        return False
-    tun.enable(True)
-    return True
 
 
 # decode buckets run on the persistent MLP kernel (rows <= 64; smaller buckets keep the launch-per-op path unless
@@ -254,15 +221,6 @@ class ModelRunner:
         if self.comm.size > 1 and self.comm.rank == 0:
             print(f"[engine] TP={self.comm.size} decode all-reduce: "
                   f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
-        # wide projections on the library GEMMs (row-major weight copies, weights.attach_library): LIB_MIN_ROWS
-        self.lib = prefill_lib_enabled(dev)
-        self._gu = None
-        if self.lib:
-            attach_library(w)
-            load_tuned_gemms()
-            # [rows, 2F] gate / up product of the library path, allocated once (captured graphs hold its address):
-            # a pass with more rows than this runs gate_up on the tiled kernel instead
-            self._gu = torch.empty(max(max_prefill_tokens, Bm + 2048), 2 * F, **bf)
         self.graphs = {}
         self.graph_pool = None
         self.pf_graphs = {}   # row bucket -> captured prefill graph
@@ -601,24 +559,13 @@ class ModelRunner:
         done.record(self._side)
         return done
 
-    def _proj(self, a, wt, ws, out, kind: str) -> None:
-        """out = a·wᵀ in bf16: the library GEMM on the row-major copy from LIB_MIN_ROWS[kind] rows, else the tiled
-        kernels."""
-        if self.lib and ws is not None and a.shape[0] >= LIB_MIN_ROWS[kind]:
-            torch.matmul(a, ws.t(), out=out)
-        else:
-            ops.gemm_out(a, wt, out)
+    def _proj(self, a, wt, out) -> None:
+        """out = a·wᵀ in bf16 on the engine's tiled-layout GEMMs (every row count: no library GEMM)."""
+        ops.gemm_out(a, wt, out)
 
     def _gate_up(self, x, L, h) -> None:
-        """h = SiLU(x·W_gateᵀ)·(x·W_upᵀ): fused epilogue on the tiled kernels, or the library GEMM into a [rows, 2F]
-        product (gate / up interleaved in 8-column blocks, as the tiled rows) + the vectorised silu_mul pass."""
-        rows = x.shape[0]
-        if self.lib and L.wgu_s is not None and LIB_MIN_ROWS["gate_up"] <= rows <= self._gu.shape[0]:
-            gu = self._gu[:rows]
-            torch.matmul(x, L.wgu_s.t(), out=gu)
-            ops.silu_mul(gu, h)
-        else:
-            ops.gemm_silu(x, L.wgu_t, h)
+        """h = SiLU(x·W_gateᵀ)·(x·W_upᵀ) with the fused SiLU·mul epilogue (gate / up rows interleaved by 8)."""
+        ops.gemm_silu(x, L.wgu_t, h)
 
     def _prefill_post_attention(self, T: int, attn, L, w_next, resid, x, h, tmp) -> None:
         """resid += all_reduce(attn·Woᵀ); x = norm(resid); resid += all_reduce(silu-mlp(x)); x = norm(resid)·w_next.
@@ -631,14 +578,14 @@ class ModelRunner:
         eps = self.cfg.rms_eps
         chunks = prefill_row_chunks(T, self.comm.size)
         if len(chunks) == 1:
-            self._prefill_resid(attn, L.wo_t, resid, L.ffn_norm, x, tmp, L.wo_s, "o")
+            self._prefill_resid(attn, L.wo_t, resid, L.ffn_norm, x, tmp)
             self._gate_up(x, L, h)
-            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp, L.wd_s, "down")
+            self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
             return
         main = torch.cuda.current_stream(self.device) if tmp.is_cuda else None
         ar1 = []
         for a, b in chunks:
-            self._proj(attn[a:b], L.wo_t, L.wo_s, tmp[a:b], "o")
+            self._proj(attn[a:b], L.wo_t, tmp[a:b])
             ar1.append(self._comm_async(tmp[a:b]))
         ar2 = []
         for (a, b), ev in zip(chunks, ar1):
@@ -646,25 +593,24 @@ class ModelRunner:
                 main.wait_event(ev)
             ops.rmsnorm(resid[a:b], L.ffn_norm, x[a:b], eps, delta=tmp[a:b])
             self._gate_up(x[a:b], L, h[a:b])
-            self._proj(h[a:b], L.wd_t, L.wd_s, tmp[a:b], "down")  # tmp rows [a, b) are free: their O all-reduce was consumed
+            self._proj(h[a:b], L.wd_t, tmp[a:b])  # tmp rows [a, b) are free: their O all-reduce was consumed
             ar2.append(self._comm_async(tmp[a:b]))
         for (a, b), ev in zip(chunks, ar2):
             if ev is not None:
                 main.wait_event(ev)
             ops.rmsnorm(resid[a:b], w_next, x[a:b], eps, delta=tmp[a:b])
 
-    def _prefill_resid(self, a, wt, resid, norm_w, x, tmp, ws=None, kind: str = "o") -> None:
+    def _prefill_resid(self, a, wt, resid, norm_w, x, tmp) -> None:
         """resid += a·wᵀ, x = RMSNorm(resid).  Thousands of rows: the product goes out as a bf16 tile (row-contiguous
         stores) and the norm kernel adds it -- the fused fp32 read-modify-write epilogue measured +120 us per
         8192-row projection (profiles/r2/prefill_kernels_8k.md).  Up to PREFILL_SLAB_ROWS rows on the tiled kernels
         (split K) the norm reduces the fp32 split-K slabs itself, as in decode: no reduce launch, no bf16 round trip."""
         rows = a.shape[0]
-        lib = self.lib and ws is not None and rows >= LIB_MIN_ROWS[kind]
-        if self.comm.size == 1 and not lib and rows <= PREFILL_SLAB_ROWS and self.split_part.numel() >= 8 * rows * wt.shape[0]:
+        if self.comm.size == 1 and rows <= PREFILL_SLAB_ROWS and self.split_part.numel() >= 8 * rows * wt.shape[0]:
             ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
             ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, part=self.split_part, nsplit=ns)
             return
-        self._proj(a, wt, ws, tmp, kind)
+        self._proj(a, wt, tmp)
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 
@@ -780,12 +726,12 @@ class ModelRunner:
         resid, x, q, attn, h, tmp, qkv = (d[k] for k in ("resid", "x", "q", "attn", "h", "tmp", "qkv"))
         ops.rmsnorm(resid, w.layers[0].attn_norm, x, eps, embed=w.embed, ids=d["ids"])
         nl = len(w.layers)
-        # projections on the engine's tiled-layout GEMMs (csrc/kernels/gemm_tiled.hip for T > 128 rows; gate_up with its
-        # fused SiLU·mul epilogue) below lib_min rows, on the library GEMM above (_proj / _gate_up)
+        # projections on the engine's tiled-layout GEMMs (gemm_pipe.hip / gemm_tiled.hip for T > 128 rows; gate_up with
+        # its fused SiLU·mul epilogue): no library GEMM
         for li, L in enumerate(w.layers):
             # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
             # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
-            self._proj(x, L.wqkv_t, L.wqkv_s, qkv, "qkv")
+            self._proj(x, L.wqkv_t, qkv)
             ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
                                 d["wt"], attn, self.part_o, self.part_ml, d["part"], 1)
@@ -858,7 +804,7 @@ class ModelRunner:
         nl = len(w.layers)
         for li, L in enumerate(w.layers):
             kc, vc = self.kv.k[li], self.kv.v[li]
-            self._proj(x, L.wqkv_t, L.wqkv_s, qkv, "qkv")
+            self._proj(x, L.wqkv_t, qkv)
             ops.rope_kv_write(qkv, pos, slots, self.rope, q, kc, vc, nh, nkv)
             ops.paged_attention(0, q[r], kc, vc, self.block_tables[r], self.q_start[r], self.q_len[r],
                                 self.ctx_len[r], self.work_seq[r], self.work_tile[r], attn[r], self.part_o,

@@ -27,7 +27,7 @@ from dataclasses import dataclass
 import torch
 
 from ..models.mistral import MistralConfig
-from ..ops.reference import gate_up_perm, rotary_perm, tile_weight, untile_weight
+from ..ops.reference import gate_up_perm, rotary_perm, tile_weight
 
 
 @dataclass
@@ -43,13 +43,6 @@ class LayerWeights:
     wo_t: torch.Tensor = None
     wgu_t: torch.Tensor = None
     wd_t: torch.Tensor = None
-    # optional row-major [N, K] copies (same row order as the tiled ones) for the library GEMMs of long prefills
-    # (attach_library): hipBLASLt runs 8192-row projections at 1.5-1.6 PFLOP/s against 1.25-1.34 for gemm_phased
-    # (profiles/r4/gemm_wide_r4.md); 288 GB of HBM has room for the second 14.5 GB copy
-    wqkv_s: torch.Tensor = None
-    wo_s: torch.Tensor = None
-    wgu_s: torch.Tensor = None
-    wd_s: torch.Tensor = None
 
 
 @dataclass
@@ -102,17 +95,6 @@ def attach_tiled(w: EngineWeights) -> EngineWeights:
     if w.lm_head_t is None:
         w.lm_head_t = tile_weight(w.lm_head)
     w.lm_head = None
-    return w
-
-
-@torch.no_grad()
-def attach_library(w: EngineWeights) -> EngineWeights:
-    """Row-major copies of the four projections for the library (hipBLASLt) prefill GEMMs, built from the tiled
-    copies on their device (idempotent)."""
-    for L in w.layers:
-        if L.wo_s is None:
-            L.wqkv_s, L.wo_s, L.wgu_s, L.wd_s = (untile_weight(t).contiguous()
-                                                 for t in (L.wqkv_t, L.wo_t, L.wgu_t, L.wd_t))
     return w
 
 

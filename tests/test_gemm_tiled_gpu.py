@@ -72,8 +72,12 @@ def test_tiled_silu_gate_up(gpu, M):
     _check(out, ref, f"gate_up silu M={M}", rel=2e-2)
 
 
+@pytest.mark.parametrize("cfg", ["auto", "8"])
 @pytest.mark.parametrize("M", [300, 2048])
-def test_tiled_qkv_rope_kv_write(gpu, M):
+def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
+    if cfg != "auto":
+        monkeypatch.setenv("DSSE_T_CFG", cfg)
+        ops.refresh_env()
     g = torch.Generator().manual_seed(M + 2)
     x = _rand((M, H), g, gpu)
     w = R.tile_weight(_rand(((NH + 2 * NKV) * 128, H), g, gpu, 1 / 64))
@@ -94,8 +98,7 @@ def test_tiled_qkv_rope_kv_write(gpu, M):
     _check(vc.cpu(), vr, "v cache", rel=2e-2)
 
 
-@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("2", "4"), ("4", "1"), ("4", "2"), ("5", "1"), ("5", "2"),
-                                       ("6", "1"), ("7", "2")])
+@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("5", "1"), ("5", "2"), ("8", "1"), ("8", "2"), ("8", "4")])
 def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     monkeypatch.setenv("DSSE_T_CFG", cfg)
     monkeypatch.setenv("DSSE_T_SPLIT", split)
@@ -103,33 +106,35 @@ def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     g = torch.Generator().manual_seed(int(cfg) * 10 + int(split))
     for M in (1, 70, 256, 600):
         x = _rand((M, 2048), g, gpu)
-        w = R.tile_weight(_rand((1024 if cfg not in ("4", "6", "7") else 1536, 2048), g, gpu, 1 / 45))
+        w = R.tile_weight(_rand((1024 if cfg != "8" else 1536, 2048), g, gpu, 1 / 45))
         out = torch.empty(M, w.shape[0], device=gpu)
         ops.gemm_out(x, w, out)
         _check(out, _ref(x, w), f"cfg {cfg} split {split} M={M}", rel=2e-3)
 
 
 @pytest.mark.parametrize("M", [256, 1000, 8192])
-def test_phased_schedule_all_epilogues(gpu, monkeypatch, M):
-    """cfg 4, the phased 256 x 256 schedule (two wave rows one barrier apart, four half-tile DMA phases per K
-    step): bf16 store, residual add and SiLU·mul at Mistral-7B shapes, ragged M included."""
-    monkeypatch.setenv("DSSE_T_CFG", "4")
+def test_pipe_schedule_all_epilogues(gpu, monkeypatch, M):
+    """cfg 8, the 256 x 256 tile of gemm_pipe.hip (two wave rows one barrier apart, four half-tile phases per K step,
+    every LDS-DMA half-tile five phases ahead of its counted wait, LDS-staged bf16 stores): bf16 store, residual add
+    and SiLU·mul at Mistral-7B shapes, ragged M included."""
+    cfg = "8"
+    monkeypatch.setenv("DSSE_T_CFG", cfg)
     ops.refresh_env()
     g = torch.Generator().manual_seed(M + 40)
     x = _rand((M, H), g, gpu)
     wq = R.tile_weight(_rand(((NH + 2 * NKV) * 128, H), g, gpu, 1 / 64))
     out = torch.empty(M, wq.shape[0], device=gpu, dtype=torch.bfloat16)
     ops.gemm_out(x, wq, out)
-    _check(out, _ref(x, wq), f"phased qkv M={M}")
+    _check(out, _ref(x, wq), f"pipe qkv M={M}")
     h = _rand((M, F), g, gpu)
     wd = R.tile_weight(_rand((H, F), g, gpu, 1 / math.sqrt(F)))
     r0 = torch.randn(M, H, generator=g).to(gpu)
     r = r0.clone()
     ops.gemm_resid(h, wd, r)
-    _check(r, r0 + _ref(h, wd), f"phased down resid M={M}", rel=2e-3)
+    _check(r, r0 + _ref(h, wd), f"pipe down resid M={M}", rel=2e-3)
     wgu = R.tile_weight(_rand((2 * F, H), g, gpu, 1 / 64))
     hs = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
     ops.gemm_silu(x, wgu, hs)
     gu = _ref(x, wgu).view(M, 2 * F // 16, 16)
     ref = (torch.nn.functional.silu(gu[..., :8]) * gu[..., 8:]).reshape(M, F)
-    _check(hs, ref, f"phased gate_up silu M={M}", rel=2e-2)
+    _check(hs, ref, f"pipe gate_up silu M={M}", rel=2e-2)

@@ -38,8 +38,8 @@ GEMM_CONFIGS = {
     "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
     "tiled-default": {"DSSE_GEMM_IMPL": "4"},
     "tiled-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "1", "DSSE_T_SPLIT": "2"},
-    "tiled-256x64": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "2"},
-    "tiled-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "3"},
+    "tiled-128x256": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "5"},
+    "pipe-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "8"},
     "skinny-default": {"DSSE_GEMM_IMPL": "0"},
     "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
     "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},

@@ -90,30 +90,25 @@ def test_engine_wide_batch_path_gpu(gpu, monkeypatch, impl):
         ops.refresh_env()
 
 
-def test_engine_forward_library_gemm_only_behind_the_row_thresholds():
-    """Every projection goes through the engine's GEMM ops (tiled weight layout) except the wide ones that
-    ModelRunner._proj / _gate_up send to the library GEMM from LIB_MIN_ROWS rows (on the row-major copies that
-    attach_library adds on a GPU only): no other library matmul in the model runner, and converted engine weights
-    hold no row-major copy."""
+def test_engine_forward_has_no_library_gemm():
+    """Every projection of the engine (decode, prefill, mixed steps, at every row count) goes through the engine's
+    hand-written GEMM ops on the tiled weight layout: no torch.matmul / mm / linear / @ anywhere in the engine package
+    (round 5 deleted the hipBLASLt path and its row-major weight copies), and converted engine weights hold no row-major
+    copy."""
     import ast
     import inspect
 
-    from distributed_sse_for_llm_response_amd.engine import model_runner
+    from distributed_sse_for_llm_response_amd.engine import engine, kv_cache, model_runner, weights
 
-    tree = ast.parse(inspect.getsource(model_runner))
-    allowed = set()
-    for fn in ast.walk(tree):
-        if isinstance(fn, ast.FunctionDef) and fn.name in ("_proj", "_gate_up"):
-            allowed |= {id(n) for n in ast.walk(fn)}
-    for node in ast.walk(tree):
-        assert not isinstance(node, ast.BinOp) or not isinstance(node.op, ast.MatMult), ast.unparse(node)
-        if isinstance(node, ast.Attribute) and node.attr in ("matmul", "mm", "bmm", "addmm", "linear"):
-            assert id(node) in allowed, ast.unparse(node)
-    assert set(model_runner.LIB_MIN_ROWS) == {"qkv", "o", "gate_up", "down"}
-    assert min(model_runner.LIB_MIN_ROWS.values()) >= 256  # decode buckets <= 192 rows never take the library path
-    assert not model_runner.prefill_lib_enabled("cpu")
+    for mod in (model_runner, engine, kv_cache, weights):
+        tree = ast.parse(inspect.getsource(mod))
+        for node in ast.walk(tree):
+            assert not isinstance(node, ast.BinOp) or not isinstance(node.op, ast.MatMult), ast.unparse(node)
+            if isinstance(node, ast.Attribute):
+                assert node.attr not in ("matmul", "mm", "bmm", "addmm", "linear", "tunable"), ast.unparse(node)
+    assert not hasattr(model_runner, "LIB_MIN_ROWS") and not hasattr(weights, "attach_library")
     w = convert_standard(TINY, init_standard_weights(TINY, seed=1))
     assert w.lm_head is None and all(L.wqkv is None and L.wo is None and L.wgu is None and L.wd is None
                                      for L in w.layers)
-    assert all(L.wo_s is None for L in w.layers)
+    assert all(not hasattr(L, "wo_s") for L in w.layers)
     assert w.nbytes() > 0

@@ -45,9 +45,7 @@ for s in "$@"; do
     prof256) step prof256 600 rocprofv3 --kernel-trace --stats -d "$out/prof256" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
     prof64_mega) DSSE_MEGA=1 step prof64_mega 600 rocprofv3 --kernel-trace --stats -d "$out/prof64_mega" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
-    ttft8k_nolib) DSSE_PREFILL_LIB=0 step ttft8k_nolib 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     ttft512) step ttft512 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
-    ttft512_nolib) DSSE_PREFILL_LIB=0 step ttft512_nolib 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
     profttft8k)
       step profttft8k 600 rocprofv3 --kernel-trace -d "$out/profttft8k" -o run --output-format csv -- python3 tools/bench_ttft.py --prompt-len 8192 --decode-steps 0 --profile-marker
       python3 tools/trace_sum.py "$(ls "$out"/profttft8k/*/run_kernel_trace.csv "$out"/profttft8k/run_kernel_trace.csv 2>/dev/null | head -1)" --div 3 --after-kernel bitwise_not --title "8k-token prefill, per prompt (3 timed prompts, setup and warm-up excluded)" > "$out/profttft8k.md" 2>&1 ;;
@@ -64,7 +62,6 @@ for s in "$@"; do
     serving40_mx256) DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving40_mx256 900 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 512 --itl-ratios 0 ;;
     serving13_mx256_d0) DSSE_PIPELINE_DEPTH=0 DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256_d0 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
-    tunable) step tunable 900 python -u tools/bench_tunable.py --M 8192,4096,2048,1024,512,256,320 --out "$out/tunableop_results.csv" ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill or rope_kv" ;;
     flash_stamps) DSSE_FLASH_STAMPS="$out/fs.bin" step flash_stamps 300 python -u tools/bench_prefill_attn.py --T 8192
