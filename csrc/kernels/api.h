@@ -65,46 +65,6 @@ struct AttnParams {
   bf16* v_out;              // = v_cache, writable
 };
 
-// Persistent decode MLP block (decode_mega.hip): O projection -> residual + RMSNorm -> gate_up + SiLU·mul -> down
-// -> residual + RMSNorm, one launch of 256 resident workgroups for <= 64 rows (Mistral-7B shapes, TP = 1).
-struct MegaMlpParams {
-  bf16* attn;          // [M, H] O-projection input (written by the optional attention phase)
-  const bf16* wo;      // tiled [H, H]
-  const bf16* wgu;     // tiled [2F, H], gate/up rows interleaved in 8-row blocks
-  const bf16* wd;      // tiled [H, F]
-  float* resid;        // [M, H] fp32 residual stream (in / out)
-  const bf16* w_ffn;   // [H] post-attention norm weight
-  const bf16* w_next;  // [H] next layer's input norm (or the final norm)
-  bf16* xm;            // [M, H] gate_up input
-  bf16* h;             // [M, F] SiLU(gate)·up
-  bf16* x;             // [M, H] next layer's input
-  float* slabs;        // [8, M, H] split-K partial products
-  const bf16* wqkv;    // optional: the NEXT layer's tiled QKV weight [(nh + 2 nkv) * 128 = 6144, H]; its projection of x
-                       // runs as the block's last phase (4 fp32 split-K slabs into qkv_slabs, for the folded attention)
-  float* qkv_slabs;    // [4, M, 6144] (may alias slabs: written only after every slab above was consumed)
-  // optional FIRST phase: this layer's decode attention (attention.hip mode 3's folded QKV epilogue: slab sum, RoPE,
-  // the step's K / V written into the cache, then paged attention) on the QKV slabs an earlier launch left in
-  // qkv_in, writing `attn` (so the layer is one launch).  qkv_in == nullptr: attention ran as its own launch.
-  const float* qkv_in;   // [qkv_in_S, M, 6144] fp32 slabs, columns in the engine's rotary-pair order
-  int qkv_in_S;
-  bf16* k_cache;         // [blocks, 8, 32, 128]
-  bf16* v_cache;         // [blocks, 8, 128, 32] (token-permuted pages)
-  const int* block_tables;
-  int max_blocks, num_blocks, num_slots, rope_len;
-  const int* q_len;      // [M] 1 = live, 0 = inactive
-  const int* ctx_len;    // [M]
-  const int* positions;  // [M]
-  const int* slots;      // [M]
-  const float2* rope;    // [rope_len, 64]
-  float scale_log2;
-  unsigned long long* stamps;  // optional [256][16] s_memrealtime (100 MHz) phase stamps, decode_mega.hip
-  int pf_steps;                // seam prefetch steps per compute wave (0 .. mega::kPF), decode_mega.hip
-  unsigned* sync;      // dsse_mega_sync_words() words, zeroed once at allocation, never reset
-  unsigned* err;       // set to 1 when a bounded wait timed out (the engine's health word, read at drain time)
-  int M;
-  float eps;
-};
-
 struct SampleParams {
   const float* logits;  // [B, ld]
   int ld, V;            // row stride, local vocab size
@@ -155,10 +115,6 @@ hipError_t dsse_silu_mul(int T, int F, const void* gu, void* h, hipStream_t st);
 hipError_t dsse_decode_prep(int B, const int* active, const int* positions, const int* block_tables,
                             int max_blocks, int num_blocks, int* slots, int* ctx_len, int* q_len, hipStream_t st);
 hipError_t dsse_ring_advance(int* counter, hipStream_t st);
-// persistent decode MLP block (decode_mega.hip)
-size_t dsse_mega_sync_words();
-hipError_t dsse_mega_mlp(const dsse::MegaMlpParams* p, hipStream_t st);
-hipError_t dsse_prefetch(const void* src, int64_t bytes, int wgs, unsigned* sink, hipStream_t st);
 // TP all-reduce + residual + RMSNorm over IPC peer buffers (allreduce.hip)
 size_t dsse_ar_buffer_bytes(int rows, int H);
 hipError_t dsse_ar_alloc(size_t bytes, void** ptr, void* handle64, int* uncached);

@@ -458,13 +458,13 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     if (p->nparts > 1)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else if (mode == 0) {
-    // decode: p->kwv (DSSE_ATTN_KWV, read by the bindings) = waves per workgroup splitting the keys (1/2/4/8).
+    // decode: p->kwv (attn_kwv in DSSE_KERNEL_CFG, read by the bindings) = waves per workgroup splitting the keys (1/2/4/8).
     // Measured (profiles/attention_decode_r1.md): 4 key-split waves are best up to ~1k workgroups (64 streams x
     // 8 kv heads: 29 us at 560 keys, 5.1 TB/s), one wave per (sequence, kv head) above (256 streams: 100 vs
     // 109 us, 5.9 TB/s).  (A next-page register prefetch variant cost 2-10 % and was removed.)
     const dim3 grid(num_work, p->hkv, p->nparts);
     const int kwv = p->kwv ? p->kwv : (grid.x * grid.y * grid.z >= 2048 ? 1 : 4);
-    const int pd = p->pd == 2 && kwv <= 2 ? 2 : 1;  // DSSE_ATTN_PD=2: 2-page register ring (1 / 2 waves)
+    const int pd = p->pd == 2 && kwv <= 2 ? 2 : 1;  // attn_pd=2 (DSSE_KERNEL_CFG): 2-page register ring (1 / 2 waves)
     if (kwv == 8) hipLaunchKernelGGL((paged_attention_kernel<1, 8, 1>), grid, dim3(512), 0, st, *p);
     else if (kwv == 1 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 2>), grid, dim3(64), 0, st, *p);
     else if (kwv == 2 && pd == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 2>), grid, dim3(128), 0, st, *p);

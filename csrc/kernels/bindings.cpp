@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
@@ -42,26 +43,41 @@ void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
 }
 
-// Tuning knobs (DSSE_* environment variables) are read once per thread and cached in a thread-local map: no
-// getenv and no lock on the launch path.  refresh_env() (op dsse::refresh_env, for the tuning tools that change
-// them in-process) bumps a generation that makes every thread re-read on its next lookup.
+// Kernel-configuration overrides: ONE environment variable, DSSE_KERNEL_CFG = "key=value,key=value" (diagnostics and
+// the tests that force a kernel path; e.g. "gemm_impl=4,t_cfg=8,t_split=2").  Keys name the selector inputs below
+// (gemm_impl, t_cfg, t_split, s_nw, s_nt, s_rd, s_split, s_ring, ring2, resid_nw, resid_split, qkv_split, w_split, w_rd,
+// gemm_nt, gemm_kw, attn_kwv, attn_pd, fused_qkv_attn, trap_fpe); docs/operations.md lists them.  Parsed once per
+// thread into a thread-local map: no getenv and no lock on the launch path.  refresh_env() (op dsse::refresh_env, for
+// the tools that change it in-process) bumps a generation that makes every thread re-parse on its next lookup.
 std::atomic<uint64_t> g_env_gen{1};
-int env_int(const char* name, int dflt) {
-  thread_local std::unordered_map<std::string, int> cache;
+std::unordered_map<std::string, int> parse_kernel_cfg() {
+  std::unordered_map<std::string, int> m;
+  const char* v = std::getenv("DSSE_KERNEL_CFG");
+  if (!v) return m;
+  std::string s(v), item;
+  for (size_t i = 0; i <= s.size(); ++i) {
+    if (i == s.size() || s[i] == ',' || s[i] == ' ' || s[i] == ';') {
+      const size_t eq = item.find('=');
+      if (eq != std::string::npos && eq > 0) m[item.substr(0, eq)] = std::atoi(item.c_str() + eq + 1);
+      item.clear();
+    } else {
+      item += (char)std::tolower((unsigned char)s[i]);
+    }
+  }
+  return m;
+}
+int env_int(const char* key, int dflt) {
+  thread_local std::unordered_map<std::string, int> cfg;
   thread_local uint64_t gen = 0;
   const uint64_t g = g_env_gen.load(std::memory_order_acquire);
   if (gen != g) {
-    cache.clear();
+    cfg = parse_kernel_cfg();
     gen = g;
   }
-  auto it = cache.find(name);
-  if (it == cache.end()) {
-    const char* v = std::getenv(name);
-    it = cache.emplace(name, v ? std::atoi(v) : INT32_MIN).first;
-  }
-  return it->second == INT32_MIN ? dflt : it->second;
+  auto it = cfg.find(key);
+  return it == cfg.end() ? dflt : it->second;
 }
-// DSSE_TRAP_FPE=1: print the native stack of a host SIGFPE (integer division by zero) before dying.
+// trap_fpe=1: print the native stack of a host SIGFPE (integer division by zero) before dying.
 void fpe_handler(int sig) {
   void* frames[64];
   const int n = backtrace(frames, 64);
@@ -72,8 +88,7 @@ void fpe_handler(int sig) {
   raise(sig);
 }
 const bool g_fpe_trap = [] {
-  const char* v = std::getenv("DSSE_TRAP_FPE");
-  if (v && v[0] == '1') signal(SIGFPE, fpe_handler);
+  if (parse_kernel_cfg().count("trap_fpe") && parse_kernel_cfg()["trap_fpe"] == 1) signal(SIGFPE, fpe_handler);
   return true;
 }();
 
@@ -82,13 +97,13 @@ void refresh_env() { g_env_gen.fetch_add(1, std::memory_order_acq_rel); }
 
 
 // Tile selection for the skinny GEMM.  NT = output tiles per wave, KW = waves splitting K.
-// Defaults come from the gfx950 sweep in tools/tune_gemm.py; DSSE_GEMM_NT / DSSE_GEMM_KW override.
+// Defaults come from the gfx950 sweep in tools/tune_gemm.py; DSSE_KERNEL_CFG gemm_nt / gemm_kw override.
 void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
   mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   nt = 1;
   const int chunks = K / 128;
   kw = chunks >= 32 ? 8 : 4;
-  const int e_nt = env_int("DSSE_GEMM_NT", 0), e_kw = env_int("DSSE_GEMM_KW", 0);
+  const int e_nt = env_int("gemm_nt", 0), e_kw = env_int("gemm_kw", 0);
   if (e_nt) nt = e_nt;
   if (e_kw) kw = e_kw;
   if (mt == 4 && nt == 2 && kw == 8) kw = 4;  // spill guard (see gemm_skinny.hip)
@@ -96,8 +111,7 @@ void pick_tiles(int M, int N, int K, int mode, int& mt, int& nt, int& kw) {
   (void)mode;
 }
 
-// X-streaming kernel configuration (gemm_stream.hip).  Env overrides: DSSE_S_NT, DSSE_S_NW, DSSE_S_RD,
-// DSSE_S_SPLIT.
+// X-streaming kernel configuration (gemm_stream.hip).  DSSE_KERNEL_CFG overrides: s_nt, s_nw, s_rd, s_split.
 struct SCfg {
   int mt, nt, nw, rd, S;
   bool ok;
@@ -108,23 +122,23 @@ struct SCfg {
 SCfg pick_stream(int M, int N, int K, int mode = -1) {
   SCfg c{};
   c.mt = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : (M <= 256 ? 16 : 4))));
-  c.nt = M > 256 ? 1 : env_int("DSSE_S_NT", 1);  // row blocks (M > 256) are instantiated for nt = 1
+  c.nt = M > 256 ? 1 : env_int("s_nt", 1);  // row blocks (M > 256) are instantiated for nt = 1
   // 8 waves per workgroup when that still gives ~one workgroup per CU without split-K (gate_up,
   // LM head), else 4 (narrow O / down / QKV: more, shorter workgroups; measured, profiles/gemm_stream_r1.md)
-  c.nw = env_int("DSSE_S_NW", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
+  c.nw = env_int("s_nw", (N / (16 * c.nt)) / 8 >= 192 ? 8 : 4);
   if (c.nt == 2 && c.mt <= 4) c.nw = 8;  // instantiated (nt, nw): (1, 8), (2, 8), (1, 4) — gemm_stream.hip
   if (c.nt == 2 && c.mt >= 8) c.nw = 4;   // mt 8 / 16: (1, 8), (1, 4), (2, 4)
   // 7 waves when that puts exactly one workgroup on each CU where 8 leaves CUs idle (gate_up at TP = 1:
   // 1792 tile groups -> 256 instead of 224 workgroups; 51.1 vs 56.0 us at M = 64, profiles/gemm_nw_r1.md)
   const int tg1 = N / 16;
-  if (env_int("DSSE_S_NW", 0) == 0 && c.mt == 4 && c.nt == 1 && M <= 64 && c.nw == 8 && tg1 % 8 == 0 &&
+  if (env_int("s_nw", 0) == 0 && c.mt == 4 && c.nt == 1 && M <= 64 && c.nw == 8 && tg1 % 8 == 0 &&
       tg1 / 8 < 256 && tg1 % 7 == 0 && tg1 / 7 <= 256)
     c.nw = 7;
   const bool odd_nw = c.mt == 4 && c.nt == 1 && M <= 64 && c.nw >= 2 && c.nw <= 7;  // (4, 1, 2..7, rd 1)
   if (c.nw != 4 && !odd_nw) c.nw = 8;
   if (N % (16 * c.nt) != 0 || (N / (16 * c.nt)) % c.nw != 0) c.nt = 1;
   if ((N / 16) % c.nw != 0) c.nw = 4;
-  c.rd = env_int("DSSE_S_RD", 1);
+  c.rd = env_int("s_rd", 1);
   if (c.nt == 2 || c.rd != 2 || M > 64 || (c.nw != 4 && c.nw != 8)) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
   if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
@@ -132,7 +146,7 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
   c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
   if (!c.ok) return c;
   const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
-  int S = env_int("DSSE_S_SPLIT", 0);
+  int S = env_int("s_split", 0);
   if (S <= 0 || slices % S != 0) {
     // smallest split that gives ~one workgroup per CU (256 CUs), never more than 1.25x that
     S = 1;
@@ -149,19 +163,19 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
 
 // gemm_stream launch, or its LDS-DMA ring form (gemm_ring_kernel) where that applies: 33-64 rows, one 16-column
 // tile per wave: 4 slots with 4 waves per workgroup, 3 slots with 7 / 8 (the 7-8-wave shapes; LDS; gate_up on 7
-// waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8).  DSSE_S_RING=0 turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
+// waves = 256 workgroups: 64-stream step 4.38 vs 4.50 ms with 8).  s_ring=0 (DSSE_KERNEL_CFG) turns it off.  Measured on MI355X, 64-stream step: 4.51 / 4.52 ms vs 4.61 / 4.63 on gemm_stream; 5 slots at 4
 // waves 4.55 / 4.66 (gate_up 45.8 -> 43.5 us, LM head 52.5 -> 48.3; profiles/r2/ring_*.log).
-// Ring GEMM variant: DSSE_RING2 unset = the decoupled-look-ahead kernel (gemm_ring2) for 65-128 rows only
+// Ring GEMM variant: ring2 (DSSE_KERNEL_CFG) unset = the decoupled-look-ahead kernel (gemm_ring2) for 65-128 rows only
 // (128-stream step 6.19-6.22 vs 6.32-6.34 ms; at 33-64 rows 4.44 vs 4.40 ms: profiles/r3/ring2_ab.log,
 // step_p64_r{0,2}.md), 1 = every shape it is instantiated for, 0 = never.
 int ring2_for(int M) {
-  const int v = env_int("DSSE_RING2", -1);
+  const int v = env_int("ring2", -1);
   return v == 0 ? 0 : (v == 1 ? 1 : (M > 64 ? 1 : 0));
 }
 
 hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const void* X, int M, const void* W, int K,
                          int N, const dsse::GemmEpi* ep, float* part) {
-  const int ring = env_int("DSSE_S_RING", 1);
+  const int ring = env_int("s_ring", 1);
   // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
   const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32) ||
                          (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4);
@@ -179,7 +193,7 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
 }
 
 // Wide-batch kernel configuration (gemm_wide.hip, 32x32x16 MFMAs, 128 columns per workgroup).  Env
-// overrides: DSSE_W_SPLIT, DSSE_W_RD.
+// overrides (DSSE_KERNEL_CFG): w_split, w_rd.
 struct WCfg {
   int mb, rd, S;
   bool ok;
@@ -188,13 +202,13 @@ WCfg pick_wide(int M, int N, int K) {
   WCfg c{};
   c.mb = M <= 128 ? 4 : 8;
   const int cps = c.mb == 8 ? 1 : 2;
-  c.rd = env_int("DSSE_W_RD", c.mb == 8 ? 2 : 1);
+  c.rd = env_int("w_rd", c.mb == 8 ? 2 : 1);
   if (c.mb == 8 && c.rd != 3) c.rd = 2;
   if (c.mb == 4 && c.rd != 2) c.rd = 1;
   c.ok = M <= 256 && N % 128 == 0 && K % (128 * cps) == 0;
   if (!c.ok) return c;
   const int wgs = N / 128, slices = K / (128 * cps);
-  int S = env_int("DSSE_W_SPLIT", 0);
+  int S = env_int("w_split", 0);
   if (S <= 0 || slices % S != 0) {
     S = 1;
     for (int d = 1; d <= slices; ++d) {
@@ -217,15 +231,15 @@ hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X,
 
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
-// Tiled LDS-DMA GEMM (gemm_tiled.hip; prefill and wide batches).  Env overrides: DSSE_T_CFG (0 = 256x128,
-// 1 = 128x128, 2 = 256x64 tile), DSSE_T_SPLIT.
+// Tiled LDS-DMA GEMMs (gemm_tiled.hip, gemm_pipe.hip; prefill and wide batches).  DSSE_KERNEL_CFG overrides: t_cfg
+// (0 = 256x128, 1 = 128x128, 5 = 128x256, 8 = 256x256 gemm_pipe), t_split.
 struct TCfg {
   int cfg, S;
   bool ok;
 };
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
-  int cfg = env_int("DSSE_T_CFG", -1);
+  int cfg = env_int("t_cfg", -1);
   if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8) {
     // round 5 (profiles/r5/gemm_pipe_r5.md): the 256x256 tile of gemm_pipe.hip (cfg 8: 8 waves, every LDS-DMA
     // half-tile five phases ahead of its wait) once it yields >= ~160 workgroups -- 1.35-1.40 PFLOP/s at 8192 rows,
@@ -259,7 +273,7 @@ TCfg pick_tiled(int M, int N, int K) {
   c.ok = N % BN == 0 && K % (cfg == 8 ? 128 : 64) == 0;
   if (!c.ok) return c;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  int S = env_int("DSSE_T_SPLIT", 0);
+  int S = env_int("t_split", 0);
   const int kq = cfg == 8 ? 128 : 64;  // K granule of a slice (gemm_pipe: >= 2 steps of 64)
   if (S <= 0 || K % (kq * S) != 0) {
     S = 1;  // split K only for the few-tile wide-decode shapes (slabs cost M x N x 4 B each)
@@ -271,9 +285,9 @@ TCfg pick_tiled(int M, int N, int K) {
 
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 2 = X streamed through LDS
 // slices (gemm_stream.hip), 3 = gemm_wide.hip (32x32 MFMAs), 4 = gemm_tiled.hip (register-blocked, LDS-DMA).
-// DSSE_GEMM_IMPL forces one (1, the removed whole-slice X-in-LDS kernel, maps to the fallback).
+// gemm_impl (DSSE_KERNEL_CFG) forces one (1, the removed whole-slice X-in-LDS kernel, maps to the fallback).
 int gemm_impl(int M, int N, int K) {
-  const int impl = env_int("DSSE_GEMM_IMPL", -1);
+  const int impl = env_int("gemm_impl", -1);
   if (M > 64) {
     // every branch returns a kernel whose shape contract holds (or -1): prefill calls arrive with any M and
     // tensor-parallel shard shapes
@@ -411,9 +425,9 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
     }
   } else if (impl == 2) {
     SCfg c = pick_stream(M, N, K);
-    // 17-64 rows on the ring: DSSE_RESID_NW / DSSE_RESID_SPLIT = waves per workgroup and K split of the O / down
+    // 17-64 rows on the ring: resid_nw / resid_split (DSSE_KERNEL_CFG) = waves per workgroup and K split of the O / down
     // projections (more K slices: fewer X bytes per workgroup, more slab bytes for the norm)
-    const int rnw = env_int("DSSE_RESID_NW", 0), rsp = env_int("DSSE_RESID_SPLIT", 0);
+    const int rnw = env_int("resid_nw", 0), rsp = env_int("resid_split", 0);
     if (M > 32 && M <= 64 && rnw > 0 && rsp > 1 && (N / 16) % rnw == 0 && K % (128 * rsp) == 0) {
       c.ring_nw = rnw;
       c.S = rsp;
@@ -562,18 +576,6 @@ void decode_prep(const Tensor& active, const Tensor& positions, const Tensor& bl
 
 // Warm the Infinity Cache with the first `bytes` of `t` (all of it when bytes < 0) on `wgs` workgroups; `sink`:
 // an int32 tensor of >= 1024 words the kernel never writes in practice (it keeps the loads alive).
-void prefetch(const Tensor& t, Tensor& sink, int64_t bytes, int64_t wgs) {
-  check_gpu(t, "t");
-  check_gpu(sink, "sink");
-  check_dtype(sink, at::kInt, "sink");
-  TORCH_CHECK(t.is_contiguous(), "prefetch needs a contiguous tensor");
-  TORCH_CHECK(sink.numel() >= 1024, "sink must hold 1024 words");
-  const int64_t total = t.numel() * t.element_size();
-  const int64_t n = bytes < 0 ? total : std::min(bytes, total);
-  DSSE_CHECK_HIP(dsse_prefetch(t.data_ptr(), n, (int)std::max<int64_t>(1, std::min<int64_t>(wgs, 1024)),
-                               reinterpret_cast<unsigned*>(sink.data_ptr<int>()), cur_stream()));
-}
-
 void ring_advance(Tensor& counter) {
   check_gpu(counter, "counter");
   check_dtype(counter, at::kInt, "counter");
@@ -631,9 +633,9 @@ dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cach
   p.part = (int)part;
   p.nparts = (int)nparts;
   p.scale_log2 = 1.4426950408889634f / sqrtf(128.f);
-  const int env_kwv = env_int("DSSE_ATTN_KWV", 0);
+  const int env_kwv = env_int("attn_kwv", 0);
   p.kwv = (env_kwv == 1 || env_kwv == 2 || env_kwv == 4 || env_kwv == 8) ? env_kwv : 0;
-  const int env_pd = env_int("DSSE_ATTN_PD", 0);
+  const int env_pd = env_int("attn_pd", 0);
   p.pd = (env_pd == 1 || env_pd == 2) ? env_pd : 0;
   return p;
 }
@@ -662,13 +664,13 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
 // leaves fp32 split-K slabs in `slabs` and attention mode 3 sums them, applies RoPE, writes this step's K / V
 // into the cache and attends -- one launch (the split-K reduce) fewer per layer.  Falls back to gemm_qkv_rope
 // + decode attention when the chosen GEMM cannot leave slabs (the register-streaming kernel of tiny batches),
-// for GQA groups other than 1, 2, 4 heads, when `slabs` is too small, or with DSSE_FUSED_QKV_ATTN=0.  Returns the number of slabs (0 = fallback).
+// for GQA groups other than 1, 2, 4 heads, when `slabs` is too small, or with fused_qkv_attn=0 (DSSE_KERNEL_CFG).  Returns the number of slabs (0 = fallback).
 int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& positions, const Tensor& slots,
                              const Tensor& rope, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, int64_t nh,
                              int64_t nkv, Tensor& slabs, const Tensor& block_tables, const Tensor& q_start,
                              const Tensor& q_len, const Tensor& ctx_len, const Tensor& work_seq,
                              const Tensor& work_tile, Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t part,
-                             int64_t nparts, int64_t slabs_ready) {
+                             int64_t nparts) {
   check_gpu(x, "x");
   check_gpu(w, "w");
   check_gpu(slabs, "slabs");
@@ -678,23 +680,19 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
                         N == (nh + 2 * nkv) * 128;
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
   int S = 0;
-  if (slabs_ready > 0) S = (int)slabs_ready;  // the persistent MLP kernel already wrote the QKV slabs (decode_mega.hip)
-  else if (impl == 4) S = pick_tiled(M, N, K).S;
+  if (impl == 4) S = pick_tiled(M, N, K).S;
   else if (impl == 3) S = pick_wide(M, N, K).S;
   else if (impl == 2) {
     S = pick_stream(M, N, K, dsse::kQkvRope).S;
-    // DSSE_QKV_SPLIT: split-K of the QKV projection alone (its slabs are read by the attention kernel)
-    const int qs = env_int("DSSE_QKV_SPLIT", 0);
+    // qkv_split (DSSE_KERNEL_CFG): split-K of the QKV projection alone (its slabs are read by the attention kernel)
+    const int qs = env_int("qkv_split", 0);
     const int slices = K / (128 * ((M <= 64 || M > 256) ? 4 : (M <= 128 ? 2 : 1)));  // gemm_stream.hip stream_cps
     if (qs > 0 && slices % qs == 0) S = qs;
   }
   auto q3 = q_out.view({-1, nh, 128});
   auto o3 = out.view({-1, nh, 128});
   const bool group_ok = nkv > 0 && nh % nkv == 0 && (nh / nkv == 1 || nh / nkv == 2 || nh / nkv == 4);  // attention.hip
-  TORCH_CHECK(slabs_ready <= 0 || (group_ok && slabs.numel() >= (int64_t)S * M * N),
-              "qkv_attention_decode: slabs_ready needs a GQA group of 1 / 2 / 4 and S x M x N slabs");
-  if (slabs_ready <= 0 &&
-      (S <= 0 || !group_ok || slabs.numel() < (int64_t)S * M * N || env_int("DSSE_FUSED_QKV_ATTN", 1) == 0)) {
+  if ((S <= 0 || !group_ok || slabs.numel() < (int64_t)S * M * N || env_int("fused_qkv_attn", 1) == 0)) {
     gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv);
     paged_attention(0, q3, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq, work_tile, o3, part_o,
                     part_ml, part, nparts);
@@ -717,9 +715,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   dsse::GemmEpi ep{};
   const void* X = x.data_ptr();
   float* sl = slabs.data_ptr<float>();
-  if (slabs_ready > 0) {
-    // slabs written by an earlier kernel on this stream
-  } else if (impl == 4) {
+  if (impl == 4) {
     const TCfg c = pick_tiled(M, N, K);
     DSSE_CHECK_HIP(tiled_call(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl));
   } else if (impl == 3) {
@@ -741,27 +737,6 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   p.v_out = reinterpret_cast<bf16*>(v_cache.data_ptr());
   DSSE_CHECK_HIP(dsse_paged_attention(3, (int)work_seq.numel(), &p, cur_stream()));
   return S;
-}
-
-// The decode QKV projection alone, as S fp32 split-K slabs [S, M, N] in `slabs` (the layer-0 input of the persistent
-// layer kernel, decode_mega.hip: every later layer's slabs come from the previous layer's launch).  Returns S.
-int64_t gemm_qkv_slabs(const Tensor& x, const Tensor& w, Tensor& slabs) {
-  check_gpu(x, "x");
-  check_gpu(w, "w");
-  check_gpu(slabs, "slabs");
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
-  check_dtype(slabs, at::kFloat, "slabs");
-  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == K && K % 128 == 0 && N % 16 == 0 && M >= 1 && M <= 64,
-              "gemm_qkv_slabs: [M <= 64, K] x [N, K]");
-  const SCfg c = pick_stream(M, N, K, dsse::kQkvRope);
-  TORCH_CHECK(gemm_impl(M, N, K) == 2 && c.ok && c.S > 1, "gemm_qkv_slabs: shape outside the split-K stream kernels");
-  TORCH_CHECK(slabs.numel() >= (int64_t)c.S * M * N, "gemm_qkv_slabs: slabs too small");
-  dsse::GemmEpi ep{};
-  DSSE_CHECK_HIP(stream_launch(dsse::kQkvRope, c, c.S, 1, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
-                               slabs.data_ptr<float>()));
-  return c.S;
 }
 
 dsse::SampleParams sample_params(const Tensor& temperature, const Tensor& top_k, const Tensor& top_p,
@@ -891,121 +866,6 @@ void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, do
                                  reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-// Persistent decode MLP block (decode_mega.hip): O -> residual + RMSNorm -> gate_up + SiLU·mul -> down -> residual +
-// RMSNorm in ONE launch of 256 resident workgroups (one per CU).  Mistral-7B shapes (H 4096, F 14336), TP = 1, M <= 64.
-// sync: int32 [mega_sync_words()] zeroed once, owned by one decode context (never used by two launches at once).
-bool mega_supported() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  return cus == 256;
-}
-int64_t mega_sync_words() { return (int64_t)dsse_mega_sync_words(); }
-void mega_mlp(const Tensor& attn, const Tensor& wo, const Tensor& wgu, const Tensor& wd, Tensor& resid,
-              const Tensor& w_ffn, const Tensor& w_next, Tensor& xm, Tensor& h, Tensor& x, Tensor& slabs, Tensor& sync,
-              Tensor& err, double eps, const c10::optional<Tensor>& wqkv, const c10::optional<Tensor>& qkv_slabs,
-              const c10::optional<Tensor>& qkv_in, int64_t qkv_in_S, const c10::optional<Tensor>& k_cache,
-              const c10::optional<Tensor>& v_cache, const c10::optional<Tensor>& block_tables,
-              const c10::optional<Tensor>& q_len, const c10::optional<Tensor>& ctx_len,
-              const c10::optional<Tensor>& positions, const c10::optional<Tensor>& slots,
-              const c10::optional<Tensor>& rope, const c10::optional<Tensor>& stamps, int64_t pf_steps) {
-  for (const Tensor* t : {&attn, &wo, &wgu, &wd, (const Tensor*)&resid, &w_ffn, &w_next, (const Tensor*)&xm,
-                          (const Tensor*)&h, (const Tensor*)&x, (const Tensor*)&slabs, (const Tensor*)&sync,
-                          (const Tensor*)&err})
-    check_gpu(*t, "mega_mlp tensor");
-  for (const Tensor* t : {&attn, &wo, &wgu, &wd, &w_ffn, &w_next, (const Tensor*)&xm, (const Tensor*)&h,
-                          (const Tensor*)&x})
-    check_dtype(*t, at::kBFloat16, "mega_mlp bf16 tensor");
-  check_dtype(resid, at::kFloat, "resid");
-  check_dtype(slabs, at::kFloat, "slabs");
-  check_dtype(sync, at::kInt, "sync");
-  check_dtype(err, at::kInt, "err");
-  constexpr int H = 4096, F = 14336;
-  const int M = (int)attn.size(0);
-  TORCH_CHECK(attn.dim() == 2 && attn.size(1) == H && M >= 1 && M <= 64, "mega_mlp: attn must be [M <= 64, 4096]");
-  TORCH_CHECK(wo.size(0) == H && wo.size(1) == H && wgu.size(0) == 2 * F && wgu.size(1) == H && wd.size(0) == H &&
-                  wd.size(1) == F, "mega_mlp: weights must be Mistral-7B shaped (tiled layout)");
-  TORCH_CHECK(resid.dim() == 2 && resid.size(0) >= M && resid.size(1) == H, "mega_mlp: resid [>= M, 4096]");
-  TORCH_CHECK(xm.size(0) >= M && xm.size(1) == H && x.size(0) >= M && x.size(1) == H, "mega_mlp: xm / x [>= M, 4096]");
-  TORCH_CHECK(h.size(0) >= M && h.size(1) == F, "mega_mlp: h [>= M, 14336]");
-  TORCH_CHECK(w_ffn.numel() == H && w_next.numel() == H, "mega_mlp: norm weights [4096]");
-  TORCH_CHECK(slabs.numel() >= (int64_t)8 * M * H, "mega_mlp: slabs hold 8 x M x 4096 floats");
-  TORCH_CHECK(sync.numel() >= mega_sync_words(), "mega_mlp: sync block too small");
-  TORCH_CHECK(mega_supported(), "mega_mlp: needs a 256-CU gfx950 device");
-  const bool q = wqkv.has_value() && wqkv->defined();
-  if (q) {
-    TORCH_CHECK(qkv_slabs.has_value() && qkv_slabs->defined(), "mega_mlp: wqkv needs qkv_slabs");
-    check_gpu(*wqkv, "wqkv");
-    check_gpu(*qkv_slabs, "qkv_slabs");
-    check_dtype(*wqkv, at::kBFloat16, "wqkv");
-    check_dtype(*qkv_slabs, at::kFloat, "qkv_slabs");
-    TORCH_CHECK(wqkv->size(0) == 6144 && wqkv->size(1) == H, "mega_mlp: wqkv must be [6144, 4096] (tiled)");
-    TORCH_CHECK(qkv_slabs->numel() >= (int64_t)4 * M * 6144, "mega_mlp: qkv_slabs hold 4 x M x 6144 floats");
-  }
-  dsse::MegaMlpParams p{};
-  p.attn = reinterpret_cast<bf16*>(attn.data_ptr());
-  p.wo = reinterpret_cast<const bf16*>(wo.data_ptr());
-  p.wgu = reinterpret_cast<const bf16*>(wgu.data_ptr());
-  p.wd = reinterpret_cast<const bf16*>(wd.data_ptr());
-  p.resid = resid.data_ptr<float>();
-  p.w_ffn = reinterpret_cast<const bf16*>(w_ffn.data_ptr());
-  p.w_next = reinterpret_cast<const bf16*>(w_next.data_ptr());
-  p.xm = reinterpret_cast<bf16*>(xm.data_ptr());
-  p.h = reinterpret_cast<bf16*>(h.data_ptr());
-  p.x = reinterpret_cast<bf16*>(x.data_ptr());
-  p.slabs = slabs.data_ptr<float>();
-  p.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
-  p.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
-  p.wqkv = q ? reinterpret_cast<const bf16*>(wqkv->data_ptr()) : nullptr;
-  p.qkv_slabs = q ? qkv_slabs->data_ptr<float>() : nullptr;
-  if (qkv_in.has_value() && qkv_in->defined()) {
-    // the layer's decode attention as the first phase (GQA 32 / 8 heads, page 32, one query per sequence)
-    for (const c10::optional<Tensor>* t : {&k_cache, &v_cache, &block_tables, &q_len, &ctx_len, &positions, &slots, &rope})
-      TORCH_CHECK(t->has_value() && (*t)->defined(), "mega_mlp: the attention phase needs every attention tensor");
-    for (const Tensor* t : {&*qkv_in, &*k_cache, &*v_cache, &*block_tables, &*q_len, &*ctx_len, &*positions, &*slots,
-                            &*rope})
-      check_gpu(*t, "mega_mlp attention tensor");
-    check_dtype(*qkv_in, at::kFloat, "qkv_in");
-    check_dtype(*rope, at::kFloat, "rope");
-    for (const Tensor* t : {&*block_tables, &*q_len, &*ctx_len, &*positions, &*slots}) check_dtype(*t, at::kInt, "metadata");
-    check_dtype(*k_cache, at::kBFloat16, "k_cache");
-    check_dtype(*v_cache, at::kBFloat16, "v_cache");
-    TORCH_CHECK(qkv_in_S >= 1 && qkv_in->numel() >= qkv_in_S * M * 6144, "mega_mlp: qkv_in holds S x M x 6144 floats");
-    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == 8 && k_cache->size(2) == dsse::kBS && k_cache->size(3) == 128,
-                "mega_mlp: k_cache [blocks, 8, 32, 128]");
-    TORCH_CHECK(v_cache->sizes() == at::IntArrayRef({k_cache->size(0), 8, 128, dsse::kBS}), "mega_mlp: v_cache [blocks, 8, 128, 32]");
-    TORCH_CHECK(block_tables->dim() == 2 && block_tables->size(0) >= M, "mega_mlp: block_tables [>= M, max_blocks]");
-    TORCH_CHECK(q_len->numel() >= M && ctx_len->numel() >= M && positions->numel() >= M && slots->numel() >= M,
-                "mega_mlp: per-row metadata too short");
-    TORCH_CHECK(rope->dim() == 3 && rope->size(1) == 64 && rope->size(2) == 2, "mega_mlp: rope [P, 64, 2]");
-    p.qkv_in = qkv_in->data_ptr<float>();
-    p.qkv_in_S = (int)qkv_in_S;
-    p.k_cache = reinterpret_cast<bf16*>(k_cache->data_ptr());
-    p.v_cache = reinterpret_cast<bf16*>(v_cache->data_ptr());
-    p.block_tables = block_tables->data_ptr<int>();
-    p.max_blocks = (int)block_tables->size(1);
-    p.num_blocks = (int)k_cache->size(0);
-    p.num_slots = (int)(k_cache->size(0) * dsse::kBS);
-    p.q_len = q_len->data_ptr<int>();
-    p.ctx_len = ctx_len->data_ptr<int>();
-    p.positions = positions->data_ptr<int>();
-    p.slots = slots->data_ptr<int>();
-    p.rope = reinterpret_cast<const float2*>(rope->data_ptr<float>());
-    p.rope_len = (int)rope->size(0);
-    p.scale_log2 = 1.4426950408889634f / std::sqrt(128.f);
-  }
-  if (stamps.has_value() && stamps->defined()) {
-    check_gpu(*stamps, "stamps");
-    check_dtype(*stamps, at::kLong, "stamps");
-    TORCH_CHECK(stamps->numel() >= 256 * 16, "mega_mlp: stamps hold 256 x 16 int64");
-    p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
-  }
-  p.pf_steps = pf_steps < 0 ? 4 : (int)std::min<int64_t>(pf_steps, 4);  // seam prefetch steps (decode_mega.hip kPF)
-  p.M = M;
-  p.eps = (float)eps;
-  DSSE_CHECK_HIP(dsse_mega_mlp(&p, cur_stream()));
-}
-
 int64_t kernels_abi_version() { return 13; }
 
 #if DSSE_KERNEL_CHECKS
@@ -1053,14 +913,13 @@ TORCH_LIBRARY(dsse, m) {
   m.def("decode_prep(Tensor active, Tensor positions, Tensor block_tables, Tensor(a!) slots, "
         "Tensor(b!) ctx_len, Tensor(c!) q_len, int num_blocks=2147483647) -> ()");
   m.def("ring_advance(Tensor(a!) counter) -> ()");
-  m.def("prefetch(Tensor t, Tensor(a!) sink, int bytes, int wgs) -> ()");
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
         "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
   m.def("qkv_attention_decode(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor(d!) slabs, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(e!) out, "
-        "Tensor(f!) part_o, Tensor(g!) part_ml, int part, int nparts, int slabs_ready=0) -> int");
+        "Tensor(f!) part_o, Tensor(g!) part_ml, int part, int nparts) -> int");
   m.def("sample_candidates(Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds, "
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
@@ -1070,15 +929,6 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
   m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
         "Tensor(c!) epoch, Tensor(d!) err) -> ()");
-  m.def("gemm_qkv_slabs(Tensor x, Tensor w, Tensor(a!) slabs) -> int");
-  m.def("mega_supported() -> bool", &mega_supported);
-  m.def("mega_sync_words() -> int", &mega_sync_words);
-  m.def("mega_mlp(Tensor attn, Tensor wo, Tensor wgu, Tensor wd, Tensor(a!) resid, Tensor w_ffn, Tensor w_next, "
-        "Tensor(b!) xm, Tensor(c!) h, Tensor(d!) x, Tensor(e!) slabs, Tensor(f!) sync, Tensor(g!) err, float eps, "
-        "Tensor? wqkv=None, Tensor(h!)? qkv_slabs=None, Tensor? qkv_in=None, int qkv_in_S=0, "
-        "Tensor(i!)? k_cache=None, Tensor(j!)? v_cache=None, Tensor? block_tables=None, Tensor? q_len=None, "
-        "Tensor? ctx_len=None, Tensor? positions=None, Tensor? slots=None, Tensor? rope=None, "
-        "Tensor(k!)? stamps=None, int pf_steps=-1) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
@@ -1096,12 +946,9 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("decode_prep", &decode_prep);
   m.impl("ring_advance", &ring_advance);
-  m.impl("prefetch", &prefetch);
   m.impl("paged_attention", &paged_attention);
   m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
   m.impl("ar_rmsnorm", &ar_rmsnorm);
-  m.impl("mega_mlp", &mega_mlp);
-  m.impl("gemm_qkv_slabs", &gemm_qkv_slabs);
 }

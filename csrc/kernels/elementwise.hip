@@ -296,30 +296,6 @@ extern "C" hipError_t dsse_decode_prep(int B, const int* active, const int* posi
   return hipGetLastError();
 }
 
-// Read a byte range and discard it: pulls weights into the memory-side Infinity Cache (MALL, 256 MB, shared by
-// the XCDs) ahead of the kernel that streams them (default cache policy: the lines allocate).  4 x 16 B loads in
-// flight per thread; the XOR of the first words feeds a store that never happens, so the loads stay.
-__global__ void __launch_bounds__(256) prefetch_kernel(const uint4* __restrict__ src, int64_t n16, unsigned* sink) {
-  unsigned acc = 0;
-  const int64_t stride = (int64_t)gridDim.x * 1024;
-  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[min(i + 256 * u, n16 - 1)];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc ^= v[u].x;
-  }
-  if (acc == 0x9E3779B9u && threadIdx.x == 0) sink[blockIdx.x] = acc;
-}
-
-extern "C" hipError_t dsse_prefetch(const void* src, int64_t bytes, int wgs, unsigned* sink, hipStream_t st) {
-  const int64_t n16 = bytes / 16;
-  if (n16 <= 0) return hipSuccess;
-  const int grid = (int)std::min<int64_t>(wgs, (n16 + 1023) / 1024);
-  hipLaunchKernelGGL(prefetch_kernel, dim3(grid), dim3(256), 0, st, reinterpret_cast<const uint4*>(src), n16, sink);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t dsse_ring_advance(int* counter, hipStream_t st) {
   hipLaunchKernelGGL(ring_advance_kernel, dim3(1), dim3(1), 0, st, counter);
   return hipGetLastError();

@@ -51,36 +51,8 @@ PREFILL_GRAPH_SEQS = 16  # sequences per captured prefill batch (more: eager)
 DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
 # Health words (runner.health, int32 on the device, copied to the host with every drained step; nonzero = the step's
 # outputs cannot be trusted and the engine fails: engine.py EngineFault).
-HEALTH_MEGA_WAIT = 0    # a bounded wait inside the persistent decode MLP kernel timed out (decode_mega.hip)
-HEALTH_TP_PEER = 1      # a TP peer's all-reduce row did not arrive in time (allreduce.hip)
-HEALTH_WORDS = ("persistent decode kernel wait timed out", "TP peer all-reduce wait timed out")
-
-
-def mega_reason(runner) -> str:
-    """Why the persistent decode MLP kernel (csrc/kernels/decode_mega.hip) is NOT used ("" = it is).
-
-    It runs the O / gate_up / down projections and both norms of a layer in one launch of 256 workgroups that must all
-    be resident at once (one per CU), so it needs the Mistral-7B MLP shapes at TP = 1, a 256-CU device, and a GPU this
-    process does not share with other ranks (DSSE_GPU_SHARED=1, or more local ranks than devices, turns it off: two
-    processes' persistent grids on one device could each hold half the CUs).  Opt-in (DSSE_MEGA=1): it is correct on
-    MI355X (tests/test_mega_gpu.py) but measured slower than the launch-per-op path (profiles/r4/mega_r4.md)."""
-    if os.environ.get("DSSE_MEGA", "0") != "1":
-        return "DSSE_MEGA is not 1"
-    if runner.device.type != "cuda":
-        return "not on a GPU"
-    if runner.comm.size > 1:
-        return "TP > 1"
-    w = runner.w
-    if runner.cfg.hidden_size != 4096 or w.ffn != 14336:
-        return "not the Mistral-7B MLP shape"
-    if os.environ.get("DSSE_GPU_SHARED", "0") == "1":
-        return "DSSE_GPU_SHARED=1"
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-    if local_world > max(1, torch.cuda.device_count()):
-        return "several ranks share a GPU"
-    if not ops.mega_supported():
-        return "device is not a 256-CU gfx950"
-    return ""
+HEALTH_TP_PEER = 0      # a TP peer's all-reduce row did not arrive in time (allreduce.hip)
+HEALTH_WORDS = ("TP peer all-reduce wait timed out",)
 
 
 # TP prefill: the row-independent post-attention half of each layer (O -> all-reduce -> norm -> gate_up -> down ->
@@ -97,12 +69,6 @@ def prefill_row_chunks(T: int, tp: int) -> list:
 
 # prompt passes up to this many rows send the residual projections' split-K slabs to the norm (_prefill_resid)
 PREFILL_SLAB_ROWS = 512
-
-
-# decode buckets run on the persistent MLP kernel (rows <= 64; smaller buckets keep the launch-per-op path unless
-# DSSE_MEGA_MIN_B lowers the bound)
-MEGA_MIN_B = int(os.environ.get("DSSE_MEGA_MIN_B", "33"))
-MEGA_MAX_B = 64
 
 
 def mixed_mode() -> str:
@@ -199,11 +165,6 @@ class ModelRunner:
             slab_floats = max(slab_floats, 8 * min(PREFILL_SLAB_ROWS, max_prefill_tokens) * H)
         self.split_part = torch.zeros(slab_floats, device=dev, dtype=torch.float32)
         self.health = torch.zeros(4, device=dev, dtype=torch.int32)
-        self.mega_reason = mega_reason(self)
-        self.mega = not self.mega_reason and Bm >= MEGA_MIN_B
-        if self.mega:
-            self.xm = torch.zeros(min(Bm, MEGA_MAX_B), H, **bf)
-            self.mega_sync = ops.mega_sync(dev)
         self.logits = torch.zeros(Bm, V, device=dev, dtype=torch.float32)
         nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
         self._cand = {b: torch.zeros(b, nch, 2, device=dev, dtype=torch.float32) for b in batch_buckets(Bm)}
@@ -243,27 +204,6 @@ class ModelRunner:
         if B > DECODE_GEMM_MAX_M:
             self._decode_layers_wide(B, resid, x, part, nparts)
             return
-        if self.mega and MEGA_MIN_B <= B <= MEGA_MAX_B:
-            # two launches per layer: the folded decode attention (QKV slab sum + RoPE + K/V write + attention), then
-            # the persistent block (decode_mega.hip): O -> norm -> gate_up -> down -> norm -> the NEXT layer's QKV
-            # projection, one launch whose weight stream runs across every seam.  Layer 0's QKV is its own launch.
-            fused_qkv = os.environ.get("DSSE_MEGA_QKV", "1") != "0"
-            # attention inside the persistent launch measured slower than its own launch (profiles/r4/mega_r4.md)
-            if fused_qkv and os.environ.get("DSSE_MEGA_ATTN", "0") == "1":
-                self._decode_layers_mega(B, resid, x)
-                return
-            for li, L in enumerate(w.layers):
-                self._qkv_attention(li, L, B, x, part, nparts, slabs_ready=4 if (fused_qkv and li > 0) else 0)
-                nxt = w.layers[li + 1] if li + 1 < nl else None
-                ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm,
-                             nxt.attn_norm if nxt is not None else w.final_norm, self.xm[r], self.h[r], x,
-                             self.split_part, self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps,
-                             wqkv=nxt.wqkv_t if (fused_qkv and nxt is not None) else None,
-                             qkv_slabs=self.split_part)
-            ops.gemm_out(x, w.lm_head_t, self.logits[r])
-            self._sample_commit(B)
-            ops.ring_advance(self.ring_counter)
-            return
         for li, L in enumerate(w.layers):
             self._qkv_attention(li, L, B, x, part, nparts)
             if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
@@ -280,28 +220,6 @@ class ModelRunner:
             else:
                 ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
                 comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps)
-        ops.gemm_out(x, w.lm_head_t, self.logits[r])
-        self._sample_commit(B)
-        ops.ring_advance(self.ring_counter)
-
-    def _decode_layers_mega(self, B: int, resid, x) -> None:
-        """ONE launch per layer (decode_mega.hip with its attention phase): the layer's decode attention on the QKV slabs
-        the previous launch left (slab sum + RoPE + the step's K / V + paged attention), O -> norm -> gate_up -> down ->
-        norm, and the next layer's QKV projection; layer 0's QKV slabs come from one GEMM launch before the loop."""
-        w, eps = self.w, self.cfg.rms_eps
-        r = slice(0, B)
-        nl = len(w.layers)
-        S = ops.gemm_qkv_slabs(x, w.layers[0].wqkv_t, self.split_part)
-        for li, L in enumerate(w.layers):
-            nxt = w.layers[li + 1] if li + 1 < nl else None
-            att = dict(qkv_in=self.split_part, qkv_in_S=S, k_cache=self.kv.k[li], v_cache=self.kv.v[li],
-                       block_tables=self.block_tables[r], q_len=self.q_len[r], ctx_len=self.ctx_len[r],
-                       positions=self.positions[r], slots=self.slots[r], rope=self.rope)
-            ops.mega_mlp(self.attn[r], L.wo_t, L.wgu_t, L.wd_t, resid, L.ffn_norm,
-                         nxt.attn_norm if nxt is not None else w.final_norm, self.xm[r], self.h[r], x, self.split_part,
-                         self.mega_sync, self.health[HEALTH_MEGA_WAIT:HEALTH_MEGA_WAIT + 1], eps,
-                         wqkv=nxt.wqkv_t if nxt is not None else None, qkv_slabs=self.split_part, attention=att)
-            S = 4
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
@@ -333,7 +251,7 @@ class ModelRunner:
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)
 
-    def _qkv_attention(self, li: int, L, B: int, x, part: int, nparts: int, slabs_ready: int = 0) -> None:
+    def _qkv_attention(self, li: int, L, B: int, x, part: int, nparts: int) -> None:
         """QKV projection + RoPE + KV write + decode attention of layer li.  The projection's split-K slabs go
         to split_part (free here: the previous norm consumed it) and the attention kernel folds their reduction,
         RoPE and the K/V write in (ops.qkv_attention_decode)."""
@@ -342,7 +260,7 @@ class ModelRunner:
         ops.qkv_attention_decode(x, L.wqkv_t, self.positions[r], self.slots[r], self.rope, self.q[r], self.kv.k[li],
                                  self.kv.v[li], nh, nkv, self.split_part, self.block_tables[r], self.q_start[r],
                                  self.q_len[r], self.ctx_len[r], self.work_seq[r], self.work_tile[r], self.attn[r],
-                                 self.part_o, self.part_ml, part, nparts, slabs_ready)
+                                 self.part_o, self.part_ml, part, nparts)
 
     def _resid_proj(self, a, wt, resid, norm_w, x, tmp) -> None:
         """resid += a·wᵀ (TP: all-reduced), then x = RMSNorm(resid)·norm_w.  TP = 1: split-K slabs (if the GEMM

@@ -102,6 +102,23 @@ def gemm_resid_split(x, w, resid, part) -> int:
     return 0
 
 
+def kernel_cfg_env(**overrides) -> str:
+    """The DSSE_KERNEL_CFG string (the kernel library's one configuration override: "key=value,..."; keys in
+    csrc/kernels/bindings.cpp env_int, e.g. gemm_impl, t_cfg, s_nw) with `overrides` merged into the current value.
+    Set it in the environment, then call refresh_env()."""
+    cur = {}
+    for item in os.environ.get("DSSE_KERNEL_CFG", "").replace(";", ",").replace(" ", ",").split(","):
+        if "=" in item:
+            k, v = item.split("=", 1)
+            cur[k.strip().lower()] = v.strip()
+    for k, v in overrides.items():
+        if v is None:
+            cur.pop(k, None)
+        else:
+            cur[k] = str(v)
+    return ",".join(f"{k}={v}" for k, v in cur.items())
+
+
 def refresh_env() -> None:
     """Re-read the DSSE_* kernel tuning variables (cached by the library on first use)."""
     if load_library():
@@ -137,17 +154,6 @@ def decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_bloc
         ref.decode_prep(active, positions, block_tables, slots, ctx_len, q_len)
 
 
-def prefetch(t, sink, nbytes: int = -1, wgs: int = 256):
-    """Pull the first `nbytes` of `t` into the GPU's Infinity Cache ahead of the kernel that streams it (HIP only;
-    a no-op elsewhere).  `sink`: int32 [1024] scratch (prefetch_sink())."""
-    if _hip(t):
-        torch.ops.dsse.prefetch(t, sink, nbytes, wgs)
-
-
-def prefetch_sink(device):
-    return torch.zeros(1024, dtype=torch.int32, device=device)
-
-
 def ring_advance(counter):
     if _hip(counter):
         torch.ops.dsse.ring_advance(counter)
@@ -168,57 +174,19 @@ def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx
 
 
 def qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, slabs, block_tables, q_start,
-                         q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts,
-                         slabs_ready: int = 0) -> int:
+                         q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts) -> int:
     """Decode QKV projection + RoPE + KV write + attention.  HIP: the GEMM leaves fp32 split-K slabs in `slabs`
     and the attention kernel folds the reduction, RoPE and the K/V write in (returns the slab count; 0 = it ran
     gemm_qkv_rope + paged_attention instead).  Same result as those two ops."""
     if _hip(x):
         return int(torch.ops.dsse.qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv,
                                                        slabs, block_tables, q_start, q_len, ctx_len, work_seq,
-                                                       work_tile, out, part_o, part_ml, part, nparts, slabs_ready))
+                                                       work_tile, out, part_o, part_ml, part, nparts))
     B = x.shape[0]
     ref.gemm_qkv_rope(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv)
     ref.paged_attention(0, q_out.view(B, nh, 128), k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work_seq,
                         work_tile, out.view(B, nh, 128), part_o, part_ml, part, nparts)
     return 0
-
-
-def mega_supported() -> bool:
-    """The persistent decode MLP kernel needs a 256-CU gfx950 device (one resident workgroup per CU)."""
-    return torch.cuda.is_available() and load_library() and bool(torch.ops.dsse.mega_supported())
-
-
-def mega_sync(device) -> torch.Tensor:
-    """Counter block of the persistent decode MLP kernel: zeroed once, then owned by one decode context."""
-    load_library(required=True)
-    return torch.zeros(int(torch.ops.dsse.mega_sync_words()), dtype=torch.int32, device=device)
-
-
-def gemm_qkv_slabs(x, w, slabs) -> int:
-    """HIP only: the decode QKV projection as S fp32 split-K slabs in `slabs`; returns S."""
-    _hip(x)
-    return int(torch.ops.dsse.gemm_qkv_slabs(x, w, slabs))
-
-
-def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv=None, qkv_slabs=None,
-             attention=None, stamps=None, pf_steps: int = -1):
-    """Decode MLP block in one launch (HIP, <= 64 rows, Mistral-7B shapes): resid += attn·woᵀ; xm = norm(resid)·w_ffn;
-    h = silu(xm·w_gᵀ)·(xm·w_uᵀ); resid += h·w_dᵀ; x = norm(resid)·w_next; with `wqkv` also the next layer's QKV
-    projection of x as 4 fp32 split-K slabs in `qkv_slabs` (for qkv_attention_decode(..., slabs_ready=4)).  With
-    `attention` = dict(qkv_in, qkv_in_S, k_cache, v_cache, block_tables, q_len, ctx_len, positions, slots, rope) the
-    layer's decode attention runs first in the same launch (folded QKV epilogue, writes `attn` and the step's K / V).
-    `err` [1] int32 is set when a bounded in-kernel wait timed out (the engine's health word).  `stamps` (int64
-    [256, 16], HIP only) receives per-workgroup phase timestamps (100 MHz) for tools/bench_mega.py --stamps;
-    `pf_steps` (0-4, -1 = the default 4) weight steps each compute wave prefetches into L2 / MALL at a seam."""
-    if _hip(attn):
-        a = attention or {}
-        torch.ops.dsse.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, slabs, sync, err, eps, wqkv,
-                                qkv_slabs, a.get("qkv_in"), int(a.get("qkv_in_S", 0)), a.get("k_cache"),
-                                a.get("v_cache"), a.get("block_tables"), a.get("q_len"), a.get("ctx_len"),
-                                a.get("positions"), a.get("slots"), a.get("rope"), stamps, int(pf_steps))
-    else:
-        ref.mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps, wqkv, qkv_slabs)
 
 
 def sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand, vocab_offset=0):

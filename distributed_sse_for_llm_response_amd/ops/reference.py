@@ -149,24 +149,6 @@ def rmsnorm(resid, w, y, eps, delta=None, embed=None, ids=None, part=None, nspli
     y.copy_((r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(y.dtype))
 
 
-def mega_mlp(attn, wo, wgu, wd, resid, w_ffn, w_next, xm, h, x, eps, wqkv=None, qkv_slabs=None):
-    """The persistent decode MLP block (csrc/kernels/decode_mega.hip) as its five unfused ops (+ the next layer's QKV
-    projection as one fp32 slab followed by three zero slabs: the same sum)."""
-    M = attn.shape[0]
-    r = resid[:M]
-    gemm_resid(attn, wo, r)
-    rmsnorm(r, w_ffn, xm[:M], eps)
-    gemm_silu(xm[:M], wgu, h[:M])
-    gemm_resid(h[:M], wd, r)
-    rmsnorm(r, w_next, x[:M], eps)
-    if wqkv is not None:
-        N = wqkv.shape[0]
-        sl = qkv_slabs.view(-1)[: 4 * M * N].view(4, M, N)
-        sl.zero_()
-        sl[0] = x[:M].float() @ untile_weight(wqkv).float().t()
-
-
-# ---------------------------------------------------------------- decode metadata
 def decode_prep(active, positions, block_tables, slots, ctx_len, q_len, num_blocks: int = 2**31 - 1):
     B = active.numel()
     for b in range(B):

@@ -17,7 +17,7 @@ H, F, NH, NKV = 4096, 14336, 32, 8
 
 @pytest.fixture(autouse=True)
 def _tiled(monkeypatch):
-    monkeypatch.setenv("DSSE_GEMM_IMPL", "4")
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(gemm_impl="4"))
     ops.refresh_env()
     yield
     monkeypatch.undo()
@@ -76,7 +76,7 @@ def test_tiled_silu_gate_up(gpu, M):
 @pytest.mark.parametrize("M", [300, 2048])
 def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
     if cfg != "auto":
-        monkeypatch.setenv("DSSE_T_CFG", cfg)
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
         ops.refresh_env()
     g = torch.Generator().manual_seed(M + 2)
     x = _rand((M, H), g, gpu)
@@ -100,8 +100,8 @@ def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
 
 @pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("5", "1"), ("5", "2"), ("8", "1"), ("8", "2"), ("8", "4")])
 def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
-    monkeypatch.setenv("DSSE_T_CFG", cfg)
-    monkeypatch.setenv("DSSE_T_SPLIT", split)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_split=split))
     ops.refresh_env()
     g = torch.Generator().manual_seed(int(cfg) * 10 + int(split))
     for M in (1, 70, 256, 600):
@@ -118,7 +118,7 @@ def test_pipe_schedule_all_epilogues(gpu, monkeypatch, M):
     every LDS-DMA half-tile five phases ahead of its counted wait, LDS-staged bf16 stores): bf16 store, residual add
     and SiLU·mul at Mistral-7B shapes, ragged M included."""
     cfg = "8"
-    monkeypatch.setenv("DSSE_T_CFG", cfg)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
     ops.refresh_env()
     g = torch.Generator().manual_seed(M + 40)
     x = _rand((M, H), g, gpu)

@@ -25,30 +25,30 @@ def _close(a, b, atol, rtol, what=""):
 
 GEMM_CONFIGS = {
     "auto": {},
-    "stream-default": {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": "0"},
-    "stream-nt2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NT": "2"},
-    "stream-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
-    "stream-nw4-split4": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "4"},
-    "ring": {"DSSE_GEMM_IMPL": "2"},
-    "ring-nw4-split2": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "4", "DSSE_S_SPLIT": "2"},
-    "ring-nw8": {"DSSE_GEMM_IMPL": "2", "DSSE_S_NW": "8"},
-    "ring2-all": {"DSSE_GEMM_IMPL": "2", "DSSE_RING2": "1"},
-    "ring1-all": {"DSSE_GEMM_IMPL": "2", "DSSE_RING2": "0"},
-    "wide-default": {"DSSE_GEMM_IMPL": "3"},
-    "wide-split2-rd": {"DSSE_GEMM_IMPL": "3", "DSSE_W_SPLIT": "2", "DSSE_W_RD": "3"},
-    "tiled-default": {"DSSE_GEMM_IMPL": "4"},
-    "tiled-128-split2": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "1", "DSSE_T_SPLIT": "2"},
-    "tiled-128x256": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "5"},
-    "pipe-256sq": {"DSSE_GEMM_IMPL": "4", "DSSE_T_CFG": "8"},
-    "skinny-default": {"DSSE_GEMM_IMPL": "0"},
-    "skinny-nt2kw4": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "2", "DSSE_GEMM_KW": "4"},
-    "skinny-nt1kw8": {"DSSE_GEMM_IMPL": "0", "DSSE_GEMM_NT": "1", "DSSE_GEMM_KW": "8"},
+    "stream-default": {"gemm_impl": "2", "s_ring": "0"},
+    "stream-nt2": {"gemm_impl": "2", "s_nt": "2"},
+    "stream-nw4-split2": {"gemm_impl": "2", "s_nw": "4", "s_split": "2"},
+    "stream-nw4-split4": {"gemm_impl": "2", "s_nw": "4", "s_split": "4"},
+    "ring": {"gemm_impl": "2"},
+    "ring-nw4-split2": {"gemm_impl": "2", "s_nw": "4", "s_split": "2"},
+    "ring-nw8": {"gemm_impl": "2", "s_nw": "8"},
+    "ring2-all": {"gemm_impl": "2", "ring2": "1"},
+    "ring1-all": {"gemm_impl": "2", "ring2": "0"},
+    "wide-default": {"gemm_impl": "3"},
+    "wide-split2-rd": {"gemm_impl": "3", "w_split": "2", "w_rd": "3"},
+    "tiled-default": {"gemm_impl": "4"},
+    "tiled-128-split2": {"gemm_impl": "4", "t_cfg": "1", "t_split": "2"},
+    "tiled-128x256": {"gemm_impl": "4", "t_cfg": "5"},
+    "pipe-256sq": {"gemm_impl": "4", "t_cfg": "8"},
+    "skinny-default": {"gemm_impl": "0"},
+    "skinny-nt2kw4": {"gemm_impl": "0", "gemm_nt": "2", "gemm_kw": "4"},
+    "skinny-nt1kw8": {"gemm_impl": "0", "gemm_nt": "1", "gemm_kw": "8"},
 }
 
 
 @pytest.fixture(autouse=True)
 def _fresh_kernel_env():
-    """The library caches the DSSE_* tuning variables: re-read them around every test."""
+    """The library caches its DSSE_KERNEL_CFG overrides: re-read them around every test."""
     ops.refresh_env()
     yield
     ops.refresh_env()
@@ -56,8 +56,7 @@ def _fresh_kernel_env():
 
 @pytest.fixture(params=sorted(GEMM_CONFIGS))
 def tiles(request, monkeypatch):
-    for k, v in GEMM_CONFIGS[request.param].items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(**GEMM_CONFIGS[request.param]))
     ops.refresh_env()
     yield request.param
     monkeypatch.undo()
@@ -115,11 +114,11 @@ def test_gemm_resid_split_then_fused_norm(gpu, M, K):
 @pytest.mark.parametrize("nw,S", [(8, 8), (6, 4), (5, 4), (4, 16), (8, 4)])
 @pytest.mark.parametrize("M,K", [(64, 4096), (33, 14336), (64, 14336)])
 def test_resid_split_ring_shapes(gpu, monkeypatch, nw, S, M, K):
-    """O / down projection on the ring with DSSE_RESID_NW / DSSE_RESID_SPLIT (wider workgroups, deeper K split):
+    """O / down projection on the ring with resid_nw / resid_split (DSSE_KERNEL_CFG; wider workgroups, deeper K split):
     the slabs reduced by the norm equal resid += x·wᵀ followed by the norm."""
     N = {5: 5120, 6: 3072}.get(nw, 4096)  # N / 16 tiles divisible by nw; N a multiple of 1024 for the norm
-    monkeypatch.setenv("DSSE_RESID_NW", str(nw))
-    monkeypatch.setenv("DSSE_RESID_SPLIT", str(S))
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(resid_nw=str(nw)))
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(resid_split=str(S)))
     ops.refresh_env()
     g = torch.Generator().manual_seed(nw * 1000 + S * 10 + M + K)
     x = _rand(M, K, dev=gpu, gen=g)
@@ -165,9 +164,7 @@ def test_gemm_ring_lds_dma(gpu, monkeypatch, ring, nw, M, K, S, r2):
     N = 16 * int(nw) * 5
     x = _rand(M, K, dev=gpu, gen=g)
     w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
-    for k, v in {"DSSE_GEMM_IMPL": "2", "DSSE_S_RING": ring, "DSSE_S_NW": nw, "DSSE_S_SPLIT": S,
-                 "DSSE_RING2": r2}.items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(gemm_impl="2", s_ring=ring, s_nw=nw, s_split=S, ring2=r2))
     ops.refresh_env()
     out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
     ref = torch.zeros(M, N, dtype=torch.float32)
@@ -194,12 +191,12 @@ def test_gemm_stream_odd_wave_counts(gpu, monkeypatch, nw, M):
     N, K = 16 * nw * 6, 2048
     x = _rand(M, K, dev=gpu, gen=g)
     w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / 45, gen=g))
-    monkeypatch.setenv("DSSE_GEMM_IMPL", "2")
-    monkeypatch.setenv("DSSE_S_RING", "0")  # the gemm_stream kernel itself (the ring form takes 4 / 8 waves)
-    monkeypatch.setenv("DSSE_S_NW", str(nw))
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(gemm_impl="2"))
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(s_ring="0"))  # the gemm_stream kernel itself (the ring form takes 4 / 8 waves)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(s_nw=str(nw)))
     ops.refresh_env()
     for split in ("1", "2"):
-        monkeypatch.setenv("DSSE_S_SPLIT", split)
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(s_split=split))
         ops.refresh_env()
         out = torch.zeros(M, N, device=gpu, dtype=torch.float32)
         ref = torch.zeros(M, N, dtype=torch.float32)
@@ -455,7 +452,7 @@ def test_qkv_attention_decode_folded_epilogue(gpu, monkeypatch, cfg, M, part):
                                          wt=torch.zeros(M, dtype=torch.int32)).items()}
     res = {}
     for fused in (1, 0):
-        monkeypatch.setenv("DSSE_FUSED_QKV_ATTN", str(fused))
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(fused_qkv_attn=str(fused)))
         ops.refresh_env()
         k_, v_ = kc.clone().to(gpu), vc.clone().to(gpu)
         q = torch.zeros(M, nh * 128, device=gpu, dtype=torch.bfloat16)

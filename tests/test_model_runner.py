@@ -81,12 +81,12 @@ def test_engine_wide_batch_path_gpu(gpu, monkeypatch, impl):
 
     monkeypatch.setattr(model_runner, "DECODE_GEMM_MAX_M", 2)
     if impl == "tiled":
-        monkeypatch.setenv("DSSE_GEMM_IMPL", "4")
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(gemm_impl="4"))
     ops.refresh_env()
     try:
         assert _run(gpu, True) < 0.1
     finally:
-        monkeypatch.delenv("DSSE_GEMM_IMPL", raising=False)
+        monkeypatch.delenv("DSSE_KERNEL_CFG", raising=False)
         ops.refresh_env()
 
 

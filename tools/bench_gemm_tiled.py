@@ -62,11 +62,9 @@ def main():
             times = {k: [] for k in arms}
             for _ in range(args.rounds):
                 for k, fn in arms.items():
-                    os.environ.pop("DSSE_GEMM_IMPL", None)
-                    os.environ.pop("DSSE_T_CFG", None)
+                    os.environ.pop("DSSE_KERNEL_CFG", None)
                     if k.startswith("tiled"):
-                        os.environ["DSSE_GEMM_IMPL"] = "4"
-                        os.environ["DSSE_T_CFG"] = k[5:]
+                        os.environ["DSSE_KERNEL_CFG"] = f"gemm_impl=4,t_cfg={k[5:]}"
                     ops.refresh_env()
                     times[k].append(timeit(fn, args.iters))
             for k, ts in times.items():

@@ -2,10 +2,10 @@
 # One parameterised GPU-box session (replaces the per-experiment tools/gpu_r3*.sh scripts).
 #   tools/gpu_run.sh OUTDIR STEP [STEP ...]
 # Steps (each under its own time limit; a crash, fault or timeout ends the session at once):
-#   mega_test     tests/test_mega_gpu.py                 mega_bench    tools/bench_mega.py --M 64
 #   model_test    tests/test_model_full_dims_gpu.py      ar_test       tests/test_custom_ar_gpu.py
+#   gemm_test     tests/test_gemm_tiled_gpu.py           tp_test       tests/test_tp_gpu.py
+#   bench64       bench.py (driver form, 64 streams)     ttft512       tools/bench_ttft.py --prompt-len 512
 #   gpu_tests     the whole GPU suite (pytest -m gpu)    smoke         __graft_entry__.smoke()
-#   bench64       bench.py (driver form, 64 streams)     bench64_mega  the same with DSSE_MEGA=1
 #   bench256      bench.py --streams 256                 prof64        rocprofv3 kernel trace of bench.py
 #   ttft8k        tools/bench_ttft.py --prompt-len 8192  c3stub        8 paced stub replicas x 256 streams (CPU only)
 #   attn_bench    tools/bench_prefill_attn.py (8k / 512 causal, + SDPA arm)
@@ -29,21 +29,16 @@ step() {  # name, timeout, cmd...
 PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
 for s in "$@"; do
   case $s in
-    mega_test) step mega_test 300 $PYT tests/test_mega_gpu.py ;;
-    mega_bench) step mega_bench 300 python -u tools/bench_mega.py --M 64 ;;
-    mega_stamps) step mega_stamps 300 python -u tools/bench_mega.py --M 64 --qkv --stamps ;;
     tp_test) step tp_test 600 $PYT tests/test_tp_gpu.py ;;
     model_test) step model_test 600 $PYT tests/test_model_full_dims_gpu.py ;;
     ar_test) step ar_test 900 $PYT tests/test_custom_ar_gpu.py ;;
     gpu_tests) step gpu_tests 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench64) step bench64 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    bench64_mega) DSSE_MEGA=1 step bench64_mega 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     bench256b) step bench256b 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     prof256) step prof256 600 rocprofv3 --kernel-trace --stats -d "$out/prof256" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
-    prof64_mega) DSSE_MEGA=1 step prof64_mega 600 rocprofv3 --kernel-trace --stats -d "$out/prof64_mega" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     ttft512) step ttft512 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
     profttft8k)

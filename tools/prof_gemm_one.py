@@ -22,8 +22,7 @@ ap.add_argument("--cfg", default="3")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--library", action="store_true")
 a = ap.parse_args()
-os.environ["DSSE_GEMM_IMPL"] = "4"
-os.environ["DSSE_T_CFG"] = a.cfg
+os.environ["DSSE_KERNEL_CFG"] = f"gemm_impl=4,t_cfg={a.cfg}"
 ops.load_library(required=True)
 ops.refresh_env()
 N, K = SHAPES[a.shape]

@@ -62,9 +62,9 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the calls")
     ap.add_argument("--iters", type=int, default=40)
-    ap.add_argument("--configs", default="skinny;s;s:DSSE_S_NW=8;w;t",
+    ap.add_argument("--configs", default="skinny;s;s:s_nw=8;w;t",
                     help="';'-separated; 'skinny', 's' (X-streaming), 'w' (wide, 32x32 MFMA) or 't' (tiled), "
-                         "optionally ':K=V,K=V' env overrides")
+                         "optionally ':key=V,key=V' DSSE_KERNEL_CFG overrides")
     ap.add_argument("--hot", action="store_true", help="one weight copy (Infinity-Cache resident when it fits)")
     ap.add_argument("--out", default="")
     ap.add_argument("--grid", action="store_true", help="sweep the X-streaming parameter grid")
@@ -77,7 +77,7 @@ def main():
         for nw in (4, 8):
             for split in (1, 2, 4):
                 for rd in (1, 2):
-                    cfgs.append(f"s:DSSE_S_NW={nw},DSSE_S_SPLIT={split},DSSE_S_RD={rd}")
+                    cfgs.append(f"s:s_nw={nw},s_split={split},s_rd={rd}")
         args.configs = ";".join(cfgs)
     for name, (N, K) in shapes(args.tp).items():
         if args.ops and name not in args.ops.split(","):
@@ -88,13 +88,9 @@ def main():
         for M in [int(m) for m in args.M.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             for cfg in args.configs.split(";"):
-                for k in [k for k in os.environ if k.startswith(("DSSE_S_", "DSSE_W_", "DSSE_T_", "DSSE_GEMM_"))]:
-                    os.environ.pop(k, None)
                 impl, _, kv = cfg.partition(":")
-                os.environ["DSSE_GEMM_IMPL"] = {"skinny": "0", "s": "2", "w": "3", "t": "4"}[impl]
-                for item in filter(None, kv.split(",")):
-                    k, v = item.split("=")
-                    os.environ[k] = v
+                gi = {"skinny": "0", "s": "2", "w": "3", "t": "4"}[impl]
+                os.environ["DSSE_KERNEL_CFG"] = f"gemm_impl={gi}" + (f",{kv}" if kv else "")
                 ops.refresh_env()
                 if name == "gate_up":
                     out = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
