@@ -10,7 +10,8 @@
 //     1. e = ++epoch[b] (a per-row call counter only this workgroup touches), parity p = e & 1
 //     2. copy its partial row into its OWN IPC buffer, data[p][b] (write-through sc0 sc1 stores)
 //     3. system-scope release, then one flag store per peer q: peer_q.flags[r][b] = e
-//     4. wait for flags[q][b] >= e from every peer (system-scope relaxed polls, bounded)
+//     4. wait for flags[q][b] >= e from every peer (system-scope relaxed polls, bounded), then a system-scope
+//        acquire before any peer data is read
 //     5. read data[p][b] of every rank q = 0..T-1 over xGMI (sc0 sc1 loads), sum in rank order in fp32 (the same
 //        bits on every rank), resid[b] += sum, y[b] = rmsnorm(resid[b]) * w
 //
@@ -19,10 +20,16 @@
 // e's data (stream order).  Peers are at most one call ahead (they cannot pass call e + 1 without r's flag), so
 // `flags >= e` is exact.  All workgroups of a launch are independent (row b only waits for row b of the
 // peers), so the grid needs no co-residency; every wait is bounded (kArSpinLimit sleeps, ~1 s) and a timeout
-// sets err[0] instead of hanging the GPU (the engine checks it and falls back to RCCL).
+// sets err[0] instead of hanging the GPU: err is the runner's health word, checked at every drained step, and a
+// set word fails every stream with [ERROR] and drops readiness (engine.py EngineFault, model_runner HEALTH_WORDS).
 //
-// IPC buffer of one rank (ar_buffer_bytes): [flags: kArMaxRanks x rows uint32][pad to 4 KiB][data: 2 x rows x H
-// bf16].  Allocated uncached (hipDeviceMallocUncached) when the runtime allows it, so neither side's L2 holds
+// The same buffer carries the decode step's one all-gather (C3: every rank's sampling candidates, 8 bytes per
+// (row, vocab chunk)) in the same flag / parity scheme with its own flags and per-row counter (ar_gather_kernel),
+// so the whole TP decode step -- both all-reduces of every layer and the candidate all-gather -- runs without RCCL
+// and is captured into one hipGraph per bucket.
+//
+// IPC buffer of one rank (ar_buffer_bytes): [flags: kArMaxRanks x rows uint32][gather flags: kArMaxRanks x rows
+// uint32][pad to 4 KiB][data: 2 x rows x H bf16][gather data: 2 x rows x kGatherRowBytes].  Allocated uncached (hipDeviceMallocUncached) when the runtime allows it, so neither side's L2 holds
 // a stale copy of another process's writes; the sc0 sc1 cache-policy bits are set on every access anyway.
 #include "api.h"
 
@@ -33,8 +40,11 @@ namespace dsse {
 constexpr int kArMaxRanks = 8;
 constexpr int kArSpinLimit = 1 << 22;
 constexpr int kAuxSys = 1 | 16;  // sc0 | sc1: system-coherent (bypass the non-coherent caches)
+constexpr int kGatherRowBytes = 128;  // one row's sampling candidates: 16 vocab chunks x (score, index) fp32
 
-__host__ __device__ inline size_t ar_data_off(int rows) { return ((size_t)kArMaxRanks * rows * 4 + 4095) & ~(size_t)4095; }
+__host__ __device__ inline size_t ar_gflags_off(int rows) { return (size_t)kArMaxRanks * rows * 4; }
+__host__ __device__ inline size_t ar_data_off(int rows) { return ((size_t)2 * kArMaxRanks * rows * 4 + 4095) & ~(size_t)4095; }
+__host__ __device__ inline size_t ar_gdata_off(int rows, int H) { return ar_data_off(rows) + (size_t)2 * rows * H * 2; }
 
 // H / 8 threads per workgroup (16 bytes of bf16 per lane), H <= 8192.
 __global__ void __launch_bounds__(1024)
@@ -70,6 +80,7 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
     while (__hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e && ++spins < kArSpinLimit)
       __builtin_amdgcn_s_sleep(2);
     if (spins >= kArSpinLimit) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the peer's row is visible from here on
   }
   __syncthreads();  // every peer's row is in its memory: read it with system-coherent loads only
   // 5. sum the T partial rows in rank order (identical bits on every rank)
@@ -115,12 +126,61 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
   if (tid == 0) epoch[b] = e;
 }
 
+// C3: all-gather of one row's sampling candidates (kGatherRowBytes) over the IPC buffers, one wave per row b:
+// lanes 0-7 hold the row's 8 x 16 bytes; lanes < world do the flag exchange of peer `lane`.  Same protocol as
+// ar_rmsnorm_kernel (own buffer, per-row counter, parity double buffer, bounded waits, err on timeout).
+// out: [world, rows_out, kGatherRowBytes / 4] fp32 (rank-major), the layout of the RCCL all_gather it replaces.
+__global__ void __launch_bounds__(64)
+ar_gather_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, int M, const unsigned long long* __restrict__ peers,
+                 int rank, int world, int rows, int H, unsigned int* __restrict__ epoch, unsigned int* __restrict__ err) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const unsigned int e = epoch[b] + 1;
+  constexpr int kPieces = kGatherRowBytes / 16;
+  const size_t goff = ar_gdata_off(rows, H) + ((size_t)(e & 1) * rows + b) * kGatherRowBytes + (size_t)lane * 16;
+  const unsigned long long mine_u = peers[rank];
+  const __amdgpu_buffer_rsrc_t mrs = make_rsrc(
+      reinterpret_cast<const void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(mine_u >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mine_u)), 0x7FFFFFFF);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  if (lane < kPieces) {
+    const uint4 v = in[(size_t)b * kPieces + lane];
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, mrs, (uint32_t)goff, 0, kAuxSys);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // one wave: every lane's store drained before any flag
+  if (lane < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int* pf = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(peers[lane]) + ar_gflags_off(rows)) +
+                       (size_t)rank * rows + b;
+    __hip_atomic_store(pf, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned int* mf = reinterpret_cast<const unsigned int*>(reinterpret_cast<const char*>(mine_u) +
+                                                                   ar_gflags_off(rows)) + (size_t)lane * rows + b;
+    int spins = 0;
+    while (__hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e && ++spins < kArSpinLimit)
+      __builtin_amdgcn_s_sleep(2);
+    if (spins >= kArSpinLimit) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  // the wave left the poll loop only when every lane saw its peer's flag: read every rank's row (system-coherent)
+  for (int q = 0; q < world; ++q) {
+    if (lane < kPieces) {
+      const unsigned long long pq = peers[q];
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(
+          reinterpret_cast<const void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(pq >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)pq)), 0x7FFFFFFF);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)goff, 0, kAuxSys);
+      out[((size_t)q * M + b) * kPieces + lane] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
+  if (lane == 0) epoch[b] = e;
+}
+
 }  // namespace dsse
 
 using namespace dsse;
 
 extern "C" size_t dsse_ar_buffer_bytes(int rows, int H) {
-  return ar_data_off(rows) + (size_t)2 * rows * H * 2;
+  return ar_gdata_off(rows, H) + (size_t)2 * rows * kGatherRowBytes;
 }
 
 // Allocate one rank's zeroed IPC buffer; *uncached = 1 when hipDeviceMallocUncached was honoured.
@@ -155,5 +215,17 @@ extern "C" hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, cons
   hipLaunchKernelGGL(ar_rmsnorm_kernel, dim3(M), dim3(H / 8), 0, st, reinterpret_cast<const bf16*>(tmp), resid,
                      reinterpret_cast<const bf16*>(w), reinterpret_cast<bf16*>(y), H, eps, peers, rank, world, rows,
                      epoch, err);
+  return hipGetLastError();
+}
+
+// in: [M, kGatherRowBytes / 4] fp32 of this rank; out: [world, M, kGatherRowBytes / 4] (rank-major).  gepoch: the
+// gather's own per-row counters (independent of the all-reduce's).
+extern "C" hipError_t dsse_ar_gather(int M, const void* in, void* out, const unsigned long long* peers, int rank,
+                                     int world, int rows, int H, unsigned int* gepoch, unsigned int* err,
+                                     hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (M > rows || world > kArMaxRanks || world < 1 || rank < 0 || rank >= world) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ar_gather_kernel, dim3(M), dim3(64), 0, st, reinterpret_cast<const uint4*>(in),
+                     reinterpret_cast<uint4*>(out), M, peers, rank, world, rows, H, gepoch, err);
   return hipGetLastError();
 }

@@ -123,6 +123,8 @@ hipError_t dsse_ar_close(void* ptr, int opened);
 hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, const void* w, void* y, int H, float eps,
                            const unsigned long long* peers, int rank, int world, int rows, unsigned int* epoch,
                            unsigned int* err, hipStream_t st);
+hipError_t dsse_ar_gather(int M, const void* in, void* out, const unsigned long long* peers, int rank, int world,
+                          int rows, int H, unsigned int* gepoch, unsigned int* err, hipStream_t st);
 // Checked build: first out-of-range index per kernel file (line, value, bound, count); zeros otherwise.
 hipError_t dsse_check_gemm_skinny(int* out, int clear);
 hipError_t dsse_check_gemm_stream(int* out, int clear);

@@ -866,7 +866,29 @@ void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, do
                                  reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 13; }
+// C3 over the same IPC buffers: out[q] = rank q's `cand` rows (every rank's sampling candidates, [M, 16, 2] fp32 =
+// 128 bytes per row); gepoch: int32 [rows], the gather's own counters.
+void ar_gather(const Tensor& cand, Tensor& out, const Tensor& peers, int64_t rank, int64_t rows, int64_t H,
+               Tensor& gepoch, Tensor& err) {
+  for (const Tensor* t : {&cand, (const Tensor*)&out, &peers, (const Tensor*)&gepoch, (const Tensor*)&err})
+    check_gpu(*t, "ar_gather tensor");
+  check_dtype(cand, at::kFloat, "cand");
+  check_dtype(out, at::kFloat, "out");
+  check_dtype(peers, at::kLong, "peers");
+  check_dtype(gepoch, at::kInt, "gepoch");
+  check_dtype(err, at::kInt, "err");
+  const int M = (int)cand.size(0), world = (int)peers.numel();
+  TORCH_CHECK(cand.is_contiguous() && out.is_contiguous() && cand.numel() == (int64_t)M * 32,
+              "ar_gather: cand must be contiguous [M, 16, 2] fp32 (128 bytes per row)");
+  TORCH_CHECK(out.numel() == (int64_t)world * cand.numel(), "ar_gather: out must be [world, M, 16, 2]");
+  TORCH_CHECK(M <= rows && gepoch.numel() >= rows, "ar_gather: more rows than the buffers hold");
+  DSSE_CHECK_HIP(dsse_ar_gather(M, cand.data_ptr(), out.data_ptr(),
+                                reinterpret_cast<const unsigned long long*>(peers.data_ptr<int64_t>()), (int)rank, world,
+                                (int)rows, (int)H, reinterpret_cast<unsigned int*>(gepoch.data_ptr<int>()),
+                                reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
+}
+
+int64_t kernels_abi_version() { return 14; }
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -929,6 +951,8 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
   m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
         "Tensor(c!) epoch, Tensor(d!) err) -> ()");
+  m.def("ar_gather(Tensor cand, Tensor(a!) out, Tensor peers, int rank, int rows, int H, Tensor(b!) gepoch, "
+        "Tensor(c!) err) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
@@ -951,4 +975,5 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
   m.impl("ar_rmsnorm", &ar_rmsnorm);
+  m.impl("ar_gather", &ar_gather);
 }

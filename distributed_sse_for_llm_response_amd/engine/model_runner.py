@@ -180,8 +180,8 @@ class ModelRunner:
             # a timed-out peer wait now marks this runner's health word (checked at every drained step)
             self.comm.fast_ar.err = self.health[HEALTH_TP_PEER:HEALTH_TP_PEER + 1]
         if self.comm.size > 1 and self.comm.rank == 0:
-            print(f"[engine] TP={self.comm.size} decode all-reduce: "
-                  f"{'IPC kernel' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
+            print(f"[engine] TP={self.comm.size} decode all-reduce + candidate all-gather: "
+                  f"{'IPC kernels' if not self.fast_ar_reason else 'RCCL (' + self.fast_ar_reason + ')'}", flush=True)
         self.graphs = {}
         self.graph_pool = None
         self.pf_graphs = {}   # row bucket -> captured prefill graph
@@ -292,10 +292,16 @@ class ModelRunner:
         return [HEALTH_WORDS[i] for i in range(min(len(HEALTH_WORDS), len(words))) if int(words[i]) != 0]
 
     def close(self) -> None:
-        """Release the TP all-reduce's IPC mappings and buffer (the device is synchronised first)."""
+        """Release the TP all-reduce's IPC mappings and buffer.  Collective over the TP group: the device is
+        synchronised, then every rank passes a barrier, so no peer's kernel can still be reading this rank's buffer
+        (the IPC kernels pull peer rows) when it is unmapped and freed."""
         if self.comm.fast_ar is not None:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
+            try:
+                self.comm.barrier()
+            except Exception as e:  # noqa: BLE001 - a dead peer cannot be reading any more either
+                print(f"[engine] TP rank {self.comm.rank}: barrier before the IPC teardown failed ({e})", flush=True)
             self.comm.fast_ar.close()
             self.comm.fast_ar = None
 
@@ -312,7 +318,11 @@ class ModelRunner:
         import torch.distributed as dist
 
         ok, why = True, ""
+        if dist.get_backend(self.comm.group) == "gloo":
+            ok, why = False, "gloo backend (host-staged collectives cannot be captured)"
         try:
+            if not ok:
+                raise StopIteration
             t = torch.ones(8, device=self.device, dtype=torch.float32)
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -328,6 +338,8 @@ class ModelRunner:
             torch.cuda.synchronize(self.device)
             if not torch.all(t == float(self.comm.size)):
                 ok, why = False, f"replayed all-reduce gave {t.tolist()}"
+        except StopIteration:
+            pass
         except Exception as e:  # noqa: BLE001 - the reason is logged, decode then runs eagerly
             ok, why = False, f"{type(e).__name__}: {e}"
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
@@ -338,18 +350,33 @@ class ModelRunner:
             why = "another rank of the TP group cannot capture its collectives"
         return int(flag.item()) == 1, why
 
+    def ipc_decode(self) -> bool:
+        """TP > 1 with the IPC context up for every decode row: the decode step's collectives are the hand-written
+        IPC all-reduce (both per layer) and candidate all-gather kernels only -- no RCCL call in the step."""
+        ar = self.comm.fast_ar
+        return self.comm.size > 1 and ar is not None and ar.rows >= self.max_batch
+
     def capture(self, buckets=None) -> None:
-        """Capture the decode step of each batch bucket into its own graph (shared memory pool).  With TP > 1
-        the collectives are captured too, after a self-check (fallback: eager decode, reason logged)."""
+        """Capture the decode step of each batch bucket into its own graph (shared memory pool).  TP > 1: the decode
+        graphs hold the IPC collective kernels when that context is up (ipc_decode), else the RCCL collectives after
+        a capture self-check; the prefill / mixed graphs (their all-reduces are RCCL) only when RCCL captures.
+        Neither: eager decode (reason logged)."""
         if not self.use_graphs:
             return
+        prefill_graphs = True
         if self.comm.size > 1:
-            ok, why = self._collectives_capturable()
-            if not ok:
+            ipc = self.ipc_decode()
+            rccl_ok, why = self._collectives_capturable()
+            if not ipc and not rccl_ok:
                 print(f"[engine] TP rank {self.comm.rank}: decode graphs disabled, collectives not capturable "
                       f"({why}); decoding eagerly", flush=True)
                 self.use_graphs = False
                 return
+            prefill_graphs = rccl_ok
+            if self.comm.rank == 0:
+                print(f"[engine] TP={self.comm.size} decode graphs captured with "
+                      f"{'the IPC all-reduce + all-gather kernels (no RCCL in the step)' if ipc else 'RCCL collectives'}"
+                      f"; prefill graphs {'captured' if rccl_ok else 'off (' + why + ')'}", flush=True)
         buckets = buckets or batch_buckets(self.max_batch)
         # Warm up on a side stream (allocator + library init) before capture.
         s = torch.cuda.Stream(self.device)
@@ -369,7 +396,8 @@ class ModelRunner:
             self.graphs[B] = g
         torch.cuda.synchronize(self.device)
         self._restore_state(saved)
-        self._capture_prefill(buckets)
+        if prefill_graphs:
+            self._capture_prefill(buckets)
 
     def _capture_prefill(self, decode_buckets) -> None:
         """One graph per prefill row bucket over static buffers (_PrefillStatic); the metadata of a batch is

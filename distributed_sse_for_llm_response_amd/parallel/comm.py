@@ -8,11 +8,13 @@ into the decode hipGraph together with the kernels.
 
 The same code runs on CPU tensors with the ``gloo`` backend for the multi-process tests.
 
-Decode all-reduces on GPUs go through ``IpcAllReduce`` when it is available: one hand-written kernel per
+Decode collectives on GPUs go through ``IpcAllReduce`` when it is available: one hand-written kernel per
 all-reduce (``csrc/kernels/allreduce.hip``) that exchanges the rows of the O / down partial products through
-IPC-mapped peer buffers over xGMI and folds the residual add + RMSNorm in.  It is set up once per TP group
-(handles exchanged over the group, a self-test against ``dist.all_reduce`` decided by all ranks together) and
-RCCL stays the fallback (``DSSE_CUSTOM_AR=0`` forces it).
+IPC-mapped peer buffers over xGMI and folds the residual add + RMSNorm in, and one for the candidate all-gather
+(same buffers, flags and parity scheme).  With both, the TP decode step holds no RCCL call at all and is captured
+into one hipGraph per bucket even where RCCL cannot be captured (ranks sharing a GPU over gloo).  It is set up once
+per TP group (handles exchanged over the group, a self-test against ``dist.all_reduce`` / ``all_gather`` decided by
+all ranks together) and RCCL stays the fallback (``DSSE_CUSTOM_AR=0`` forces it).
 """
 from __future__ import annotations
 
@@ -46,7 +48,11 @@ class TPComm:
                 dist.all_reduce(t, group=self.group)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        """out: [size * numel(inp)] contiguous."""
+        """out: [size * numel(inp)] contiguous.  Sampling candidates ([rows, 16, 2] fp32) take the IPC gather
+        kernel when the IPC context is up."""
+        if self.size > 1 and self.fast_ar is not None and self.fast_ar.can_gather(inp, out):
+            self.fast_ar.gather(inp, out)
+            return
         if self.size > 1:
             if self._host_staged(out):
                 h = torch.empty(out.numel(), dtype=out.dtype)
@@ -120,6 +126,7 @@ class IpcAllReduce:
         self.own_ptr, self.peer_ptrs, self.uncached = own_ptr, peer_ptrs, uncached
         self.peers = torch.tensor(peer_ptrs, dtype=torch.int64, device=device)
         self.epoch = torch.zeros(rows, dtype=torch.int32, device=device)
+        self.gepoch = torch.zeros(rows, dtype=torch.int32, device=device)  # the candidate gather's own counters
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
 
     @classmethod
@@ -176,6 +183,18 @@ class IpcAllReduce:
         torch.ops.dsse.ar_rmsnorm(tmp, resid, norm_w, y, eps, self.peers, self.comm.rank, self.rows, self.epoch,
                                   self.err)
 
+    GATHER_ROW_FLOATS = 32  # allreduce.hip kGatherRowBytes / 4: 16 vocab chunks x (score, index)
+
+    def can_gather(self, inp, out) -> bool:
+        return (inp.is_cuda and inp.dtype == torch.float32 and out.dtype == torch.float32 and inp.is_contiguous()
+                and out.is_contiguous() and inp.dim() >= 1 and 0 < inp.shape[0] <= self.rows
+                and inp.numel() == inp.shape[0] * self.GATHER_ROW_FLOATS
+                and out.numel() == self.comm.size * inp.numel())
+
+    def gather(self, inp, out) -> None:
+        """out[q] = rank q's inp rows (rank-major, the layout of dist.all_gather_into_tensor)."""
+        torch.ops.dsse.ar_gather(inp, out, self.peers, self.comm.rank, self.rows, self.hidden, self.gepoch, self.err)
+
     def self_test(self) -> str:
         """Fused all-reduce of random partials vs RCCL/gloo sum + reference norm, at a few row counts; ""=ok."""
         from ..ops import reference as R
@@ -202,6 +221,22 @@ class IpcAllReduce:
                 err_y = float((y.cpu().float() - y_ref.float()).abs().max())
                 if err_r > 1e-3 or err_y > 5e-2:
                     return f"self-test: M={M} max |resid err| {err_r:.3g}, |y err| {err_y:.3g}"
+                # the candidate gather: exact copies of every rank's rows, rank-major
+                cand = torch.randn(M, 16, 2, generator=gen).to(self.device)
+                got = torch.zeros(self.comm.size, M, 16, 2, device=self.device)
+                self.gather(cand, got)
+                if dist.get_backend(self.comm.group) == "gloo":
+                    ref_all = torch.zeros(self.comm.size * cand.numel())
+                    dist.all_gather_into_tensor(ref_all, cand.cpu().view(-1), group=self.comm.group)
+                else:
+                    ref_dev = torch.zeros(self.comm.size * cand.numel(), device=self.device)
+                    dist.all_gather_into_tensor(ref_dev, cand.view(-1), group=self.comm.group)
+                    ref_all = ref_dev.cpu()
+                torch.cuda.synchronize(self.device)
+                if int(self.err.item()) != 0:
+                    return "self-test: a peer gather wait timed out"
+                if not torch.equal(got.cpu().view(-1), ref_all):
+                    return f"self-test: M={M} candidate gather differs from all_gather"
         return ""
 
 
