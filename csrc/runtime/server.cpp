@@ -1834,6 +1834,8 @@ void InspectionGate::hybrid_frame(RemoteInspector& ri, std::unordered_map<std::s
   if (f->done) held.erase(it);
 }
 
+constexpr int64_t kDeadAgeNs = 600LL * 1000000000LL;  // 10 minutes
+
 void InspectionGate::run(Worker& w) {
   const ServerConfig& cfg = srv_.config();
   RemoteInspector ri(cfg.inspection_endpoint, cfg.inspection_timeout_ms);
@@ -1856,8 +1858,11 @@ void InspectionGate::run(Worker& w) {
       out.assign(batch.begin(), batch.end());
       batch.clear();
     } else if (!hybrid && batch.size() > kOverloadDepth) {
-      for (const auto& f : batch)
-        if (w.dead.insert(f->conversation_id).second) fail_closed(f->conversation_id, "inspection overloaded");
+      const int64_t now = mono_ns();
+      for (const auto& f : batch) {
+        if (w.dead.emplace(f->conversation_id, now).second) fail_closed(f->conversation_id, "inspection overloaded");
+        if (f->done) w.dead.erase(f->conversation_id);  // its done frame was in this batch: no later frame comes
+      }
       batch.clear();
     }
     for (const auto& f : batch) {
@@ -1868,10 +1873,13 @@ void InspectionGate::run(Worker& w) {
       if (hybrid) {
         hybrid_frame(ri, held, f, out);
       } else {
-        if (inline_frame(ri, f, out)) w.dead.insert(f->conversation_id);
+        if (inline_frame(ri, f, out) && !f->done) w.dead.emplace(f->conversation_id, mono_ns());
       }
     }
-    if (w.dead.size() > 65536) w.dead.clear();
+    if (w.dead.size() > 4096) {  // age out entries whose done frame never arrived (never a wholesale clear)
+      const int64_t now = mono_ns();
+      for (auto it = w.dead.begin(); it != w.dead.end();) it = now - it->second > kDeadAgeNs ? w.dead.erase(it) : std::next(it);
+    }
     if (hybrid) {  // buffer windows that ran out; forget conversations idle for 10 minutes
       const int64_t now = mono_ns();
       for (auto it = held.begin(); it != held.end();) {

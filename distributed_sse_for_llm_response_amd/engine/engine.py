@@ -712,6 +712,14 @@ class LLMEngine:
         self.waiting.clear()
         return events
 
+    def error_events(self, text: str = "[ERROR]") -> list:
+        """Terminal `text` events for every live conversation WITHOUT touching engine state (the watchdog's view of a
+        loop blocked inside a step: the loop may still resume, so only it may mutate the engine)."""
+        now = time.time_ns()
+        live = [s for s in list(self.slots) + list(self.waiting) if s is not None and s.state != "finished"]
+        return [TokenEvent(s.conversation_id, -1, s.produced + 1, True, text=text, timestamp_ns=now, finish="abort",
+                           prompt_tokens=s.orig_len) for s in live]
+
     def run_until_idle(self, max_steps: int = 100000) -> list:
         out = []
         for _ in range(max_steps):

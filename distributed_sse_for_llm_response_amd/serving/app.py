@@ -73,6 +73,7 @@ class EngineLoop(threading.Thread):
         self.rt, self.engine, self.tok, self.cfg = runtime, engine, tokenizer, cfg
         self.stop_flag = threading.Event()
         self.error = None
+        self.halted = False  # set by the watchdog after it failed every stream: the loop must not touch the engine
         rt = rt_mod.load()
         self._rt = rt
         self._remote = hasattr(runtime, "observe")
@@ -166,7 +167,7 @@ class EngineLoop(threading.Thread):
         gc.collect()
         gc.freeze()
         try:
-            while not self.stop_flag.is_set() and not self._shutdown():
+            while not self.stop_flag.is_set() and not self._shutdown() and not self.halted:
                 busy = self.engine.runnable()
                 # only paused streams left: wait briefly so their resume events get through
                 wait = 0 if busy else (2 if self.engine.has_work() else 20)
@@ -185,6 +186,8 @@ class EngineLoop(threading.Thread):
                 self.tracer.begin(self.steps)
                 t0 = time.perf_counter()
                 events = self.engine.step()
+                if self.halted:  # the watchdog ended every stream while this step was blocked
+                    break
                 if self.faults.active:
                     events = self.faults.filter_events(events)
                 self.publish(events)

@@ -70,10 +70,13 @@ class FaultPlan:
         self.active = bool(spec.strip())
 
     @classmethod
-    def from_env(cls) -> "FaultPlan":
-        """DSSE_FAULTS, optionally restricted to some ranks with DSSE_FAULTS_RANKS="1,3"."""
+    def from_env(cls, follower: bool = False) -> "FaultPlan":
+        """DSSE_FAULTS, optionally restricted to some ranks with DSSE_FAULTS_RANKS="1,3".  A TP follower takes the
+        faults only when DSSE_FAULTS_RANKS names it explicitly (an unrestricted drill targets the serving ranks)."""
         ranks = os.environ.get("DSSE_FAULTS_RANKS", "")
         if ranks and os.environ.get("RANK", "0") not in ranks.split(","):
+            return cls("")
+        if follower and not ranks:
             return cls("")
         return cls(os.environ.get("DSSE_FAULTS", ""))
 
@@ -113,12 +116,15 @@ class Watchdog(threading.Thread):
         self._stop = threading.Event()
 
     def _fail(self, idle_for: float) -> None:
-        """The loop is stuck inside a device or collective wait: end every live stream with [ERROR], then exit."""
+        """The loop is stuck inside a device or collective wait: end every live stream with [ERROR], then exit.
+        The loop is halted first (on waking it publishes nothing and leaves its loop) and the [ERROR] events are built
+        from a read-only view: only the loop thread ever mutates the engine, even if its wait completes later."""
         self.failed = True
+        self.loop.halted = True
         print(json.dumps({"level": "ERROR", "msg": "engine hung; failing every stream", "seconds": round(idle_for, 3)}),
               flush=True)
         try:
-            self.loop.publish(self.loop.engine.fail_all())  # the loop thread is blocked: nothing else mutates it now
+            self.loop.publish(self.loop.engine.error_events())
         finally:
             self.set_ready(False)
             if os.environ.get("DSSE_STEP_FAIL_EXIT", "1") != "0":

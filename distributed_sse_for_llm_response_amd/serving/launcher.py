@@ -92,7 +92,7 @@ def serve_tp(cfg: ServeConfig, rank: int, local: int, world: int, tp: int, devic
     if rank != leader:
         engine, _ = build_engine(cfg, device=device, comm=comm)
         try:
-            follower_loop(engine, channel, faults=FaultPlan.from_env())
+            follower_loop(engine, channel, faults=FaultPlan.from_env(follower=True))
         finally:
             engine.r.close()
         return 0
