@@ -11,6 +11,7 @@
 #   attn_bench    tools/bench_prefill_attn.py (8k / 512 causal, + SDPA arm)
 #   gemm_bench    tools/bench_gemm_tiled.py at M = 8192 and 256 (engine dispatch vs library)
 #   attn_test     tests/test_kernels_gpu.py -k prefill     pmc_attn / pmc_gemm  two rocprofv3 --pmc passes each
+#   kern_test     tests/test_kernels_gpu.py
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/$1; shift
@@ -58,6 +59,7 @@ for s in "$@"; do
     serving13_mx256_d0) DSSE_PIPELINE_DEPTH=0 DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256_d0 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
+    kern_test) step kern_test 900 $PYT tests/test_kernels_gpu.py ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill or rope_kv" ;;
     flash_stamps) DSSE_FLASH_STAMPS="$out/fs.bin" step flash_stamps 300 python -u tools/bench_prefill_attn.py --T 8192
       python3 tools/flash_stamps.py "$out/fs.bin" > "$out/flash_stamps.md" 2>&1 ;;
