@@ -161,20 +161,25 @@ class _Drain:
 
 
 class PassCost:
-    """Measured GPU cost of the engine's step kinds, for the adaptive prefill budget (pick the
-    chunk from measured pass cost, not a fixed size).  Timing events bracket every separate prefill pass and every
-    decode step; they are read once they have completed (no host wait).  Decode: an EMA of the step per bucket.
-    Prefill passes: an exponentially weighted least-squares line ms = a + b * tokens.
+    """Measured GPU cost of the engine's step kinds, for sizing prompt work from measured cost instead of a fixed
+    size.  Timing events bracket every decode step, every mixed step and every
+    separate prefill pass; they are read once they have completed (no host wait).  Decode: an EMA of the step per
+    bucket.  Prefill passes: an exponentially weighted least-squares line ms = a + b * tokens.  Mixed steps: the
+    same kind of line for the extra over the bucket's decode step, extra = a + b * C (C = the replayed graph's
+    prompt rows).
 
-    budget(B) = the largest multiple of 64 prompt tokens whose pass costs at most (ratio - 1) x step(B): a stream
-    whose token gap spans a decode step AND a prefill pass then waits at most `ratio` x the steady step.  Until both
-    costs are measured it returns None (the caller keeps its configured budget)."""
+    budget(B): the largest multiple of 64 prompt tokens whose separate pass costs at most (ratio - 1) x step(B);
+    mixed_chunk(B, sizes): the largest captured chunk size whose mixed step costs at most ratio x step(B).  Either
+    way a stream's token gap stays within `ratio` x the occupied bucket's steady step.  Until the costs are measured
+    both return None (the caller keeps its configured size)."""
 
     def __init__(self, ratio: float, decay: float = 0.9):
         self.ratio = ratio
         self.decay = decay
         self.step_ms: dict = {}
         self._fit = [0.0] * 5  # weighted sums: w, w t, w t^2, w y, w t y
+        self._mfit = [0.0] * 5  # the same for mixed steps' extra cost over the decode step
+        self._mixed_seen: set = set()
         self._pending: deque = deque()
 
     def record(self, kind: str, key: int):
@@ -184,12 +189,21 @@ class PassCost:
         e0.record()
         return lambda: (e1.record(), self._pending.append((kind, key, e0, e1)))
 
-    def observe(self, kind: str, key: int, ms: float) -> None:
+    def observe(self, kind: str, key, ms: float) -> None:
         if kind == "decode":
             old = self.step_ms.get(key)
             self.step_ms[key] = ms if old is None else 0.8 * old + 0.2 * ms
             return
-        f, d, t = self._fit, self.decay, float(key)
+        if kind == "mixed":  # key = (B, C)
+            B, C = key
+            step = self.step_ms.get(B)
+            if step is None:
+                return
+            self._mixed_seen.add(C)
+            f, t, ms = self._mfit, float(C), ms - step
+        else:
+            f, t = self._fit, float(key)
+        d = self.decay
         for i, v in enumerate((1.0, t, t * t, ms, t * ms)):
             f[i] = d * f[i] + v
 
@@ -198,15 +212,43 @@ class PassCost:
             kind, key, e0, e1 = self._pending.popleft()
             self.observe(kind, key, e0.elapsed_time(e1))
 
-    def line(self):
-        """(a, b) of the pass-cost line, or None before two passes of different sizes were seen."""
-        w, st, stt, sy, sty = self._fit
+    def line(self, fit=None):
+        """(a, b) of the pass-cost line (`fit`: the mixed-step sums), or None before two sizes were seen."""
+        w, st, stt, sy, sty = self._fit if fit is None else fit
         den = w * stt - st * st
         if w <= 0 or den <= 1e-6 * max(1.0, w * stt):
             return None
         b = (w * sty - st * sy) / den
         a = (sy - b * st) / w
         return (max(0.0, a), b) if b > 0 else None
+
+    def mixed_line(self):
+        """(a, b) of extra = a + b * C for mixed steps: the fitted line once two chunk sizes were seen; with one
+        size, the proportional line through its mean (b = extra / C, a = 0: it over-predicts larger chunks, so the
+        first choice is conservative and the next size measured turns on the fit); None before any."""
+        if len(self._mixed_seen) >= 2:
+            line = self.line(self._mfit)
+            if line is not None:
+                return line
+        w, st, _, sy, _ = self._mfit
+        return (0.0, sy / st) if w > 0 and st > 0 and sy > 0 else None
+
+    def mixed_ms(self, B: int, C: int):
+        """Predicted GPU time of a mixed step (bucket B, C prompt rows), or None before it can be predicted."""
+        step = self.step_ms.get(B)
+        line = self.mixed_line()
+        return None if step is None or line is None else step + line[0] + line[1] * C
+
+    def mixed_chunk(self, B: int, sizes: list):
+        """The largest of `sizes` whose predicted mixed step stays within ratio x step(B) (the smallest when none
+        does), or None until the decode step of bucket B and a mixed step were measured."""
+        step = self.step_ms.get(B)
+        line = self.mixed_line()
+        if step is None or line is None or not sizes:
+            return None
+        a, b = line
+        fit = [c for c in sizes if a + b * c <= (self.ratio - 1.0) * step]
+        return max(fit) if fit else min(sizes)
 
     def budget(self, B: int, cap: int):
         step = self.step_ms.get(B)
@@ -270,9 +312,25 @@ class LLMEngine:
         # pass so that a token gap spanning a decode step and a pass stays <= r x the occupied bucket's step
         # (PassCost), up to prefill_budget; a prompt that has waited DSSE_PREFILL_BOOST_STEPS steps gets the full
         # budget (TTFT guard).  Unset / 0: the fixed prefill_budget.
-        ratio = float(os.environ.get("DSSE_PREFILL_ITL_RATIO", "0") or 0)
+        # Mixed steps (the default): the ratio is on by default (1.85: a mixed step within ~2x the bucket's step,
+        # VERDICT r4 item 2's ITL p99 target, with margin) and sizes each step's prompt chunk.
+        ratio = float(os.environ.get("DSSE_PREFILL_ITL_RATIO", "1.85" if self.mixed else "0") or 0)
         self.cost = PassCost(ratio) if ratio > 1.0 and runner.device.type == "cuda" else None
         self.boost_steps = int(os.environ.get("DSSE_PREFILL_BOOST_STEPS", "8"))
+        self._jit = None  # (host time the newest step started, its expected ms): jit_delay
+
+    def jit_delay(self, margin_s: float = 0.0015) -> float:
+        """Seconds the host can still wait before enqueueing the next step without leaving the GPU idle: the
+        in-flight step's expected end (PassCost) minus `margin_s` for the host's own step work.  A prompt that
+        arrives meanwhile then rides in the very next step instead of the one after the step already queued
+        (pipeline depth 1 alone makes a new prompt wait ~1.5 steps).  0 without a cost estimate, in
+        deterministic (TP) mode, or with no step in flight."""
+        if self.deterministic or self.cost is None or not self.inflight or self._jit is None:
+            return 0.0
+        start, est_ms = self._jit
+        if est_ms is None:
+            return 0.0
+        return max(0.0, start + est_ms / 1e3 - margin_s - time.perf_counter())
 
     # ------------------------------------------------------------------ requests
     def next_rid(self) -> int:
@@ -508,8 +566,31 @@ class LLMEngine:
         graphs = getattr(self.r, "mx_graphs", None)
         if not graphs:  # no captured mixed steps (CPU, or DSSE_MIXED_GRAPHS=0): the eager mixed step takes any size
             return True
-        entry = graphs.get(B)
-        return entry is not None and sum(len(c.tokens) for c in chunks) <= entry[0] and len(chunks) <= PREFILL_GRAPH_SEQS
+        T = sum(len(c.tokens) for c in chunks)
+        return self.r.mixed_graph_rows(B, T) is not None and len(chunks) <= PREFILL_GRAPH_SEQS
+
+    def _mixed_budget(self, B: int) -> int:
+        """Prompt rows for this mixed step of bucket B: the runner's default chunk (256), raised to the largest
+        captured size whose measured-cost step stays within the ratio (PassCost.mixed_chunk) -- never lowered
+        below the default: chunks cut to the ratio at small buckets (128 rows at 64 streams) halve the prompt
+        throughput, and at 40 req/s the queue then grows without bound (TTFT p50 0.39 s, profiles/r5/serving_r5.md).
+        A backlog longer than the chunk is split into even shares (two 256-row steps instead of 384 + 128: the
+        longest step, which sets the ITL tail, is shorter)."""
+        sizes = self.r.mixed_chunks(B) if hasattr(self.r, "mixed_chunks") and getattr(self.r, "mx_graphs", None) \
+            else []
+        cap = self.r.mixed_chunk(B)
+        if self.cost is not None and sizes:
+            self.cost.poll()
+            fit = self.cost.mixed_chunk(B, sizes)
+            if fit is not None:
+                cap = max(cap, fit)
+        backlog = sum(len(s.prompt) - s.prefilled for s in self.slots
+                      if s is not None and s.state == "prefill" and not s.aborted)
+        if backlog > cap:
+            n = -(-backlog // cap)  # steps the backlog needs at the cap
+            per = -(-backlog // n)  # their even share
+            cap = min(cap, -(-per // 64) * 64)
+        return max(self.mixed_min_tokens, cap)
 
     def set_itl_ratio(self, ratio: float) -> None:
         """Adaptive prefill budget on (ratio > 1) or off (bench_serving sweeps both in one process)."""
@@ -539,10 +620,14 @@ class LLMEngine:
             if self.waiting:
                 oldest = min(oldest, self.waiting[0].enq_step)
             if self.step_no - oldest <= self.mixed_boost_steps:
-                budget = min(budget, max(self.mixed_min_tokens, self.r.mixed_chunk(B)))
+                budget = min(budget, self._mixed_budget(B))
         chunks, finished = [], []
-        for s in self.slots:
-            if s is None or s.state != "prefill" or s.aborted or budget <= 0:
+        # shortest remaining prompt first (then arrival order): a prompt already half prefilled finishes before a
+        # new one starts, which minimises the mean time to first token
+        pending = sorted((s for s in self.slots if s is not None and s.state == "prefill" and not s.aborted),
+                         key=lambda s: (len(s.prompt) - s.prefilled, s.rid))
+        for s in pending:
+            if budget <= 0:
                 continue
             n = min(len(s.prompt) - s.prefilled, budget)
             last = s.prefilled + n == len(s.prompt)
@@ -614,15 +699,26 @@ class LLMEngine:
             else:
                 producers += [(s.slot, s) for s in prefill_done]
             ran = True
+        est_ms = None  # expected GPU time of the step enqueued now (just-in-time enqueue: jit_delay)
         if dec:
             if mixed:
+                C = r.mixed_graph_rows(B, sum(len(c.tokens) for c in chunks)) if hasattr(r, "mixed_graph_rows") \
+                    else None
+                done = (self.cost.record("mixed", (B, C)) if self.cost is not None and C is not None
+                        and r.device.type == "cuda" else None)
                 r.mixed(B, chunks, ring_row=row)
+                if done:
+                    done()
+                    est_ms = self.cost.mixed_ms(B, C)
                 self.stats["mixed_steps"] += 1
+                hist = self.stats.setdefault("mixed_graph_rows", {})
+                hist[C] = hist.get(C, 0) + 1
             else:
                 done = self.cost.record("decode", B) if self.cost is not None and r.device.type == "cuda" else None
                 r.decode(B)
                 if done:
                     done()
+                    est_ms = None if chunks else self.cost.step_ms.get(B)
             for s in dec:
                 s.decode_enqueued += 1
                 producers.append((s.slot, s))
@@ -634,6 +730,7 @@ class LLMEngine:
         for s in prefill_done:
             s.state = "decode"
             self._dirty_slots.add(s.slot)
+        t_enq = time.perf_counter()
         if ran:
             width = max(sl for sl, _ in producers) + 1 if producers else 1
             self.drain.issue(row, width)
@@ -642,6 +739,7 @@ class LLMEngine:
             self.step_no += 1
         # ---- consume drained steps: keep `depth` steps in flight, process everything that is ready
         wait = 0.0  # blocked on a drain event (GPU time, not host work)
+        t_done = None
         n_main = sum(1 for e in self.inflight if not e[4])
         depth = self.depth
         while self.inflight:
@@ -658,9 +756,13 @@ class LLMEngine:
             if bad:
                 raise EngineFault("; ".join(bad))
             n_main -= 0 if first else 1
-            wait += time.perf_counter() - tw
+            t_done = time.perf_counter()
+            wait += t_done - tw
             self.inflight.popleft()
             self._consume(toks, prods, events)
+        # the newest step started when its predecessor finished (the wait above) or, on an idle GPU, when enqueued
+        if ran:
+            self._jit = (max(t_enq, t_done), est_ms) if n_main == 1 and t_done is not None else (t_enq, est_ms)
         # aborted sequences leave at this boundary
         for s in list(self.slots):
             if s is not None and s.aborted and s.state != "finished" and not any(

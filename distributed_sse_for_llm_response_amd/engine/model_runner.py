@@ -71,13 +71,21 @@ def prefill_row_chunks(T: int, tp: int) -> list:
 PREFILL_SLAB_ROWS = 512
 
 
+# Prompt-chunk sizes of the captured mixed steps: one graph per (decode bucket, C).  The engine sizes each step's
+# chunk from the measured step costs (engine.PassCost.mixed_chunk); a prompt longer than the chunk is split evenly.
+# B + C stays within MIXED_MAX_ROWS: above 512 rows every projection falls off a wave-quantisation cliff (576 rows
+# = three 256-row tiles: 1.5-2.2x the 512-row time, profiles/r5/serving_r5.md), so the largest chunk of bucket B is
+# 512 - B rounded down to 64 rows.
+MIXED_CHUNKS = (128, 256, 384, 512)
+MIXED_MAX_ROWS = 512
+
+
 def mixed_mode() -> str:
-    """DSSE_MIXED: "0" = prompt chunks as separate prefill passes, "1" = mixed prefill + decode steps whenever
-    streams decode, "auto" = mixed steps only for decode buckets of >= DSSE_MIXED_MIN_B rows (default 192): at
-    that load a separate pass per prompt chunk (a whole extra weight stream) pushes the engine into bigger
-    buckets and longer steps, while below it separate passes keep TTFT 30-35 % lower
-    (profiles/r3/serving_arrivals.md)."""
-    return os.environ.get("DSSE_MIXED", "0")
+    """DSSE_MIXED: "1" (default) = prompt chunks ride in the decode step whenever streams decode (mixed prefill +
+    decode steps, chunk sized per step from measured cost), "0" = separate prefill passes, "auto" = mixed steps only
+    for decode buckets of >= DSSE_MIXED_MIN_B rows (default 192).  Separate passes keep TTFT lower but every pass
+    is a whole extra weight stream between two decode tokens: ITL p99 ~3x the step (profiles/r4/serving_r4.md)."""
+    return os.environ.get("DSSE_MIXED", "1")
 
 
 def mixed_min_b() -> int:
@@ -186,7 +194,7 @@ class ModelRunner:
         self.graph_pool = None
         self.pf_graphs = {}   # row bucket -> captured prefill graph
         self.pf = None        # static prefill buffers (allocated by capture)
-        self.mx_graphs = {}   # decode bucket B -> (chunk rows C, captured mixed prefill + decode graph)
+        self.mx_graphs = {}   # decode bucket B -> [(chunk rows C, captured mixed prefill + decode graph)], C ascending
 
     # ------------------------------------------------------------------ decode
     def decode_forward(self, B: int) -> None:
@@ -429,38 +437,49 @@ class ModelRunner:
             self._capture_mixed([b for b in decode_buckets if b >= mixed_min_b()])
 
     def mixed_chunk(self, B: int) -> int:
-        """Prompt rows a mixed step carries beside B decode rows: DSSE_MIXED_CHUNK when set (a fixed chunk: a whole
-        short prompt rides in one step, so the weights stream once for its prefill and the decode step), else the
-        rest of DSSE_MIXED_ROWS (default 128), at least 64; in whole 64-row flash-prefill tiles."""
-        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "256" if mixed_mode() == "auto" else "0"))
+        """The prompt rows of a mixed step before its cost is measured: DSSE_MIXED_CHUNK when set (then the only
+        captured chunk size), else 256; whole 64-row flash-prefill tiles."""
+        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "0"))
+        return -(-fixed // PREFILL_TILE) * PREFILL_TILE if fixed > 0 else 256
+
+    def mixed_chunks(self, B: int) -> list:
+        """The chunk sizes C captured for decode bucket B (B + C rows fit the static prefill buffers)."""
+        fixed = int(os.environ.get("DSSE_MIXED_CHUNK", "0"))
+        tmax = self.pf.tmax if self.pf is not None else 0
         if fixed > 0:
-            return -(-fixed // PREFILL_TILE) * PREFILL_TILE
-        rows = int(os.environ.get("DSSE_MIXED_ROWS", "128"))
-        return max(PREFILL_TILE, -(-(rows - B) // PREFILL_TILE) * PREFILL_TILE)
+            return [c for c in [self.mixed_chunk(B)] if B + c <= tmax]
+        top = (MIXED_MAX_ROWS - B) // PREFILL_TILE * PREFILL_TILE
+        sizes = sorted({c for c in MIXED_CHUNKS if c <= top} | ({top} if top >= MIXED_CHUNKS[0] else set()))
+        return [c for c in sizes if B + c <= tmax]
 
     def _capture_mixed(self, decode_buckets) -> None:
-        """One graph per decode bucket B for the mixed step with C = mixed_chunk(B) prompt rows (ModelRunner.mixed;
-        captured like the decode step: the decode state restored afterwards)."""
-        buckets = [b for b in decode_buckets if b + self.mixed_chunk(b) <= self.pf.tmax]
-        if not buckets:
+        """One graph per (decode bucket B, chunk size C in mixed_chunks(B)) for the mixed step (ModelRunner.mixed;
+        captured like the decode step: the decode state restored afterwards).  mx_graphs[B] = [(C, graph), ...]
+        by ascending C."""
+        pairs = [(B, C) for B in decode_buckets for C in self.mixed_chunks(B)]
+        if not pairs:
             return
         saved = self._snapshot_state()
         self.pf.upload_padding()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for B in buckets:
-                self._mixed_layers(B, self.mixed_chunk(B))
+            for B, C in pairs:  # eager warm-up of every shape (kernel attributes, library state)
+                self._mixed_layers(B, C)
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        for B in sorted(buckets, reverse=True):
-            C = self.mixed_chunk(B)
+        for B, C in sorted(pairs, reverse=True):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
                 self._mixed_layers(B, C)
-            self.mx_graphs[B] = (C, g)
+            self.mx_graphs.setdefault(B, []).insert(0, (C, g))
         torch.cuda.synchronize(self.device)
         self._restore_state(saved)
+
+    def mixed_graph_rows(self, B: int, T: int):
+        """C of the captured mixed graph that a step of bucket B with T prompt rows replays (the smallest C >= T),
+        or None (the step runs eagerly)."""
+        return next((c for c, _ in self.mx_graphs.get(B, ()) if c >= T), None)
 
     def _snapshot_state(self):
         return [t.clone() for t in (self.ids, self.positions, self.ring, self.ring_counter)]
@@ -689,7 +708,7 @@ class ModelRunner:
         """ONE forward over the decode slots [0, B) and the prefill chunks `seqs` (rows B .. B+T-1): every weight
         byte streams once for both, so prompt tokens absorbed while streams decode cost the in-flight streams a
         bigger GEMM (M = B + T rows) instead of a whole extra prefill pass (decode-priority
-        chunked prefill).  A captured graph of bucket B when the chunks fit its C = mixed_chunk(B) rows (metadata
+        chunked prefill).  The captured graph of bucket B with the smallest chunk size C >= the chunks' rows (metadata
         uploaded into the static prefill buffers first), else eagerly.  Decode rows: QKV as a bf16 tile ->
         vectorised RoPE + K/V write for all rows -> decode attention (partitioned flash-decoding) for the B decode
         rows and flash prefill for the chunk rows -> shared o / gate_up / down / norms -> the B decode rows sample
@@ -697,8 +716,8 @@ class ModelRunner:
         prompt sample their first token as prefill() does.  Same tokens as prefill() + decode() (greedy:
         tests/test_mixed_step.py)."""
         T = sum(len(s.tokens) for s in seqs)
-        entry = self.mx_graphs.get(B)
-        if entry is not None and T <= entry[0] and len(seqs) <= PREFILL_GRAPH_SEQS:
+        entry = next(((c, g) for c, g in self.mx_graphs.get(B, ()) if c >= T), None)
+        if entry is not None and len(seqs) <= PREFILL_GRAPH_SEQS:
             q_start, q_len = self.pf.upload(seqs, entry[0], row0=B)
             entry[1].replay()
             self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)

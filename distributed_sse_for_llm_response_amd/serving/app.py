@@ -14,6 +14,7 @@ Engine kinds:
 from __future__ import annotations
 
 import threading
+import os
 import time
 
 import torch
@@ -84,6 +85,9 @@ class EngineLoop(threading.Thread):
         self.last_progress = time.monotonic()
         self.steps = 0
         self.tokenize_errors = 0
+        # just-in-time enqueue (LLMEngine.jit_delay): the host work that must fit between polling the requests and
+        # the in-flight step's end; DSSE_JIT_MARGIN_MS=0 enqueues every step at once (one queued ahead)
+        self.jit_margin_s = float(os.environ.get("DSSE_JIT_MARGIN_MS", "1.5")) / 1e3
         if self._remote:
             engine.on_ttft = self._ttft.append
             engine.on_itl = self._itl.append
@@ -197,6 +201,10 @@ class EngineLoop(threading.Thread):
                 self._observe()
                 if self.faults.active:
                     self.faults.after_step(self.engine)
+                # just-in-time enqueue: poll new requests as late as the in-flight step allows (TTFT)
+                delay = self.engine.jit_delay(self.jit_margin_s) if self.jit_margin_s > 0 else 0.0
+                if delay > 0:
+                    time.sleep(min(delay, 0.05))
         except EngineFault as e:
             # untrusted device state: every live stream ends with [ERROR] now, readiness drops, the process exits
             # non-zero through serve_forever (the orchestrator restarts it; nothing re-execs in this process)

@@ -114,7 +114,8 @@ def test_mixed_prefill_decode_step_logits_match_reference(model, gpu, B, mode):
     n_new = 2
     prompts = [torch.randint(3, CFG.vocab_size, (int(torch.randint(3, 61, (1,), generator=g)),), generator=g).tolist()
                for _ in range(B)]
-    C = r.mx_graphs[B][0]
+    assert [c for c, _ in r.mx_graphs[B]] == r.mixed_chunks(B) and len(r.mx_graphs[B]) >= 3, "one graph per chunk size"
+    C = r.mx_graphs[B][0][0]
     prompts += [torch.randint(3, CFG.vocab_size, (n,), generator=g).tolist() for n in (C // 2 - 5, C // 2 - 9)]
     tables = [list(range(i * PAGES_PER_SEQ, (i + 1) * PAGES_PER_SEQ)) for i in range(B + n_new)]
     r.block_tables.zero_()

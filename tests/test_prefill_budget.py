@@ -56,8 +56,8 @@ def test_decode_step_ema_and_bad_fits():
     assert pc.line() is None and pc.budget(64, 512) is None
 
 
-def test_engine_sizes_prefill_chunks_from_the_cost_model():
-    """With a PassCost attached (as DSSE_PREFILL_ITL_RATIO does on a GPU), a prompt arriving while streams decode is
+def test_engine_sizes_prefill_chunks_from_the_cost_model(monkeypatch):
+    """Separate prefill passes (DSSE_MIXED=0).  With a PassCost attached (as DSSE_PREFILL_ITL_RATIO does on a GPU), a prompt arriving while streams decode is
     prefilled in chunks of the model's budget for the occupied bucket; a prompt starved past boost_steps gets the full
     PREFILL_BUDGET; the token streams equal the fixed-budget engine's (greedy)."""
     import torch
@@ -67,6 +67,7 @@ def test_engine_sizes_prefill_chunks_from_the_cost_model():
     from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
     from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights
 
+    monkeypatch.setenv("DSSE_MIXED", "0")
     w = convert_standard(TINY, init_standard_weights(TINY, seed=11))
 
     def run(cost):
@@ -107,3 +108,70 @@ def test_engine_sizes_prefill_chunks_from_the_cost_model():
     assert 256 in fixed_chunks  # the long prompt's first pass at the fixed budget
     # adaptive: 64-token passes while "a" decodes, until the starvation guard hands the rest the full budget
     assert ad_chunks[1] == 64 and max(ad_chunks) <= 256 and len(ad_chunks) > len(fixed_chunks)
+
+
+def test_mixed_chunk_from_measured_step_costs():
+    """Mixed steps: the extra over the bucket's decode step is fitted against the replayed graph's chunk rows; the
+    chunk is the largest captured size whose step stays within ratio x the decode step."""
+    pc = PassCost(1.85)
+    assert pc.mixed_chunk(128, [128, 256, 384, 512]) is None  # nothing measured yet
+    pc.observe("mixed", (128, 256), 10.0)  # ignored: the bucket's decode step is unknown
+    pc.observe("decode", 128, 6.0)
+    assert pc.mixed_chunk(128, [128, 256, 384, 512]) is None
+    pc.observe("mixed", (128, 256), 6.0 + 0.5 + 0.016 * 256)  # one size: proportional, 18 us / row
+    assert pc.mixed_chunk(128, [128, 256, 384, 512]) == 256  # 5.1 ms of room / 17.95 us -> 284 rows
+    for C in (128, 256, 384, 128, 256):
+        pc.observe("mixed", (128, C), 6.0 + 0.5 + 0.016 * C)  # extra = 0.5 ms + 16 us per prompt row
+    assert abs(pc.mixed_ms(128, 320) - (6.0 + 0.5 + 0.016 * 320)) < 1e-6
+    # room: 0.85 x 6 = 5.1 ms -> C <= 287.5: 256 of the captured sizes
+    assert pc.mixed_chunk(128, [128, 256, 384, 512]) == 256
+    pc.observe("decode", 64, 2.0)  # room 1.7 ms: not even 128 rows fit -> the smallest size
+    assert pc.mixed_chunk(64, [128, 256, 384, 512]) == 128
+    pc.observe("decode", 256, 10.0)  # room 8.5 ms -> 500 rows: 384
+    assert pc.mixed_chunk(256, [128, 256, 384, 512]) == 384
+
+
+def test_mixed_backlog_split_into_even_chunks(monkeypatch):
+    """A prompt backlog longer than the step's chunk goes out in even 64-row-rounded shares (the longest mixed step,
+    which sets the ITL tail, stays short); the streams equal the separate-pass engine's (greedy)."""
+    import torch
+
+    from distributed_sse_for_llm_response_amd.engine.engine import LLMEngine, SamplingParams
+    from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner
+    from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+    from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights
+
+    w = convert_standard(TINY, init_standard_weights(TINY, seed=12))
+
+    def run(mixed):
+        monkeypatch.setenv("DSSE_MIXED", mixed)
+        monkeypatch.setenv("DSSE_MIXED_CHUNK", "256")
+        r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device="cpu", use_graphs=False)
+        e = LLMEngine(r, eos_id=-1, prefill_budget=512)
+        sizes = []
+        orig = r.mixed
+
+        def spy(B, seqs, ring_row):
+            sizes.append(sum(len(s.tokens) for s in seqs))
+            return orig(B, seqs, ring_row=ring_row)
+
+        r.mixed = spy
+        g = torch.Generator().manual_seed(5)
+        out = {}
+        e.add_request("a", torch.randint(3, TINY.vocab_size, (20,), generator=g).tolist(),
+                      SamplingParams(temperature=0.0, max_tokens=12))
+        long_prompt = torch.randint(3, TINY.vocab_size, (300,), generator=g).tolist()
+        for step in range(200):
+            if step == 2:
+                e.add_request("b", long_prompt, SamplingParams(temperature=0.0, max_tokens=4))
+            for ev in e.step():
+                out.setdefault(ev.conversation_id, []).append(ev.token_id)
+            if step > 2 and not e.has_work():
+                break
+        return sizes, out
+
+    mixed_sizes, mixed_out = run("1")
+    sep_sizes, sep_out = run("0")
+    assert mixed_out == sep_out
+    assert sep_sizes == []
+    assert mixed_sizes == [192, 108]  # 300 rows over two steps: ceil(150 / 64) * 64 = 192, then the rest

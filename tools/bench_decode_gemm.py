@@ -7,6 +7,7 @@ A variant is OP[:key=value,...] with the keys of DSSE_KERNEL_CFG; OP is
     split_norm  gemm_resid_split + rmsnorm (slabs reduced in the norm: the TP = 1 decode path)
     resid       gemm_resid (resid += x·wᵀ, no norm)
     out         gemm_out (bf16 out)       silu   gemm_silu
+    lib         torch.matmul on a row-major copy (hipBLASLt: a yardstick only, the engine never calls it)
 Prints one line per (shape, variant): us per call (graph replay, events), effective weight bandwidth.
 """
 import argparse
@@ -41,6 +42,7 @@ def main():
         ncopy = max(2, math.ceil(a.bytes / (N * K * 2)))
         w0 = R.tile_weight(((torch.rand(N, K, generator=g) * 2 - 1) / math.sqrt(K)).bfloat16().to(dev))
         ws = [w0.clone() for _ in range(ncopy)]
+        libw = None
         for M in [int(m) for m in a.M.split(",")]:
             x = (torch.rand(M, K, generator=g) * 2 - 1).bfloat16().to(dev)
             resid = torch.randn(M, N, generator=g).to(dev)
@@ -51,6 +53,9 @@ def main():
             outh = torch.zeros(M, N // 2, device=dev, dtype=torch.bfloat16)
             for var in a.variants.split(","):
                 op, _, cfg = var.partition(":")
+                if op == "lib" and libw is None:
+                    libw = [R.untile_weight(w) for w in ws]
+                    idx = {id(w): i for i, w in enumerate(ws)}
                 os.environ["DSSE_KERNEL_CFG"] = ",".join(c for c in (base_cfg, cfg.replace(";", ",")) if c)
                 ops.refresh_env()
 
@@ -64,6 +69,8 @@ def main():
                         ops.gemm_out(x, w, outb)
                     elif op == "silu":
                         ops.gemm_silu(x, w, outh)
+                    elif op == "lib":
+                        torch.matmul(x, libw[idx[id(w)]].t(), out=outb)
                     else:
                         raise SystemExit(f"unknown op {op}")
 
@@ -88,8 +95,8 @@ def main():
                         e1.record()
                         torch.cuda.synchronize()
                         best = min(best, e0.elapsed_time(e1) * 1e3 / ncopy)
-                    print(f"{shape:8s} M={M:4d} {var:40s} {best:8.2f} us/call  {N * K * 2 / best / 1e6:6.2f} TB/s",
-                          flush=True)
+                    print(f"{shape:8s} M={M:4d} {var:40s} {best:8.2f} us/call  {N * K * 2 / best / 1e6:6.2f} TB/s "
+                          f"{2 * M * N * K / best / 1e6:7.1f} TF/s", flush=True)
                     del graph
                 except Exception as e:  # noqa: BLE001 - report and go on with the next variant
                     print(f"{shape:8s} M={M:4d} {var:40s} FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)

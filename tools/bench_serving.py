@@ -73,10 +73,11 @@ def main():
     ap.add_argument("--prompt-words", type=int, default=500, help="short prompt length (~1 token per word)")
     ap.add_argument("--long-every", type=int, default=0)
     ap.add_argument("--long-words", type=int, default=8000)
-    ap.add_argument("--prefill-budget", default="2048", help="comma list of PREFILL_BUDGET values")
-    ap.add_argument("--itl-ratios", default="0",
-                    help="comma list of DSSE_PREFILL_ITL_RATIO values (0 = fixed budget; r > 1 = adaptive budget "
-                         "capped by PREFILL_BUDGET: a step plus a pass <= r x the bucket's step)")
+    ap.add_argument("--prefill-budget", default="",
+                    help="comma list of PREFILL_BUDGET values (unset: the serving default)")
+    ap.add_argument("--itl-ratios", default="",
+                    help="comma list of DSSE_PREFILL_ITL_RATIO values (0 = fixed sizes; r > 1 = prompt work sized from "
+                         "measured cost so a token gap stays <= r x the bucket's step; unset: the engine default)")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=8448)
     ap.add_argument("--skip-s", type=float, default=2.0)
@@ -103,9 +104,15 @@ def main():
     message = " ".join(f"w{i % 997}" for i in range(a.prompt_words))
     try:
         runs = 0
-        for budget, ratio in [(int(b), float(q)) for b in a.prefill_budget.split(",") for q in a.itl_ratios.split(",")]:
-            app.engine.prefill_budget = budget
-            app.engine.set_itl_ratio(ratio)
+        budgets = [int(b) for b in a.prefill_budget.split(",")] if a.prefill_budget else [None]
+        ratios = [float(q) for q in a.itl_ratios.split(",")] if a.itl_ratios else [None]
+        for budget, ratio in [(b, q) for b in budgets for q in ratios]:
+            if budget is not None:
+                app.engine.prefill_budget = budget
+            if ratio is not None:
+                app.engine.set_itl_ratio(ratio)
+            budget = app.engine.prefill_budget
+            ratio = app.engine.cost.ratio if app.engine.cost is not None else 0.0
             for rate in [float(r) for r in a.rates.split(",")]:
                 for warm, n in ((True, a.warmup_requests), (False, a.requests)):
                     if warm and runs > 0:
@@ -127,8 +134,12 @@ def main():
                            "long_prompt_every": a.long_every, "long_prompt_tokens": a.long_words + 6 if a.long_every else 0,
                            **analyse(res["arrivals"], n, a.long_every, a.skip_s, a.max_tokens),
                            "client_errors": res.get("errors", [])[:3], "engine_stats_cumulative": {
-                               k: app.engine.stats.get(k) for k in ("prefill_tokens", "decode_steps", "steps",
-                                                                    "preemptions", "compactions")}}
+                               k: app.engine.stats.get(k) for k in ("prefill_tokens", "decode_steps", "steps", "mixed_steps",
+                                                                    "mixed_graph_rows", "preemptions", "compactions")},
+                           # the engine's measured decode step per bucket (EMA, ms): ITL p99 is judged against the
+                           # occupied bucket's value
+                           "decode_step_ms": {b: round(v, 3) for b, v in sorted(
+                               (app.engine.cost.step_ms if app.engine.cost is not None else {}).items())}}
                     print(json.dumps(out), flush=True)
     finally:
         client.stdin.close()

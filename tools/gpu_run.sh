@@ -57,6 +57,11 @@ for s in "$@"; do
     serving40_mx512) DSSE_MIXED=1 DSSE_MIXED_CHUNK=512 step serving40_mx512 900 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 512 --itl-ratios 0 ;;
     serving40_mx256) DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving40_mx256 900 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 512 --itl-ratios 0 ;;
     serving13_mx256_d0) DSSE_PIPELINE_DEPTH=0 DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256_d0 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
+    sdef13) step sdef13 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
+    sdef40) step sdef40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
+    sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
+    mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
+    soak) step soak 900 python3 tools/bench_serving.py --rates 40 --requests 2000 --max-tokens 200 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
     kern_test) step kern_test 900 $PYT tests/test_kernels_gpu.py ;;
