@@ -22,8 +22,8 @@
 #include "api.h"
 #include "gemm_epilogue.h"
 
-#ifndef DSSE_ATTN_NT
-#define DSSE_ATTN_NT 1
+#ifndef ATTN_DECODE_NT
+#define ATTN_DECODE_NT 1
 #endif
 
 namespace dsse {
@@ -76,10 +76,10 @@ paged_attention_kernel(AttnParams p) {
     const __attribute__((address_space(4))) int* cbt = (const __attribute__((address_space(4))) int*)bt;
     return DSSE_IDX(cbt[i], p.num_blocks, 0);
   };
-  // decode (QW = 1): every K/V byte is read once, by one wave -> non-temporal loads (DSSE_ATTN_NT, default on:
+  // decode (QW = 1): every K/V byte is read once, by one wave -> non-temporal loads (ATTN_DECODE_NT, default on:
   // tools/kvbench.hip measured this access pattern at 6.3 TB/s nt vs 3.6 TB/s default policy); prefill tiles
   // (QW > 1) share the lines through L1
-  constexpr bool NT = DSSE_ATTN_NT && QW == 1;
+  constexpr bool NT = ATTN_DECODE_NT && QW == 1;
   auto ldkv = [&](const bf16* a) { return NT ? ld_nt_bf16x8(a) : ld_bf16x8(a); };
   auto load_k = [&](int page, bf16x8 (&k0)[4], bf16x8 (&k1)[4]) {
     const bf16* kp = p.k_cache + ((size_t)page * p.hkv + h) * kPage * kD;

@@ -179,15 +179,15 @@ static hipError_t launch_t(const bf16* X, int ldx, int M, const bf16* W, int K, 
 template <int MODE>
 static hipError_t launch_mode(int mt, int nt, int kw, const bf16* X, int ldx, int M, const bf16* W,
                               int K, int N, const GemmEpi& ep, hipStream_t st) {
-#define DSSE_GEMM_CASE(MT_, NT_, KW_) \
+#define K_GEMM_CASE(MT_, NT_, KW_) \
   if (mt == MT_ && nt == NT_ && kw == KW_) return launch_t<MT_, NT_, KW_, MODE>(X, ldx, M, W, K, N, ep, st);
-#define DSSE_GEMM_MT(MT_) \
-  DSSE_GEMM_CASE(MT_, 1, 4) DSSE_GEMM_CASE(MT_, 1, 8) DSSE_GEMM_CASE(MT_, 2, 4) DSSE_GEMM_CASE(MT_, 2, 8)
-  DSSE_GEMM_MT(1) DSSE_GEMM_MT(2)
+#define K_GEMM_MT(MT_) \
+  K_GEMM_CASE(MT_, 1, 4) K_GEMM_CASE(MT_, 1, 8) K_GEMM_CASE(MT_, 2, 4) K_GEMM_CASE(MT_, 2, 8)
+  K_GEMM_MT(1) K_GEMM_MT(2)
   // MT = 4 (M <= 64): NT = 2 at KW = 8 spills past the 256-VGPR budget of 2 waves/SIMD.
-  DSSE_GEMM_CASE(4, 1, 4) DSSE_GEMM_CASE(4, 1, 8) DSSE_GEMM_CASE(4, 2, 4)
-#undef DSSE_GEMM_MT
-#undef DSSE_GEMM_CASE
+  K_GEMM_CASE(4, 1, 4) K_GEMM_CASE(4, 1, 8) K_GEMM_CASE(4, 2, 4)
+#undef K_GEMM_MT
+#undef K_GEMM_CASE
   return hipErrorInvalidValue;
 }
 

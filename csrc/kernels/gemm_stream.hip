@@ -23,8 +23,8 @@
 #include <cstdlib>
 #include <type_traits>
 
-#ifndef DSSE_X_TOUCH
-#define DSSE_X_TOUCH 1  // L2 warm-up loads of the next X slice (see the kernel)
+#ifndef STREAM_X_TOUCH
+#define STREAM_X_TOUCH 1  // L2 warm-up loads of the next X slice (see the kernel)
 #endif
 
 #ifndef DSSE_XCD_SPLITK
@@ -128,7 +128,7 @@ gemm_stream_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __res
   // that never executes (M >= 0), so the loads stay.
   // Only for the wide-N launches (7-8 waves, no split-K: gate_up, LM head): the split-K narrow projections,
   // with 2-7 slices per workgroup, measured slower with it (+140 us per 64-stream step).
-  constexpr bool TOUCH = DSSE_X_TOUCH && NW >= 7;
+  constexpr bool TOUCH = STREAM_X_TOUCH && NW >= 7;
   constexpr int LPR = CPS * 2;                 // 128-B lines per X row of a slice
   constexpr int TOUCH_PT = (MP * LPR + 64 * NW - 1) / (64 * NW);
   const int touch_last_row = min(M - m0, MP) - 1;
@@ -271,18 +271,18 @@ static hipError_t launch_s_mode(int mt, int nt, int nw, int rd, const bf16* X, i
   // two column tiles per wave: every X fragment read from LDS feeds two MFMAs
   if (mt == 8 && nt == 2 && nw == 4 && rd == 2) return launch_s<8, 2, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   if (mt == 16 && nt == 2 && nw == 4 && rd == 2) return launch_s<16, 2, 4, 2, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-#define DSSE_S_CASE(MT_, NT_, NW_, RD_)         \
+#define K_S_CASE(MT_, NT_, NW_, RD_)         \
   if (mt == MT_ && nt == NT_ && nw == NW_ && rd == RD_) \
     return launch_s<MT_, NT_, NW_, RD_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
-#define DSSE_S_MT(MT_) \
-  DSSE_S_CASE(MT_, 1, 8, 1) DSSE_S_CASE(MT_, 2, 8, 1) DSSE_S_CASE(MT_, 1, 4, 1) DSSE_S_CASE(MT_, 1, 4, 2) DSSE_S_CASE(MT_, 1, 8, 2)
-  DSSE_S_MT(1) DSSE_S_MT(2) DSSE_S_MT(4)
+#define K_S_MT(MT_) \
+  K_S_CASE(MT_, 1, 8, 1) K_S_CASE(MT_, 2, 8, 1) K_S_CASE(MT_, 1, 4, 1) K_S_CASE(MT_, 1, 4, 2) K_S_CASE(MT_, 1, 8, 2)
+  K_S_MT(1) K_S_MT(2) K_S_MT(4)
   // odd wave counts so that N / 16 / nw x S lands on the 256 CUs (qkv 384 tile groups: nw 3 x S 2; gate_up
   // 1792: nw 7; 36 MB-class narrow layers: nw 6)
-  DSSE_S_CASE(4, 1, 3, 1) DSSE_S_CASE(4, 1, 5, 1) DSSE_S_CASE(4, 1, 6, 1) DSSE_S_CASE(4, 1, 7, 1)
-  DSSE_S_CASE(4, 1, 2, 1)
-#undef DSSE_S_MT
-#undef DSSE_S_CASE
+  K_S_CASE(4, 1, 3, 1) K_S_CASE(4, 1, 5, 1) K_S_CASE(4, 1, 6, 1) K_S_CASE(4, 1, 7, 1)
+  K_S_CASE(4, 1, 2, 1)
+#undef K_S_MT
+#undef K_S_CASE
   return hipErrorInvalidValue;
 }
 
@@ -442,15 +442,15 @@ constexpr int ring_depth(int mt, int nw) {
 template <int MODE>
 static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                                 const GemmEpi& ep, float* part, hipStream_t st) {
-#define DSSE_R_CASE(MT_, NW_) \
+#define K_R_CASE(MT_, NW_) \
   if (mt == MT_ && nw == NW_)  \
     return launch_r<MT_, NW_, ring_depth(MT_, NW_), MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
-  DSSE_R_CASE(8, 4)
+  K_R_CASE(8, 4)
   // (4, 5) is served by gemm_ring2 only: this kernel's 5-wave form wrote one wave's columns wrong (round 3)
-  DSSE_R_CASE(4, 3) DSSE_R_CASE(4, 4) DSSE_R_CASE(4, 6) DSSE_R_CASE(4, 7) DSSE_R_CASE(4, 8)
-  DSSE_R_CASE(2, 4) DSSE_R_CASE(2, 7) DSSE_R_CASE(2, 8)
-#undef DSSE_R_CASE
+  K_R_CASE(4, 3) K_R_CASE(4, 4) K_R_CASE(4, 6) K_R_CASE(4, 7) K_R_CASE(4, 8)
+  K_R_CASE(2, 4) K_R_CASE(2, 7) K_R_CASE(2, 8)
+#undef K_R_CASE
   return hipErrorInvalidValue;
 }
 
@@ -618,16 +618,16 @@ template <int MODE>
 static hipError_t launch_r2_mode(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                                  const GemmEpi& ep, float* part, hipStream_t st) {
   const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
-#define DSSE_R2_CASE(MT_, NW_, XL_, DX_, DW_) \
+#define K_R2_CASE(MT_, NW_, XL_, DX_, DW_) \
   if (mt == MT_ && nw == NW_) return launch_r2<MT_, NW_, XL_, DX_, DW_, MODE>(X, ldx, M, W, K, N, S, ep, part, st);
   // 33-64 rows: X slot 16 KiB x 3
-  DSSE_R2_CASE(4, 3, 1, 3, 8) DSSE_R2_CASE(4, 4, 1, 3, 7) DSSE_R2_CASE(4, 5, 1, 3, 5) DSSE_R2_CASE(4, 6, 1, 3, 4)
-  DSSE_R2_CASE(4, 7, 1, 3, 4) DSSE_R2_CASE(4, 8, 1, 3, 3)
+  K_R2_CASE(4, 3, 1, 3, 8) K_R2_CASE(4, 4, 1, 3, 7) K_R2_CASE(4, 5, 1, 3, 5) K_R2_CASE(4, 6, 1, 3, 4)
+  K_R2_CASE(4, 7, 1, 3, 4) K_R2_CASE(4, 8, 1, 3, 3)
   // 17-32 rows: X slot 8 KiB x 3
-  DSSE_R2_CASE(2, 3, 1, 3, 10) DSSE_R2_CASE(2, 4, 1, 3, 8) DSSE_R2_CASE(2, 7, 1, 3, 4) DSSE_R2_CASE(2, 8, 1, 3, 4)
+  K_R2_CASE(2, 3, 1, 3, 10) K_R2_CASE(2, 4, 1, 3, 8) K_R2_CASE(2, 7, 1, 3, 4) K_R2_CASE(2, 8, 1, 3, 4)
   // 65-128 rows: X slot 32 KiB x 3, two loader waves
-  DSSE_R2_CASE(8, 4, 2, 3, 4)
-#undef DSSE_R2_CASE
+  K_R2_CASE(8, 4, 2, 3, 4)
+#undef K_R2_CASE
   return hipErrorInvalidValue;
 }
 

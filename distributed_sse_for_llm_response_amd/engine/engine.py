@@ -17,13 +17,13 @@ Per ``step()`` (host, a few hundred microseconds of Python):
    finished or paused streams do not keep the step on a bigger captured graph;
 3. upload slot metadata that changed (block tables, sampling params, active mask) with pinned,
    non-blocking copies on the compute stream;
-4. run prefill chunks within a per-step token budget (decode-priority chunked prefill: running
-   streams keep their inter-token latency while new prompts are absorbed).  With ``DSSE_MIXED=1`` the chunk
-   rides in the decode step itself instead (``ModelRunner.mixed``: one forward over the B decode rows + the
-   chunk's rows, every weight byte streamed once) with a budget that keeps the step near the next row bucket
-   (``DSSE_MIXED_ROWS`` - B tokens, at least 64); a prompt queued for more than ``DSSE_MIXED_BOOST_STEPS``
-   steps raises the budget to PREFILL_BUDGET (the TTFT guard; counted in steps, so TP ranks agree).  Off by
-   default: run eagerly it measured slower than separate passes (``profiles/r3/serving_arrivals.md``);
+4. absorb prompt work.  Default (``DSSE_MIXED=1``): the prompt chunk rides in the decode step itself
+   (``ModelRunner.mixed``: one forward over the B decode rows + the chunk's rows, every weight byte streamed once,
+   replayed from the graph of (B, chunk size)).  The chunk starts at 256 rows and grows to the largest captured
+   size whose measured step cost stays within ``DSSE_PREFILL_ITL_RATIO`` x the bucket's decode step
+   (``PassCost``); a longer backlog is split into even shares, shortest prompt first; a prompt queued for more
+   than 40 steps gets the full PREFILL_BUDGET (the TTFT guard; counted in steps, so TP ranks agree).
+   ``DSSE_MIXED=0``: separate prefill passes within a per-step token budget (decode-priority chunked prefill);
 5. replay the captured decode graph of the batch bucket (sampled ids stay on the device and feed the
    next step; token ring row ``t`` receives every token produced in step ``t``);
 6. start the device->host copy of ring row ``t`` on a side stream, then process the drained rows of
@@ -50,7 +50,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .kv_cache import PAGE, BlockAllocator, blocks_needed
-from .model_runner import PREFILL_GRAPH_SEQS, RING_SIZE, ModelRunner, PrefillSeq, batch_buckets, mixed_min_b, mixed_mode
+from .model_runner import PREFILL_GRAPH_SEQS, RING_SIZE, ModelRunner, PrefillSeq, batch_buckets, mixed_mode
 
 
 @dataclass
@@ -305,9 +305,10 @@ class LLMEngine:
         self.on_flush = None
         # mixed prefill + decode steps (ModelRunner.mixed); DSSE_MIXED=0 runs chunks as separate prefill passes
         self.mixed = mixed_mode() != "0" and hasattr(runner, "mixed")
-        self.mixed_min_b = mixed_min_b()  # "auto": mixed steps only from this decode bucket up
-        self.mixed_min_tokens = int(os.environ.get("DSSE_MIXED_MIN_TOKENS", "64"))
-        self.mixed_boost_steps = int(os.environ.get("DSSE_MIXED_BOOST_STEPS", "40"))
+        self.mixed_min_tokens = 64
+        # a prompt queued longer than this many steps gets the full prefill budget (TTFT guard, counted in steps:
+        # identical on every TP rank)
+        self.mixed_boost_steps = 40
         # adaptive prefill budget (separate passes while streams decode): DSSE_PREFILL_ITL_RATIO = r > 1 sizes each
         # pass so that a token gap spanning a decode step and a pass stays <= r x the occupied bucket's step
         # (PassCost), up to prefill_budget; a prompt that has waited DSSE_PREFILL_BOOST_STEPS steps gets the full
@@ -610,7 +611,7 @@ class LLMEngine:
             adaptive = self.cost.budget(self._decode_bucket(), self.prefill_budget)
             if adaptive is not None and self.step_no - self._oldest_prefill_step() <= self.boost_steps:
                 budget = adaptive
-        if running_decode and self.mixed and self._decode_bucket() >= self.mixed_min_b:
+        if running_decode and self.mixed:
             # the chunk rides in the decode step: keep B + chunk near the next row bucket, unless a prompt has
             # waited too long (counted in steps: identical on every TP rank)
             hi = max((s.slot for s in self.slots if s is not None and s.state == "decode"), default=-1) + 1
@@ -683,7 +684,7 @@ class LLMEngine:
                and not s.stop_after_enqueue and not s.paused]
         B = next(b for b in batch_buckets(r.max_batch) if b >= max(s.slot for s in dec) + 1) if dec else 0
         # a mixed step only when the chunks fit its captured graph (a starved prompt's big budget: separate passes)
-        mixed = bool(chunks) and bool(dec) and self.mixed and B >= self.mixed_min_b and self._mixed_fits(B, chunks)
+        mixed = bool(chunks) and bool(dec) and self.mixed and self._mixed_fits(B, chunks)
         if chunks:
             if not mixed:
                 done = (self.cost.record("prefill", sum(len(c.tokens) for c in chunks))

@@ -48,7 +48,7 @@ PREFILL_GRAPH_SEQS = 16  # sequences per captured prefill batch (more: eager)
 # norms); larger buckets take the wide path (_decode_layers_wide), whose projections the kernel library routes to
 # gemm_wide / gemm_tiled by row count (bindings.cpp gemm_impl).  Round 1 measured the split at 128 rows
 # (profiles/bucket_ab_r1.md).
-DECODE_GEMM_MAX_M = int(os.environ.get("DSSE_DECODE_GEMM_MAX_M", "128"))
+DECODE_GEMM_MAX_M = 128
 # Health words (runner.health, int32 on the device, copied to the host with every drained step; nonzero = the step's
 # outputs cannot be trusted and the engine fails: engine.py EngineFault).
 HEALTH_TP_PEER = 0      # a TP peer's all-reduce row did not arrive in time (allreduce.hip)
@@ -82,14 +82,10 @@ MIXED_MAX_ROWS = 512
 
 def mixed_mode() -> str:
     """DSSE_MIXED: "1" (default) = prompt chunks ride in the decode step whenever streams decode (mixed prefill +
-    decode steps, chunk sized per step from measured cost), "0" = separate prefill passes, "auto" = mixed steps only
-    for decode buckets of >= DSSE_MIXED_MIN_B rows (default 192).  Separate passes keep TTFT lower but every pass
-    is a whole extra weight stream between two decode tokens: ITL p99 ~3x the step (profiles/r4/serving_r4.md)."""
+    decode steps, chunk sized per step from measured cost), "0" = separate prefill passes.  Separate passes keep
+    TTFT lower but every pass is a whole extra weight stream between two decode tokens: ITL p99 ~3x the step
+    (profiles/r4/serving_r4.md, profiles/r5/serving_r5.md)."""
     return os.environ.get("DSSE_MIXED", "1")
-
-
-def mixed_min_b() -> int:
-    return int(os.environ.get("DSSE_MIXED_MIN_B", "192" if mixed_mode() == "auto" else "0"))
 
 
 def batch_buckets(max_batch: int):
@@ -434,7 +430,7 @@ class ModelRunner:
             self.pf_graphs[tb] = g
         torch.cuda.synchronize(self.device)
         if mixed_mode() != "0" and os.environ.get("DSSE_MIXED_GRAPHS", "1") != "0":
-            self._capture_mixed([b for b in decode_buckets if b >= mixed_min_b()])
+            self._capture_mixed(list(decode_buckets))
 
     def mixed_chunk(self, B: int) -> int:
         """The prompt rows of a mixed step before its cost is measured: DSSE_MIXED_CHUNK when set (then the only

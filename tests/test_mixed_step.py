@@ -52,13 +52,10 @@ def test_mixed_forward_equals_prefill_then_decode():
 
 def _engine_tokens(mixed: bool):
     os.environ["DSSE_MIXED"] = "1" if mixed else "0"
-    os.environ["DSSE_MIXED_ROWS"] = "12"
-    os.environ["DSSE_MIXED_MIN_TOKENS"] = "8"
     try:
         e = LLMEngine(_runner(), eos_id=-1, prefill_budget=64)
     finally:
-        for k in ("DSSE_MIXED", "DSSE_MIXED_ROWS", "DSSE_MIXED_MIN_TOKENS"):
-            os.environ.pop(k, None)
+        os.environ.pop("DSSE_MIXED", None)
     out = {}
     for step in range(60):
         if step in (0, 4, 9):
