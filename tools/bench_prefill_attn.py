@@ -4,7 +4,7 @@
 
     python tools/bench_prefill_attn.py [--T 8192,512] [--iters 10] [--rounds 3] [--sdpa]
 
-Prints us per call and TFLOP/s (causal FLOPs = 2 * 2 * Hq * d * T (T + 1) / 2), then a JSON summary.  --sdpa adds
+Timed as a captured graph of --iters calls (the engine's form; --eager: back-to-back eager calls).  Prints us per call and TFLOP/s (causal FLOPs = 2 * 2 * Hq * d * T (T + 1) / 2), then a JSON summary.  --sdpa adds
 torch's scaled_dot_product_attention on the same (contiguous) data as a library arm, interleaved in one process.
 Under rocprofv3 --pmc use --rounds 1 --iters 3: the kernel trace then holds only this kernel (plus torch's
 random fills, which run before the first timed call and have different names).
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sdpa", action="store_true")
+    ap.add_argument("--mode1", default="", help="comma list of key partition counts for mode-1 arms")
+    ap.add_argument("--eager", action="store_true", help="time eager back-to-back calls instead of a graph")
     args = ap.parse_args()
     ops.load_library(required=True)
     dev = torch.device("cuda", 0)
@@ -56,6 +58,17 @@ def main():
                                 dummy, dummy, 32 * math.ceil((T + 31) / 32), 1)
 
         arms = {"flash": flash}
+        # --mode1 N,...: the decode-style kernel on 64-query work items (4 tiles of 16) with the keys in N partitions
+        # merged by the combine kernel (paged_attention mode 1): more workgroups for short prompts
+        # (a mode-1 work item is 4 tiles of 16 / G queries: 16 queries of all G heads at G = 4)
+        n1 = math.ceil(T / 16)
+        wt1, ws1 = torch.arange(n1 - 1, -1, -1, **i32), torch.zeros(n1, **i32)
+        for npart in [int(v) for v in args.mode1.split(",") if v]:
+            part = 32 * math.ceil(T / npart / 32)
+            po = torch.empty(n1 * args.hkv * npart * 64 * 128, device=dev)
+            pml = torch.empty(n1 * args.hkv * npart * 64 * 2, device=dev)
+            arms[f"m1p{npart}"] = (lambda po=po, pml=pml, part=part, npart=npart: ops.paged_attention(
+                1, q, k_cache, v_cache, bt, q_start, q_len, ctx_len, ws1, wt1, out, po, pml, part, npart))
         if args.sdpa:
             # contiguous [1, H, T, d] copies of the same K/V (GQA expanded), causal
             kk = k_cache[bt[0].long()].permute(1, 0, 2, 3).reshape(args.hkv, T, 128)
@@ -71,19 +84,48 @@ def main():
         torch.cuda.synchronize()
         first = out.clone()
         times = {k: [] for k in arms}
+        # timed as a captured graph of `iters` calls (as the engine runs prefill): a short prompt's kernel is shorter
+        # than the host's per-call dispatch, so eager back-to-back calls would time the host
+        graphs = {}
+        if not args.eager:
+            for k, fn in arms.items():
+                if k == "sdpa":
+                    continue
+                fn()
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(args.iters):
+                        fn()
+                graphs[k] = g
         for _ in range(args.rounds):
             for k, fn in arms.items():
                 fn()
                 torch.cuda.synchronize()
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
-                for _ in range(args.iters):
-                    fn()
+                if k in graphs:
+                    graphs[k].replay()
+                else:
+                    for _ in range(args.iters):
+                        fn()
                 en.record()
                 torch.cuda.synchronize()
                 times[k].append(st.elapsed_time(en) * 1e3 / args.iters)
         # race screen: the kernel is deterministic, so every call must reproduce the first output bit for bit
+        flash()
+        torch.cuda.synchronize()
         same = bool(torch.equal(first, out))
+        for k in arms:
+            if k.startswith("m1p"):
+                out.zero_()
+                arms[k]()
+                torch.cuda.synchronize()
+                err = (out.float() - first.float()).abs().max().item()
+                res[f"T{T}_{k}_max_abs_vs_flash"] = round(err, 5)
+                print(f"T={T:6d} {k} max |out - flash| = {err:.5f}", flush=True)
+        flash()
+        torch.cuda.synchronize()
         res[f"T{T}_repeat_identical"] = same
         print(f"T={T:6d} repeated calls bit-identical: {same}", flush=True)
         if args.sdpa:
