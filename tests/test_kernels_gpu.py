@@ -244,14 +244,13 @@ def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
     _close(vc, vr, 3e-2, 2e-2, "v cache")
 
 
-@pytest.mark.parametrize("cfg", ["auto", "tiled-default", "tiled-128-split2", "tiled-256x64"])
+@pytest.mark.parametrize("cfg", ["auto", "tiled-default", "tiled-128-split2", "tiled-128x256", "pipe-256sq"])
 @pytest.mark.parametrize("M", [129, 192, 200, 256])
 def test_decode_bucket_epilogues(gpu, monkeypatch, cfg, M):
     """Every epilogue of the 129-256-row decode buckets (bf16 / fp32 store, residual add, SiLU*mul, QKV + RoPE +
     K/V write, split-K slabs reduced by the norm) on the tiled kernels, at row counts that are not multiples of
     the tile height, against the fp32 reference."""
-    for k, v in GEMM_CONFIGS[cfg].items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(**GEMM_CONFIGS[cfg]))
     ops.refresh_env()
     g = torch.Generator().manual_seed(M * 7 + len(cfg))
     K = 2048
@@ -431,8 +430,7 @@ def test_paged_attention_decode(gpu, ctxs, part):
 def test_qkv_attention_decode_folded_epilogue(gpu, monkeypatch, cfg, M, part):
     """Attention mode 3 (QKV split-K reduce + RoPE + K/V write folded into the decode attention kernel) against
     the two-op path (gemm_qkv_rope + decode attention): same K/V cache bytes, same attention output."""
-    for k, v in GEMM_CONFIGS[cfg].items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(**GEMM_CONFIGS[cfg]))
     nh, nkv, H = 32, 8, 1024
     g = torch.Generator().manual_seed(M * 31 + part)
     ctxs = torch.randint(1, 700, (M,), generator=g).tolist()
