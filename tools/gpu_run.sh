@@ -59,6 +59,8 @@ for s in "$@"; do
     serving13_mx256_d0) DSSE_PIPELINE_DEPTH=0 DSSE_MIXED=1 DSSE_MIXED_CHUNK=256 step serving13_mx256_d0 900 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --prefill-budget 512 --itl-ratios 0 ;;
     sdef13) step sdef13 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     sdef40) step sdef40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
+    sdef13j08) DSSE_JIT_MARGIN_MS=0.8 step sdef13j08 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
+    sdef40j08) DSSE_JIT_MARGIN_MS=0.8 step sdef40j08 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
     sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
     soak) step soak 900 python3 tools/bench_serving.py --rates 40 --requests 2000 --max-tokens 200 ;;
