@@ -270,11 +270,12 @@ TCfg pick_tiled(int M, int N, int K) {
   const int BM = cfg == 1 || cfg == 5 ? 128 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
   c.cfg = cfg;
   c.S = 1;
-  c.ok = N % BN == 0 && K % (cfg == 8 ? 128 : 64) == 0;
+  const bool pipe = cfg == 8;
+  c.ok = N % BN == 0 && K % (pipe ? 128 : 64) == 0;
   if (!c.ok) return c;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   int S = env_int("t_split", 0);
-  const int kq = cfg == 8 ? 128 : 64;  // K granule of a slice (gemm_pipe: >= 2 steps of 64)
+  const int kq = pipe ? 128 : 64;  // K granule of a slice (gemm_pipe: >= 2 steps of 64)
   if (S <= 0 || K % (kq * S) != 0) {
     S = 1;  // split K only for the few-tile wide-decode shapes (slabs cost M x N x 4 B each)
     while (M <= kMaxDecodeM && tiles * S < min_wgs && K % (kq * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;

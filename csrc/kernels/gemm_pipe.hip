@@ -8,22 +8,26 @@
 //
 //   * 8 waves = 2 wave rows (128 rows each) x 4 wave columns (64 columns each); a wave's 128 x 64 tile is four
 //     64 x 32 quadrants; a K step of 64 runs as four phases, one quadrant (16 MFMAs 16x16x32) per phase:
-//         phase 0  quadrant (0, 0)   reads A rows q0 + B cols q0   issue  A-half 1 of step t+1
-//         phase 1  quadrant (0, 1)   reads B cols q1
-//         phase 2  quadrant (1, 1)   reads A rows q1                issue  A-half 0, B-half 0 of step t+2
-//         phase 3  quadrant (1, 0)   (operands in registers)        issue  B-half 1 of step t+2
+//         phase 0  quadrant (0, 0)   reads A rows q0 + B cols q0   issue  B-half 1 of step t+1
+//         phase 1  quadrant (0, 1)   reads B cols q1                issue  A-half 1 of step t+1
+//         phase 2  quadrant (1, 1)   reads A rows q1                issue  A-half 0 of step t+2
+//         phase 3  quadrant (1, 0)   (operands in registers)        issue  B-half 0 of step t+2
+//     one half-tile per phase (round 5: +1-5 % at 8192 rows, +2-10 % at 2048 over the round-5 first form that issued
+//     0 / 1 / 2 / 1 half-tiles in phases 1 / 0 / 2 / 3, profiles/r5/pipe_even_ab_r5.log),
 //     each phase = [fragment reads, DMA issue, counted vmcnt] s_barrier lgkmcnt(0) [16 MFMAs, prio 1] s_barrier,
 //     with the two wave rows one barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other's LDS
 //     reads (the 8-phase template of the CDNA HIP guide, §5; the half-tile order is this kernel's own);
 //   * a "half-tile" is what one phase's quadrant reads across the workgroup: A-half q = the 64-row quadrant q of
 //     BOTH wave rows (128 rows x 128 B = 16 KiB), B-half q = the 32-column quadrant q of all four wave columns
 //     (8 column tiles x 2 KiB); each is 16 one-KiB LDS-DMA instructions, two per wave;
-//   * WAR: a half of buffer t & 1 is re-staged (for step t+2) only in a phase after the one whose reads retired it
-//     (A0 / B0 read in phase 0, re-staged in phase 2; B1 read in 1, re-staged in 3; A1 read in 2, re-staged in
-//     phase 0 of step t+1) -- with the lagging wave row that is still >= 1 barrier after its lgkmcnt(0);
-//   * RAW: counted waits -- phase 0 retires B-half 1 of step t (vmcnt 10), phase 1 A-half 1 of step t (vmcnt 8),
-//     phase 3 A0 / B0 of step t+1 (vmcnt 10) -- each in the phase before the first read, so the lagging row has
-//     passed it one barrier before the leading row reads (never vmcnt(0) in the steady loop);
+//   * WAR: a half is re-staged >= 2 phases after its last read (A0 / B0 of buffer t & 1 read in phase 0 of t,
+//     re-staged for t+2 in phases 2 / 3; B1 of buffer (t+1) & 1 last read in phase 1 of t-1, re-staged in phase 0 of
+//     t; A1 read in phase 2 of t-1, re-staged in phase 1 of t) -- the lagging wave row is then still >= 1 barrier
+//     past its lgkmcnt(0);
+//   * RAW: counted waits, 8 in each of phases 0, 1 and 3 (four half-tiles of 2 instructions each younger than the
+//     one retired): phase 0 retires B-half 1 of step t, phase 1 A-half 1 of t, phase 3 A0 / B0 of t+1 -- each in the
+//     phase before its first read, so the lagging row has passed it one barrier before the leading row reads (never
+//     vmcnt(0) in the steady loop);
 //   * buffer-load LDS-DMA: one SGPR offset per K step, per-lane offsets fixed for the whole loop (no per-step VALU
 //     address arithmetic); rows past M read as zeros (out-of-range offsets, no memory traffic); the last two steps
 //     issue nothing past the end and count their waits exactly;
@@ -161,50 +165,56 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
     asm volatile("s_barrier" ::: "memory");
   };
 
-  // ---- prologue: step 0 whole, step 1 without its A-half 1 (issued in phase 0 of step 0, as in the loop)
-  issue_a(0, 0);
-  issue_b(0, 0);
-  issue_b(1, 0);
-  issue_a(1, 0);
-  issue_a(0, 1);
-  issue_b(0, 1);
-  issue_b(1, 1);
-  asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");  // A0 / B0 of step 0 landed everywhere
-  if (wm == 1) asm volatile("s_barrier" ::: "memory");  // wave row 1 runs one barrier behind row 0
-
-  // one K step; TAIL 0 = steady, 1 = step t+1 exists but t+2 does not, 2 = last step
-  auto step = [&](int t, auto tail_tag) {
-    constexpr int TAIL = decltype(tail_tag)::value;
-    const char* buf = smem + (t & 1) * kBuf;
-    // LDS-DMA issued in the fragment-read sections (counts: file header)
-    read_a(buf, 0);
-    read_b(buf, 0);
-    if constexpr (TAIL < 2) issue_a(1, t + 1);
-    if constexpr (TAIL < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B-half 1 of step t
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    mma(0, 0);
-    read_b(buf, 1);
-    if constexpr (TAIL < 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-half 1 of step t
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    mma(0, 1);
-    read_a(buf, 1);
-    if constexpr (TAIL == 0) {
-      issue_a(0, t + 2);
-      issue_b(0, t + 2);
-    }
-    mma(1, 1);
-    if constexpr (TAIL == 0) {
-      issue_b(1, t + 2);
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0 / B0 of step t+1
-    } else if constexpr (TAIL == 1) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    mma(1, 0);
-  };
-  int t = 0;
-  for (; t < nk - 2; ++t) step(t, std::integral_constant<int, 0>{});
-  step(t++, std::integral_constant<int, 1>{});  // nk >= 2 (host contract)
-  step(t, std::integral_constant<int, 2>{});
+  {
+    // prologue: step 0 whole, then A0 / B0 of step 1 (its B1 / A1 go out in phases 0 / 1 of step 0)
+    issue_a(0, 0);
+    issue_b(0, 0);
+    issue_b(1, 0);
+    issue_a(1, 0);
+    issue_a(0, 1);
+    issue_b(0, 1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // A0 / B0 of step 0 landed everywhere
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");  // wave row 1 runs one barrier behind row 0
+    // TAIL 0 = steady, 1 = step t+1 exists but t+2 does not, 2 = last step.  RAW: B1(t) waited in phase 0 and read
+    // in phase 1, A1(t) waited in 1 and read in 2, A0 / B0(t+1) waited in 3 and read in phase 0 of t+1 (the
+    // barrier that opens the reading phase follows every wave's wait).  WAR: B1 of buffer (t+1)&1 was last read in
+    // phase 1 of t-1, A1 in phase 2 of t-1, A0 / B0 of buffer t&1 in phase 0 of t -- each restaged >= 2 phases later.
+    auto step_even = [&](int t, auto tail_tag) {
+      constexpr int TAIL = decltype(tail_tag)::value;
+      const char* buf = smem + (t & 1) * kBuf;
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if constexpr (TAIL < 2) {
+        issue_b(1, t + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B-half 1 of step t
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      mma(0, 0);
+      read_b(buf, 1);
+      if constexpr (TAIL < 2) {
+        issue_a(1, t + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-half 1 of step t
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      mma(0, 1);
+      read_a(buf, 1);
+      if constexpr (TAIL == 0) issue_a(0, t + 2);
+      mma(1, 1);
+      if constexpr (TAIL == 0) {
+        issue_b(0, t + 2);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0 / B0 of step t+1
+      } else if constexpr (TAIL == 1) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      mma(1, 0);
+    };
+    int t = 0;
+    for (; t < nk - 2; ++t) step_even(t, std::integral_constant<int, 0>{});
+    step_even(t++, std::integral_constant<int, 1>{});  // nk >= 2 (host contract)
+    step_even(t, std::integral_constant<int, 2>{});
+  }
   // balance the barrier count of the two rows
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
 

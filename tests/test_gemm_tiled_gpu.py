@@ -98,7 +98,8 @@ def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
     _check(vc.cpu(), vr, "v cache", rel=2e-2)
 
 
-@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("5", "1"), ("5", "2"), ("8", "1"), ("8", "2"), ("8", "4")])
+@pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("5", "1"), ("5", "2"), ("8", "1"), ("8", "2"), ("8", "4"),
+                                       ("8", "8")])
 def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_split=split))
@@ -115,8 +116,8 @@ def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
 @pytest.mark.parametrize("M", [256, 1000, 8192])
 def test_pipe_schedule_all_epilogues(gpu, monkeypatch, M):
     """cfg 8, the 256 x 256 tile of gemm_pipe.hip (two wave rows one barrier apart, four half-tile phases per K step,
-    every LDS-DMA half-tile five phases ahead of its counted wait, LDS-staged bf16 stores): bf16 store, residual add
-    and SiLU·mul at Mistral-7B shapes, ragged M included."""
+    one half-tile issued per phase, each five or six phases ahead of its read, LDS-staged bf16 stores): bf16 store,
+    residual add and SiLU·mul at Mistral-7B shapes, ragged M included."""
     cfg = "8"
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
     ops.refresh_env()
@@ -138,3 +139,21 @@ def test_pipe_schedule_all_epilogues(gpu, monkeypatch, M):
     gu = _ref(x, wgu).view(M, 2 * F // 16, 16)
     ref = (torch.nn.functional.silu(gu[..., :8]) * gu[..., 8:]).reshape(M, F)
     _check(hs, ref, f"pipe gate_up silu M={M}", rel=2e-2)
+
+
+@pytest.mark.parametrize("M", [300, 2048, 8192])
+def test_pipe_repeat_bit_identical(gpu, monkeypatch, M):
+    """Race screen for the pipe schedule: the kernel is deterministic, so 20 back-to-back calls on the same operands
+    must reproduce the first output bit for bit (an LDS half-tile read before its DMA landed, or re-staged before
+    every wave read it, shows up as a differing tile)."""
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg="8"))
+    ops.refresh_env()
+    g = torch.Generator().manual_seed(M + 7)
+    x = _rand((M, H), g, gpu)
+    w = R.tile_weight(_rand((2 * F, H), g, gpu, 1 / 64))
+    out = torch.empty(M, 2 * F, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_out(x, w, out)
+    first = out.clone()
+    for i in range(20):
+        ops.gemm_out(x, w, out)
+        assert torch.equal(out, first), f"call {i + 1} differs from the first"
