@@ -58,6 +58,11 @@ DEV int a_swz(int row) { return (row >> 1) & 5; }
 // NS: LDS stages (3: one stage's DMA stays in flight across the publishing barrier; 2: the next stage is issued
 // after the barrier and waited for at the next one).  FB: 2 = both k sub-steps' fragments are read before the
 // first MFMA (the second read's latency hides under the first MFMA cluster), 1 = one sub-step at a time.
+#ifndef DSSE_TILED_BURST
+#define DSSE_TILED_BURST 0
+#endif
+constexpr bool kBurst = DSSE_TILED_BURST;  // A/B build only: every tile issues its stage in one burst
+
 template <int WM, int WN, int MT, int NT, int NS, int FB, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN)
 gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
@@ -101,15 +106,23 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
     b_src[i] = W + ((size_t)(n0 / 16 + (j >> 1)) * KC) * kTileChunk + (j & 1) * 512 + lane * 8;
   }
 
-  auto issue = [&](int stage, int t) {
+  auto issue_a = [&](int stage, int t) {
     const int kk = k0 + 64 * t, c = kk >> 7, h = (kk >> 6) & 1;
     char* base = smem + stage * G::STAGE;
 #pragma unroll
     for (int i = 0; i < G::A_INS; ++i)
       glds16(a_src[i] + c * 128 + 16 * h + a_koff[i], base + (w * G::A_INS + i) * 1024);
+  };
+  auto issue_b = [&](int stage, int t) {
+    const int kk = k0 + 64 * t, c = kk >> 7, h = (kk >> 6) & 1;
+    char* base = smem + stage * G::STAGE;
 #pragma unroll
     for (int i = 0; i < G::B_INS; ++i)
       glds16(b_src[i] + (size_t)c * kTileChunk + h * 1024, base + G::A_BYTES + (w * G::B_INS + i) * 1024);
+  };
+  auto issue = [&](int stage, int t) {
+    issue_a(stage, t);
+    issue_b(stage, t);
   };
 
   f32x4 acc[MT][NT];
@@ -138,8 +151,18 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
     if (NS == 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * INS) : "memory");
     else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    // the stage step t+NS-1 overwrites was last read in step t-1, which every wave finished before this barrier
-    if (t + NS - 1 < nk) issue((t + NS - 1) % NS, t + NS - 1);
+    // the stage step t+NS-1 overwrites was last read in step t-1, which every wave finished before this barrier.
+    // 128x256 tile (the weight-heavy 129-256-row decode buckets): its X half goes out now, its weight half between
+    // the two MFMA clusters, so the DMA issue is spread over the step (the order gemm_pipe.hip measured faster):
+    // gate_up at 256 rows 74.9 vs 80.0 us, down 52.7 vs 54.9.  The 128x128 tile measured slower spread (qkv 256
+    // rows 36.5 vs 33.6, o 26.6 vs 25.2) and 256x128 even, so those issue the stage in one burst
+    // (profiles/r5/gemm_pipe_r5.md, tiled_ab_r5.log)
+    constexpr bool spread = FB == 2 && WM == 2 && WN == 4 && !kBurst;
+    const bool more = t + NS - 1 < nk;
+    if (more) {
+      if constexpr (spread) issue_a((t + NS - 1) % NS, t + NS - 1);
+      else issue((t + NS - 1) % NS, t + NS - 1);
+    }
     const char* As = smem + (t % NS) * G::STAGE;
     const char* Bs = As + G::A_BYTES;
     auto read = [&](int sp, bf16x8 (&a)[MT], bf16x8 (&b)[NT]) {
@@ -162,6 +185,7 @@ gemm_tiled_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __rest
       read(0, a0, b0);
       read(1, a1, b1);
       mma(a0, b0);
+      if (spread && more) issue_b((t + NS - 1) % NS, t + NS - 1);
       mma(a1, b1);
     } else {
 #pragma unroll

@@ -70,6 +70,7 @@ def _parallel(jobs, verbose):
 
 KERNEL_VARIANTS = {
     "checked": ["-DDSSE_KERNEL_CHECKS=1"],  # device index-check debug build (tools/check_kernels.py)
+    "burst": ["-DDSSE_TILED_BURST=1"],  # A/B build: gemm_tiled issues each stage's DMA in one burst
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
 

@@ -82,6 +82,15 @@ for s in "$@"; do
       step pmc_gemm_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_gemm_a" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
       step pmc_gemm_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_gemm_b" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
       python3 tools/pmc_sum.py "$out/pmc_gemm_a" "$out/pmc_gemm_b" --kernel gemm --title "gate_up GEMM (N 28672, K 4096) at M = 8192 and 256" > "$out/pmc_gemm.md" 2>&1 ;;
+    tiled_ab)  # gemm_tiled stage-issue order: spread (default build) vs one burst (kernels-burst build)
+      for v in "" burst; do
+        DSSE_KERNELS_VARIANT=$v step "tiled_ab_qkv_$v" 300 python -u tools/bench_decode_gemm.py --shape qkv --M 160,256,384,512 --variants out &&
+        DSSE_KERNELS_VARIANT=$v step "tiled_ab_o_$v" 300 python -u tools/bench_decode_gemm.py --shape o,down --M 160,256,384,512 --variants split_norm &&
+        DSSE_KERNELS_VARIANT=$v step "tiled_ab_gu_$v" 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 160,256,384,512 --variants silu
+      done ;;
+    mall)  # decode GEMMs with weights cycling through HBM (1.2 GB of copies) vs two copies resident in the MALL
+      step mall_cold 300 python -u tools/bench_decode_gemm.py --shape qkv,o,down --M 64,128,256 --variants out,split_norm &&
+      step mall_hot 300 python -u tools/bench_decode_gemm.py --shape qkv,o,down --M 64,128,256 --variants out,split_norm --bytes 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
