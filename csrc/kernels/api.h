@@ -98,8 +98,8 @@ hipError_t dsse_gemm_wide(int mode, int mb, int rd, int S, int partial_only, con
                           int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W,
                            int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
-hipError_t dsse_gemm_pipe(int mode, int S, int partial_only, const void* X, int ldx, int M, const void* W, int K,
-                          int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
+hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M, const void* W,
+                          int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);

@@ -222,17 +222,18 @@ WCfg pick_wide(int M, int N, int K) {
   return c;
 }
 
-// cfg 8 = the pipelined 256 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's configurations
+// cfg 8 / 9 = the pipelined 256 x 256 / 192 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's configurations
 hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W, int K,
                       int N, const dsse::GemmEpi* ep, float* part) {
-  if (cfg == 8) return dsse_gemm_pipe(mode, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
+  if (cfg == 8 || cfg == 9)
+    return dsse_gemm_pipe(mode, cfg == 9 ? 192 : 256, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
   return dsse_gemm_tiled(mode, cfg, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
 }
 
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
 // Tiled LDS-DMA GEMMs (gemm_tiled.hip, gemm_pipe.hip; prefill and wide batches).  DSSE_KERNEL_CFG overrides: t_cfg
-// (0 = 256x128, 1 = 128x128, 5 = 128x256, 8 = 256x256 gemm_pipe), t_split.
+// (0 = 256x128, 1 = 128x128, 5 = 128x256, 8 = 256x256 gemm_pipe, 9 = 192x256 gemm_pipe), t_split.
 struct TCfg {
   int cfg, S;
   bool ok;
@@ -240,7 +241,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("t_cfg", -1);
-  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8) {
+  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8 && cfg != 9) {
     // round 5 (profiles/r5/gemm_pipe_r5.md): the 256x256 tile of gemm_pipe.hip (cfg 8: 8 waves, every LDS-DMA
     // half-tile five phases ahead of its wait) once it yields >= ~160 workgroups -- 1.35-1.40 PFLOP/s at 8192 rows,
     // +5-7 % over round 4's phased cfg 4; below that the 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
@@ -264,13 +265,18 @@ TCfg pick_tiled(int M, int N, int K) {
     // 128x128 (50 / 153 vs 65 / 205 us; profiles/r3/prefill_chunk_gemm.md)
     if (N <= 8192 && M > 256 && M <= 512) cfg = (K > 8192 || N > 4096) ? 8 : 0;
     if (N <= 4096 && M > 512 && M <= 1024) cfg = 1;
+    // round 5 (profiles/r5/pipe192_r5.log): 257-384 rows -- the mixed prefill + decode steps' 320 / 384 rows -- leave
+    // the second 256-row block a quarter to three quarters empty; the 192-row pipe tile (cfg 9) fills it: gate_up
+    // 88.2 vs 99.1 us at 384 rows (87.6 vs 96.6 at 320), down + norm 58.0 vs 62.9 (54.4 vs 61.2), qkv 37.1 vs 41.5
+    // (34.2 vs 38.2); o (cfg 0) even, so it stays
+    if (cfg == 8 && M > 256 && M <= 384) cfg = 9;
   }
   constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
-  // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8)
-  const int BM = cfg == 1 || cfg == 5 ? 128 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
+  // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8, 9)
+  const int BM = cfg == 1 || cfg == 5 ? 128 : cfg == 9 ? 192 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
   c.cfg = cfg;
   c.S = 1;
-  const bool pipe = cfg == 8;
+  const bool pipe = cfg == 8 || cfg == 9;
   c.ok = N % BN == 0 && K % (pipe ? 128 : 64) == 0;
   if (!c.ok) return c;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);

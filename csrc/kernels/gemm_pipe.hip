@@ -1,4 +1,4 @@
-// Prefill / wide GEMM, 256 x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
+// Prefill / wide GEMM, 256 (or 192) x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
 // weight layout (api.h kTileChunk), M >= 256 (smaller M: split K, grid.z-style slices in the tile index).
 //
 // Why a new schedule (profiles/r4/pmc_gemm_r4.md): gemm_phased (gemm_tiled.hip cfg 4) issued the last A half of step
@@ -57,7 +57,12 @@ DEV int a_swz(int row) { return (row >> 1) & 5; }
 
 }  // namespace gp
 
-template <int MODE>
+// BM: rows per workgroup tile, 256 or 192.  192 keeps the 256-row LDS image and schedule, and fills 48 of every
+// 64-row quadrant (the other 16 slot rows load as zeros, no traffic, and no MFMA reads them): 12 MFMAs per phase
+// instead of 16, for row counts that leave a 256-row block one-half to one-quarter empty (the mixed prefill + decode
+// steps' 320-384 rows, the 129-192-row decode bucket).  Slot row s of quadrant q, wave row wr holds X row
+// m0 + wr * BM / 2 + q * BM / 4 + s.
+template <int MODE, int BM>
 __global__ void __launch_bounds__(512)
 gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
                  GemmEpi ep, float* __restrict__ part) {
@@ -68,7 +73,9 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   const int wm = w >> 2, wn = w & 3;
 
   // ---- tile order: bijective XCD remap, then groups of 8 row blocks swept column by column (L2 panel reuse)
-  const int nbm = (M + 255) / 256, nbn = N / 256, ntile = nbm * nbn;
+  constexpr int QR = BM / 4, QI = QR / 16;  // X rows per quadrant, MFMA row tiles per quadrant
+  static_assert(BM == 256 || BM == 192, "row tile");
+  const int nbm = (M + BM - 1) / BM, nbn = N / 256, ntile = nbm * nbn;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
   const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
@@ -76,7 +83,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   constexpr int GM = 8;
   const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
   const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
-  const int m0 = bm * 256, n0 = bn * 256;
+  const int m0 = bm * BM, n0 = bn * 256;
   const int k0 = ks * Kr, nk = Kr >> 6;
   const int KC = K >> 7;
 
@@ -92,10 +99,11 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
     for (int i = 0; i < 2; ++i) {
       const int j = 2 * w + i;                                     // instruction j of the 16 of this half
       const int rb = (j >> 3) * 128 + q * 64 + (j & 7) * 8;        // first of its 8 rows
-      const int row = rb + (lane >> 3);
+      const int row = rb + (lane >> 3), sr = (j & 7) * 8 + (lane >> 3);  // LDS slot row, slot row in the quadrant
+      const int xrow = m0 + (j >> 3) * (BM / 2) + q * QR + sr;          // the X row it holds
       const int pc = (lane & 7) ^ a_swz(row);
       a_lo[q][i] = rb * 128;
-      a_vo[q][i] = m0 + row < M ? (uint32_t)(((size_t)(m0 + row) * ldx + 32 * (pc >> 1) + 8 * (pc & 1)) * 2) : kOOB;
+      a_vo[q][i] = sr < QR && xrow < M ? (uint32_t)(((size_t)xrow * ldx + 32 * (pc >> 1) + 8 * (pc & 1)) * 2) : kOOB;
       const int tb = (j >> 2) * 4 + q * 2 + ((j >> 1) & 1), sub = j & 1;  // column tile of the block, k sub-step
       b_lo[q][i] = kA + tb * 2048 + sub * 1024;
       b_vo[q][i] = (uint32_t)((((size_t)(n0 / 16 + tb) * KC) * kTileChunk + sub * 512 + lane * 8) * 2);
@@ -138,7 +146,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   bf16x8 a[4][2], b[4][2];
   auto read_a = [&](const char* buf, int qm) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < QI; ++i)
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp)
         a[i][sp] = *reinterpret_cast<const bf16x8*>(buf + a_rd[sp] + (64 * qm + 16 * i) * 128);
@@ -157,7 +165,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 #pragma unroll
     for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < QI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[4 * qm + i][2 * qn + j] = mfma16x16x32(a[i][sp], b[2 * qn + j][sp], acc[4 * qm + i][2 * qn + j]);
@@ -218,7 +226,9 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   // balance the barrier count of the two rows
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
 
-  const int row0 = m0 + wm * 128, tile0 = n0 / 16 + wn * 4;
+  // acc[4 qm + i] holds X rows row0 + QR qm + 16 i (i < QI)
+  const int row0 = m0 + wm * (BM / 2), tile0 = n0 / 16 + wn * 4;
+  auto mrow = [&](int mt) { return row0 + QR * (mt >> 2) + 16 * (mt & 3); };
   if constexpr (MODE == kStoreBf16) {
     // stage the wave's 128 x 64 bf16 tile in LDS (all DMA retired, everyone past its last fragment read), then
     // 16-byte row stores: 8 lanes per 128-byte row, 8 rows per instruction
@@ -239,8 +249,9 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int rr = 8 * it + (lane >> 3), ch = lane & 7;
+      if ((rr & 63) >= QR) continue;  // BM 192: slot rows 48-63 of a quadrant hold no X row
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + rr * 64 + ((ch ^ (rr & 7)) << 3));
-      const int m = row0 + rr;
+      const int m = row0 + QR * (rr >> 6) + (rr & 63);
       if (m < M) *reinterpret_cast<bf16x8*>(out + (size_t)m * ep.ldo + n0 + wn * 64 + ch * 8) = v;
     }
     return;
@@ -249,35 +260,44 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) silu_epilogue4(ep, M, row0 + 16 * mt + 4 * g, tile0 + nt, r, acc[mt][nt]);
+      for (int nt = 0; nt < 4; ++nt)
+        if ((mt & 3) < QI) silu_epilogue4(ep, M, mrow(mt) + 4 * g, tile0 + nt, r, acc[mt][nt]);
     return;
   }
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
+  for (int mt = 0; mt < 8; ++mt) {
+    if ((mt & 3) >= QI) continue;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float v = acc[mt][nt][i];
         const float partner = (MODE == kQkvRope) ? __shfl_xor(v, 8) : 0.f;
-        epilogue<MODE>(ep, part_ks, M, N, row0 + 16 * mt + 4 * g + i, tile0 + nt, r, v, partner);
+        epilogue<MODE>(ep, part_ks, M, N, mrow(mt) + 4 * g + i, tile0 + nt, r, v, partner);
       }
+  }
 }
 
-template <int MODE>
-static hipError_t launch_pipe(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
-                              float* part, hipStream_t st) {
+template <int MODE, int BM>
+static hipError_t launch_pipe_bm(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
+                                 float* part, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<MODE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<MODE, BM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)gp::kLDS);
     attr_set = true;
   }
-  const int nbm = (M + 255) / 256, nbn = N / 256;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE>), dim3(nbm * nbn * S), dim3(512), gp::kLDS, st, X, ldx, M, W, K, N,
+  const int nbm = (M + BM - 1) / BM, nbn = N / 256;
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, BM>), dim3(nbm * nbn * S), dim3(512), gp::kLDS, st, X, ldx, M, W, K, N,
                      K / S, ep, part);
   return hipGetLastError();
+}
+template <int MODE>
+static hipError_t launch_pipe(int bm, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
+                              const GemmEpi& ep, float* part, hipStream_t st) {
+  return bm == 192 ? launch_pipe_bm<MODE, 192>(X, ldx, M, W, K, N, S, ep, part, st)
+                   : launch_pipe_bm<MODE, 256>(X, ldx, M, W, K, N, S, ep, part, st);
 }
 
 }  // namespace dsse
@@ -285,23 +305,24 @@ static hipError_t launch_pipe(const bf16* X, int ldx, int M, const bf16* W, int 
 // Shape contract (checked here): N % 256 == 0, K % (128 S) == 0 (>= 2 K steps of 64 per slice), the tiled weight
 // layout (api.h), X rows of ldx >= K elements.  S > 1: fp32 slabs [S, M, N] into `part`, reduced by
 // launch_splitk_reduce unless partial_only.
-extern "C" hipError_t dsse_gemm_pipe(int mode, int S, int partial_only, const void* X, int ldx, int M, const void* W,
-                                     int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st) {
+extern "C" hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M,
+                                     const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st) {
   using namespace dsse;
-  if (M < 1 || N % 256 != 0 || S < 1 || K % (128 * S) != 0 || ldx < K) return hipErrorInvalidValue;
+  if (M < 1 || N % 256 != 0 || S < 1 || K % (128 * S) != 0 || ldx < K || (bm != 256 && bm != 192))
+    return hipErrorInvalidValue;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
   if (S == 1 && !partial_only) {
     switch (mode) {
-      case kStoreBf16: return launch_pipe<kStoreBf16>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kStoreF32: return launch_pipe<kStoreF32>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kResidAdd: return launch_pipe<kResidAdd>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kSiluMul: return launch_pipe<kSiluMul>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
-      case kQkvRope: return launch_pipe<kQkvRope>(x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreBf16: return launch_pipe<kStoreBf16>(bm, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kStoreF32: return launch_pipe<kStoreF32>(bm, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kResidAdd: return launch_pipe<kResidAdd>(bm, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kSiluMul: return launch_pipe<kSiluMul>(bm, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
+      case kQkvRope: return launch_pipe<kQkvRope>(bm, x, ldx, M, w, K, N, 1, *ep, nullptr, st);
     }
     return hipErrorInvalidValue;
   }
-  hipError_t e = launch_pipe<kPartial>(x, ldx, M, w, K, N, S, *ep, part, st);
+  hipError_t e = launch_pipe<kPartial>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
 }

@@ -91,6 +91,10 @@ for s in "$@"; do
     mall)  # decode GEMMs with weights cycling through HBM (1.2 GB of copies) vs two copies resident in the MALL
       step mall_cold 300 python -u tools/bench_decode_gemm.py --shape qkv,o,down --M 64,128,256 --variants out,split_norm &&
       step mall_hot 300 python -u tools/bench_decode_gemm.py --shape qkv,o,down --M 64,128,256 --variants out,split_norm --bytes 1 ;;
+    pipe192)  # gemm_pipe on the 192-row tile (cfg 9) vs the default pick at 129-384 rows
+      step pipe192_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv --M 160,192,320,384 --variants out,out:t_cfg=9,out:t_cfg=8 &&
+      step pipe192_gu 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 160,192,320,384 --variants silu,silu:t_cfg=9,silu:t_cfg=8 &&
+      step pipe192_od 300 python -u tools/bench_decode_gemm.py --shape o,down --M 160,192,320,384 --variants split_norm,split_norm:t_cfg=9,split_norm:t_cfg=8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
