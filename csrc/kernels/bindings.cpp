@@ -45,7 +45,7 @@ void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
 
 // Kernel-configuration overrides: ONE environment variable, DSSE_KERNEL_CFG = "key=value,key=value" (diagnostics and
 // the tests that force a kernel path; e.g. "gemm_impl=4,t_cfg=8,t_split=2").  Keys name the selector inputs below
-// (gemm_impl, t_cfg, t_split, s_nw, s_nt, s_rd, s_split, s_ring, ring2, resid_nw, resid_split, qkv_split, w_split, w_rd,
+// (gemm_impl, t_cfg, t_split, t_small, s_nw, s_nt, s_rd, s_split, s_ring, ring2, resid_nw, resid_split, qkv_split, w_split, w_rd,
 // gemm_nt, gemm_kw, attn_kwv, attn_pd, fused_qkv_attn, trap_fpe); docs/operations.md lists them.  Parsed once per
 // thread into a thread-local map: no getenv and no lock on the launch path.  refresh_env() (op dsse::refresh_env, for
 // the tools that change it in-process) bumps a generation that makes every thread re-parse on its next lookup.
@@ -225,8 +225,8 @@ WCfg pick_wide(int M, int N, int K) {
 // cfg 8 / 9 = the pipelined 256 x 256 / 192 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's configurations
 hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W, int K,
                       int N, const dsse::GemmEpi* ep, float* part) {
-  if (cfg == 8 || cfg == 9)
-    return dsse_gemm_pipe(mode, cfg == 9 ? 192 : 256, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
+  if (cfg == 8 || cfg == 9 || cfg == 10)
+    return dsse_gemm_pipe(mode, cfg == 10 ? 128 : cfg == 9 ? 192 : 256, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
   return dsse_gemm_tiled(mode, cfg, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
 }
 
@@ -241,7 +241,7 @@ struct TCfg {
 TCfg pick_tiled(int M, int N, int K) {
   TCfg c{};
   int cfg = env_int("t_cfg", -1);
-  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8 && cfg != 9) {
+  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8 && cfg != 9 && cfg != 10) {
     // round 5 (profiles/r5/gemm_pipe_r5.md): the 256x256 tile of gemm_pipe.hip (cfg 8: 8 waves, every LDS-DMA
     // half-tile five phases ahead of its wait) once it yields >= ~160 workgroups -- 1.35-1.40 PFLOP/s at 8192 rows,
     // +5-7 % over round 4's phased cfg 4; below that the 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
@@ -259,6 +259,14 @@ TCfg pick_tiled(int M, int N, int K) {
     // for the weight-heavy 129-256-row shapes: gate_up 68.1 vs 73.9 us (256 rows) / 64.4 vs 66.2 (192), down
     // (K 14336) 42.9 vs 50.5 / 41.0 vs 42.0
     if (M > 128 && M <= 256 && (N > 8192 || K > 8192)) cfg = 5;
+    // round 5 (profiles/r5/pipe128_r5.log): the pipe schedule on 128 / 192-row tiles (cfg 10 / 9) for the decode
+    // buckets' qkv (N 6144) and down (K 14336): qkv 30.6 vs 33.1 us at 256 rows, 28.7 vs 30.4 at 192; down + norm
+    // 48.4 vs 52.1 at 256 (cfg 10), 43.8 vs 48.1 at 192 (cfg 9).  gate_up and o measured slower on them and keep
+    // cfg 5 / cfg 1
+    if (M > 160 && M <= 256 && N % 256 == 0 && N <= 8192 && env_int("t_small", 1)) {
+      if (K > 8192) cfg = M <= 192 ? 9 : 10;
+      else if (N > 4096) cfg = 10;
+    }
     // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: 257-512 rows down
     // (K 14336) on the 256x256 tile split 8 ways (cfg 8: 69 vs 72 us on round 4's phased tile, vs 92 us on
     // 256x128), o on 256x128 (33 vs 38 us), qkv on cfg 8 (43 vs 46 us); 513-1024 rows N <= 4096 (o, down) on
@@ -273,10 +281,10 @@ TCfg pick_tiled(int M, int N, int K) {
   }
   constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
   // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8, 9)
-  const int BM = cfg == 1 || cfg == 5 ? 128 : cfg == 9 ? 192 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
+  const int BM = cfg == 1 || cfg == 5 || cfg == 10 ? 128 : cfg == 9 ? 192 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
   c.cfg = cfg;
   c.S = 1;
-  const bool pipe = cfg == 8 || cfg == 9;
+  const bool pipe = cfg >= 8;
   c.ok = N % BN == 0 && K % (pipe ? 128 : 64) == 0;
   if (!c.ok) return c;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);

@@ -74,7 +74,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 
   // ---- tile order: bijective XCD remap, then groups of 8 row blocks swept column by column (L2 panel reuse)
   constexpr int QR = BM / 4, QI = QR / 16;  // X rows per quadrant, MFMA row tiles per quadrant
-  static_assert(BM == 256 || BM == 192, "row tile");
+  static_assert(BM == 256 || BM == 192 || BM == 128, "row tile");
   const int nbm = (M + BM - 1) / BM, nbn = N / 256, ntile = nbm * nbn;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
@@ -296,6 +296,7 @@ static hipError_t launch_pipe_bm(const bf16* X, int ldx, int M, const bf16* W, i
 template <int MODE>
 static hipError_t launch_pipe(int bm, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                               const GemmEpi& ep, float* part, hipStream_t st) {
+  if (bm == 128) return launch_pipe_bm<MODE, 128>(X, ldx, M, W, K, N, S, ep, part, st);
   return bm == 192 ? launch_pipe_bm<MODE, 192>(X, ldx, M, W, K, N, S, ep, part, st)
                    : launch_pipe_bm<MODE, 256>(X, ldx, M, W, K, N, S, ep, part, st);
 }
@@ -308,7 +309,7 @@ static hipError_t launch_pipe(int bm, const bf16* X, int ldx, int M, const bf16*
 extern "C" hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M,
                                      const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st) {
   using namespace dsse;
-  if (M < 1 || N % 256 != 0 || S < 1 || K % (128 * S) != 0 || ldx < K || (bm != 256 && bm != 192))
+  if (M < 1 || N % 256 != 0 || S < 1 || K % (128 * S) != 0 || ldx < K || (bm != 256 && bm != 192 && bm != 128))
     return hipErrorInvalidValue;
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);

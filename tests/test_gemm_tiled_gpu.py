@@ -72,8 +72,8 @@ def test_tiled_silu_gate_up(gpu, M):
     _check(out, ref, f"gate_up silu M={M}", rel=2e-2)
 
 
-@pytest.mark.parametrize("cfg", ["auto", "8", "9"])
-@pytest.mark.parametrize("M", [300, 2048])
+@pytest.mark.parametrize("cfg", ["auto", "8", "9", "10"])
+@pytest.mark.parametrize("M", [256, 300, 2048])
 def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
     if cfg != "auto":
         monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
@@ -99,7 +99,8 @@ def test_tiled_qkv_rope_kv_write(gpu, monkeypatch, M, cfg):
 
 
 @pytest.mark.parametrize("cfg,split", [("0", "2"), ("1", "1"), ("5", "1"), ("5", "2"), ("8", "1"), ("8", "2"), ("8", "4"),
-                                       ("8", "8"), ("9", "1"), ("9", "2"), ("9", "4")])
+                                       ("8", "8"), ("9", "1"), ("9", "2"), ("9", "4"), ("10", "1"),
+                                       ("10", "4")])
 def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_split=split))
@@ -107,18 +108,18 @@ def test_tiled_configs_and_split_k(gpu, monkeypatch, cfg, split):
     g = torch.Generator().manual_seed(int(cfg) * 10 + int(split))
     for M in (1, 70, 256, 600):
         x = _rand((M, 2048), g, gpu)
-        w = R.tile_weight(_rand((1536 if cfg in ("8", "9") else 1024, 2048), g, gpu, 1 / 45))
+        w = R.tile_weight(_rand((1536 if cfg in ("8", "9", "10") else 1024, 2048), g, gpu, 1 / 45))
         out = torch.empty(M, w.shape[0], device=gpu)
         ops.gemm_out(x, w, out)
         _check(out, _ref(x, w), f"cfg {cfg} split {split} M={M}", rel=2e-3)
 
 
 @pytest.mark.parametrize("cfg,M", [("8", 256), ("8", 1000), ("8", 8192), ("9", 150), ("9", 192), ("9", 320),
-                                   ("9", 384), ("9", 1000)])
+                                   ("9", 384), ("9", 1000), ("10", 200), ("10", 256), ("10", 1000)])
 def test_pipe_schedule_all_epilogues(gpu, monkeypatch, cfg, M):
     """cfg 8, the 256 x 256 tile of gemm_pipe.hip (two wave rows one barrier apart, four half-tile phases per K step,
     one half-tile issued per phase, each five or six phases ahead of its read, LDS-staged bf16 stores), and cfg 9, the
-    same schedule on a 192-row tile (48 of every 64 slot rows filled): bf16 store, residual add and SiLU·mul at
+    same schedule on 192 / 128-row tiles (cfg 9 / 10: 48 / 32 of every 64 slot rows filled): bf16 store, residual add and SiLU·mul at
     Mistral-7B shapes, ragged M included."""
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg))
     ops.refresh_env()
@@ -142,7 +143,7 @@ def test_pipe_schedule_all_epilogues(gpu, monkeypatch, cfg, M):
     _check(hs, ref, f"pipe gate_up silu M={M}", rel=2e-2)
 
 
-@pytest.mark.parametrize("cfg,M", [("8", 300), ("8", 2048), ("8", 8192), ("9", 384)])
+@pytest.mark.parametrize("cfg,M", [("8", 300), ("8", 2048), ("8", 8192), ("9", 384), ("10", 256)])
 def test_pipe_repeat_bit_identical(gpu, monkeypatch, cfg, M):
     """Race screen for the pipe schedule: the kernel is deterministic, so 20 back-to-back calls on the same operands
     must reproduce the first output bit for bit (an LDS half-tile read before its DMA landed, or re-staged before

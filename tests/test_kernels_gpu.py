@@ -41,6 +41,7 @@ GEMM_CONFIGS = {
     "tiled-128x256": {"gemm_impl": "4", "t_cfg": "5"},
     "pipe-256sq": {"gemm_impl": "4", "t_cfg": "8"},
     "pipe-192": {"gemm_impl": "4", "t_cfg": "9"},
+    "pipe-128": {"gemm_impl": "4", "t_cfg": "10"},
     "skinny-default": {"gemm_impl": "0"},
     "skinny-nt2kw4": {"gemm_impl": "0", "gemm_nt": "2", "gemm_kw": "4"},
     "skinny-nt1kw8": {"gemm_impl": "0", "gemm_nt": "1", "gemm_kw": "8"},
@@ -246,7 +247,7 @@ def test_gemm_qkv_rope_and_kv_write(gpu, tiles, M):
 
 
 @pytest.mark.parametrize("cfg", ["auto", "tiled-default", "tiled-128-split2", "tiled-128x256", "pipe-256sq",
-                                 "pipe-192"])
+                                 "pipe-192", "pipe-128"])
 @pytest.mark.parametrize("M", [129, 192, 200, 256])
 def test_decode_bucket_epilogues(gpu, monkeypatch, cfg, M):
     """Every epilogue of the 129-256-row decode buckets (bf16 / fp32 store, residual add, SiLU*mul, QKV + RoPE +

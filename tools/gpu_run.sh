@@ -95,6 +95,16 @@ for s in "$@"; do
       step pipe192_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv --M 160,192,320,384 --variants out,out:t_cfg=9,out:t_cfg=8 &&
       step pipe192_gu 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 160,192,320,384 --variants silu,silu:t_cfg=9,silu:t_cfg=8 &&
       step pipe192_od 300 python -u tools/bench_decode_gemm.py --shape o,down --M 160,192,320,384 --variants split_norm,split_norm:t_cfg=9,split_norm:t_cfg=8 ;;
+    pipe128)  # gemm_pipe on a 128-row tile (cfg 10) vs the default pick and cfg 9 at 129-256 rows
+      step pipe128_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv --M 128,192,256 --variants out,out:t_cfg=10,out:t_cfg=9 &&
+      step pipe128_gu 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 128,192,256 --variants silu,silu:t_cfg=10,silu:t_cfg=9 &&
+      step pipe128_od 300 python -u tools/bench_decode_gemm.py --shape o,down --M 128,192,256 --variants split_norm,split_norm:t_cfg=10,split_norm:t_cfg=9 &&
+      DSSE_KERNEL_CFG=t_cfg=10 step pipe128_test 300 $PYT tests/test_gemm_tiled_gpu.py -k "silu or resid or qkv" ;;
+    small_ab)  # 256-stream step: cfg 9 / 10 picks for the decode buckets' qkv / down (default) vs t_small=0, alternating
+      for i in 1 2; do
+        step "small_on_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
+        DSSE_KERNEL_CFG=t_small=0 step "small_off_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
