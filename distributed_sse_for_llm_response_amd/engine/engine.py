@@ -93,6 +93,8 @@ class Sequence:
     produced: int = 0           # tokens drained and published
     first_token_ns: int = 0
     last_token_ns: int = 0
+    queued_ns: int = 0          # add_request (after the serving loop polled and tokenized it)
+    admit_ns: int = 0           # first prompt chunk planned into a step (0: prefilled by the separate-pass path)
     aborted: bool = False
     stop_after_enqueue: bool = False
     paused: bool = False        # flow control: held out of the decode batch (KV and position kept)
@@ -298,6 +300,7 @@ class LLMEngine:
         self._bt_new: list = []  # (sequence, page index, block) appended since the last upload
         self._pending: list = []  # events raised between steps (aborts of queued requests), returned by the next
         self.on_ttft = None
+        self.ttft_trace = None  # a list: (arrival, queued, admitted, first token) ns per sequence
         self.on_itl = None
         # on_flush(events): called with the events gathered so far before the step blocks on a drain that is not
         # ready yet (the serving loop publishes them at once: early-drained first tokens do not wait for the
@@ -347,7 +350,7 @@ class LLMEngine:
             prompt = prompt[-max_prompt:]  # keep the tail (most recent context)
         s = Sequence(rid=next(self._rid) if rid is None else rid, conversation_id=conversation_id,
                      prompt=list(prompt), params=p, arrival_ns=arrival_ns or time.time_ns(), orig_len=len(prompt),
-                     enq_step=self.step_no)
+                     enq_step=self.step_no, queued_ns=time.time_ns())
         self.waiting.append(s)
         self.by_conv[conversation_id] = s
         return s
@@ -631,6 +634,8 @@ class LLMEngine:
             if budget <= 0:
                 continue
             n = min(len(s.prompt) - s.prefilled, budget)
+            if s.prefilled == 0:
+                s.admit_ns = time.time_ns()
             last = s.prefilled + n == len(s.prompt)
             chunks.append(PrefillSeq(slot=s.slot, tokens=s.prompt[s.prefilled:s.prefilled + n], start_pos=s.prefilled,
                                      block_table=s.blocks, last_chunk=last))
@@ -788,6 +793,8 @@ class LLMEngine:
                 s.first_token_ns = now
                 if self.on_ttft:
                     self.on_ttft((now - s.arrival_ns) / 1e9)
+                if self.ttft_trace is not None:  # TTFT split (tools/bench_serving.py): arrival, queued, admitted, token
+                    self.ttft_trace.append((s.arrival_ns, s.queued_ns, s.admit_ns, now))
             elif self.on_itl and s.last_token_ns:
                 self.on_itl((now - s.last_token_ns) / 1e9)
             s.last_token_ns = now

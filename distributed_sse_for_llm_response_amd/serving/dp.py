@@ -97,6 +97,14 @@ def spawn_dp(cfg: ServeConfig, world: int) -> int:
         procs.append(subprocess.Popen([sys.executable, "-m", "distributed_sse_for_llm_response_amd", "serve",
                                        "--dp-worker-only"], env=e))
     os.environ.update({"MASTER_PORT": env["MASTER_PORT"], "RANK": "0", "LOCAL_RANK": "0"})
+    # SIGTERM (an orchestrator's stop, a test's terminate()) ends this process through the finally below, so the
+    # worker processes are stopped with it instead of outliving it; they also watch for this process's death
+    import signal
+
+    def _term(signum, frame):
+        raise KeyboardInterrupt
+
+    signal.signal(signal.SIGTERM, _term)
     try:
         if cfg.engine == "gpu":
             torch.cuda.set_device(0)
@@ -119,8 +127,14 @@ def worker_only_main(cfg: ServeConfig) -> int:
     if cfg.engine == "gpu":
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
+    parent = os.getppid()
     loop = run_worker(cfg, rank, device)
     while loop.is_alive():
         loop.join(0.5)
+        if os.getppid() != parent:  # the launching process died without stopping us: do not outlive it
+            print(f"[serve] dp worker {rank}: launcher {parent} is gone, exiting", flush=True)
+            loop.stop_flag.set()
+            loop.join(5)
+            break
     time.sleep(0.1)
     return 0

@@ -64,6 +64,23 @@ def analyse(arrivals, n_req, long_every, skip_s, max_tokens):
             "mean_concurrent_streams": round(conc, 1), "tokens_per_s": round(toks / win, 1), "window_s": round(win, 2)}
 
 
+def ttft_split(trace):
+    """p50 / p90 (ms) of the server-side parts of TTFT: arrival (HTTP request in the runtime) -> queued in the engine
+    (polled + tokenized), queued -> first prompt chunk planned, planned -> first token drained, and the whole."""
+    if not trace:
+        return {}
+    parts = {"poll_tokenize": [(q - a) / 1e6 for a, q, _, _ in trace],
+             "queue": [(d - q) / 1e6 for _, q, d, _ in trace if d],
+             "prefill_steps": [(t - d) / 1e6 for _, _, d, t in trace if d],
+             "server_ttft": [(t - a) / 1e6 for a, _, _, t in trace]}
+    out = {}
+    for k, v in parts.items():
+        if v:
+            v = sorted(v)
+            out[k] = {"p50": round(v[len(v) // 2], 2), "p90": round(v[int(len(v) * 0.9)], 2)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="mistral-7b-v0.3")
@@ -123,6 +140,7 @@ def main():
                            "duration_s": 1200}
                     if a.long_every and not warm:
                         req.update(long_every=a.long_every, long_words=a.long_words)
+                    app.engine.ttft_trace = []
                     client.stdin.write(json.dumps(req) + "\n")
                     client.stdin.flush()
                     res = json.loads(client.stdout.readline())
@@ -133,6 +151,7 @@ def main():
                            "max_tokens": a.max_tokens, "prompt_tokens": a.prompt_words + 6,
                            "long_prompt_every": a.long_every, "long_prompt_tokens": a.long_words + 6 if a.long_every else 0,
                            **analyse(res["arrivals"], n, a.long_every, a.skip_s, a.max_tokens),
+                           "server_ttft_split_ms": ttft_split(app.engine.ttft_trace),
                            "client_errors": res.get("errors", [])[:3], "engine_stats_cumulative": {
                                k: app.engine.stats.get(k) for k in ("prefill_tokens", "decode_steps", "steps", "mixed_steps",
                                                                     "mixed_graph_rows", "preemptions", "compactions")},

@@ -105,6 +105,11 @@ for s in "$@"; do
         step "small_on_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
         DSSE_KERNEL_CFG=t_small=0 step "small_off_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256
       done ;;
+    pd_ab)  # 256-stream step: one-wave decode attention with a 2-page register ring (attn_pd=2) vs one page, alternating
+      for i in 1 2; do
+        step "pd1_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
+        DSSE_KERNEL_CFG=attn_pd=2 step "pd2_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
