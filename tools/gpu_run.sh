@@ -110,6 +110,15 @@ for s in "$@"; do
         step "pd1_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
         DSSE_KERNEL_CFG=attn_pd=2 step "pd2_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256
       done ;;
+    split_sweep)  # split-K / tile sweep for the narrow projections at the mixed steps' and the 256 bucket's rows
+      step sweep_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv --M 256,384 --variants "out,out:t_cfg=9;t_split=2,out:t_cfg=9;t_split=8,out:t_cfg=10;t_split=2,out:t_cfg=10;t_split=8" &&
+      step sweep_o 300 python -u tools/bench_decode_gemm.py --shape o --M 256,384 --variants "split_norm,split_norm:t_cfg=9;t_split=4,split_norm:t_cfg=9;t_split=8,split_norm:t_cfg=10;t_split=4,split_norm:t_cfg=10;t_split=8,split_norm:t_cfg=0;t_split=2,split_norm:t_cfg=1;t_split=2" &&
+      step sweep_down 300 python -u tools/bench_decode_gemm.py --shape down --M 256,384 --variants "split_norm,split_norm:t_cfg=9;t_split=4,split_norm:t_cfg=10;t_split=4,split_norm:t_cfg=10;t_split=16" ;;
+    jit_ab)  # 13 req/s serving: JIT margin 1.5 ms (default) vs 1.1 ms, alternating
+      for i in 1 2; do
+        step "jit15_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 &&
+        DSSE_JIT_MARGIN_MS=1.1 step "jit11_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
