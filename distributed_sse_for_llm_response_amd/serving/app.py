@@ -138,6 +138,27 @@ class EngineLoop(threading.Thread):
             print(f"[engine] request {req['conversation_id']} rejected by the tokenizer: {e!r}", flush=True)
             return None
 
+    def _take(self, reqs):
+        for req in reqs:
+            prompt = self.tokenize(req)
+            if prompt is not None:
+                self.engine.add_request(req["conversation_id"], prompt, self._params(req), arrival_ns=req["arrival_ns"])
+
+    def _jit_wait(self):
+        """Wait until the just-in-time deadline (LLMEngine.jit_delay), taking in the requests that arrive meanwhile
+        -- tokenized and queued as they come, so the host work left at the deadline is the step's plan and enqueue
+        and a prompt that arrives during the wait still rides in the next step."""
+        if self.jit_margin_s <= 0:
+            return
+        t_end = time.perf_counter() + min(self.engine.jit_delay(self.jit_margin_s), 0.05)
+        while True:
+            left = t_end - time.perf_counter()
+            if left < 1e-3:  # the poll's timeout has millisecond granularity
+                if left > 0:
+                    time.sleep(left)
+                return
+            self._take(self.rt.poll_requests(256, int(left * 1e3)))
+
     def _observe(self):
         e = self.engine
         running, free = float(e.num_running()), float(e.alloc.num_free)
@@ -175,11 +196,7 @@ class EngineLoop(threading.Thread):
                 busy = self.engine.runnable()
                 # only paused streams left: wait briefly so their resume events get through
                 wait = 0 if busy else (2 if self.engine.has_work() else 20)
-                for req in self.rt.poll_requests(256, wait):
-                    prompt = self.tokenize(req)
-                    if prompt is not None:
-                        self.engine.add_request(req["conversation_id"], prompt, self._params(req),
-                                                arrival_ns=req["arrival_ns"])
+                self._take(self.rt.poll_requests(256, wait))
                 for conv in self.rt.pop_cancellations():
                     self.engine.abort(conv)
                 for conv, paused in self.flow_events():
@@ -201,10 +218,8 @@ class EngineLoop(threading.Thread):
                 self._observe()
                 if self.faults.active:
                     self.faults.after_step(self.engine)
-                # just-in-time enqueue: poll new requests as late as the in-flight step allows (TTFT)
-                delay = self.engine.jit_delay(self.jit_margin_s) if self.jit_margin_s > 0 else 0.0
-                if delay > 0:
-                    time.sleep(min(delay, 0.05))
+                # just-in-time enqueue: plan the next step as late as the in-flight step allows (TTFT)
+                self._jit_wait()
         except EngineFault as e:
             # untrusted device state: every live stream ends with [ERROR] now, readiness drops, the process exits
             # non-zero through serve_forever (the orchestrator restarts it; nothing re-execs in this process)

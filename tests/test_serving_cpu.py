@@ -220,3 +220,41 @@ def test_tokenizer_failure_fails_only_that_request():
     assert loop.tokenize_errors == 1
     (convs, ids, seqs, dones, ts, texts, finish, ptoks), = loop.rt.published
     assert convs == ["bad-1"] and dones == [True] and texts == ["[ERROR]"] and finish == [3]
+
+
+def test_jit_wait_takes_requests_in_until_the_deadline():
+    """EngineLoop._jit_wait: the loop waits for the in-flight step's deadline (LLMEngine.jit_delay) on the request
+    queue, so a request arriving meanwhile is tokenized and queued at once (off the enqueue's critical path), and
+    the wait still lasts until the deadline."""
+    import time as _t
+
+    from distributed_sse_for_llm_response_amd.serving.app import EngineLoop
+
+    calls, added = [], []
+
+    class _Rt:
+        def poll_requests(self, n, timeout_ms):
+            calls.append(timeout_ms)
+            if len(calls) == 1:
+                _t.sleep(0.005)
+                return [{"conversation_id": "j", "arrival_ns": 1}]
+            _t.sleep(timeout_ms / 1e3)
+            return []
+
+    class _Engine:
+        def jit_delay(self, margin):
+            return 0.03
+
+        def add_request(self, conv, prompt, params, arrival_ns=None):
+            added.append((conv, _t.perf_counter()))
+
+    loop = EngineLoop.__new__(EngineLoop)
+    loop.rt, loop.engine, loop.jit_margin_s = _Rt(), _Engine(), 0.0015
+    loop.tokenize = lambda req: [1, 2, 3]
+    loop._params = lambda req: None
+    t0 = _t.perf_counter()
+    loop._jit_wait()
+    dt = _t.perf_counter() - t0
+    assert [c for c, _ in added] == ["j"] and added[0][1] - t0 < 0.02  # queued when it arrived
+    assert 0.028 <= dt < 0.06, dt  # and the wait still ran to the deadline
+    assert all(0 < c <= 30 for c in calls), calls
