@@ -47,6 +47,7 @@ import time
 from collections import deque
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from .kv_cache import PAGE, BlockAllocator, blocks_needed
@@ -301,6 +302,7 @@ class LLMEngine:
         self._pending: list = []  # events raised between steps (aborts of queued requests), returned by the next
         self.on_ttft = None
         self.ttft_trace = None  # a list: (arrival, queued, admitted, first token) ns per sequence
+        self.enq_trace = None   # a list: (step kind, host seconds from step start to enqueue)
         self.on_itl = None
         # on_flush(events): called with the events gathered so far before the step blocks on a drain that is not
         # ready yet (the serving loop publishes them at once: early-drained first tokens do not wait for the
@@ -406,29 +408,33 @@ class LLMEngine:
             return
         r = self.r
         Bm = r.max_batch
-        active = torch.zeros(Bm, dtype=torch.int32)
-        temp = torch.zeros(Bm, dtype=torch.float32)
-        topk = torch.zeros(Bm, dtype=torch.int32)
-        topp = torch.ones(Bm, dtype=torch.float32)
-        seeds = torch.zeros(Bm, 2, dtype=torch.int32)
+        # built in numpy (one element write ~0.1 us; on torch CPU tensors ~1 us each: with ~130 live slots the
+        # element loop cost ~1 ms of host time per step that changed a slot, on the JIT enqueue's critical path)
+        active = np.zeros(Bm, dtype=np.int32)
+        temp = np.zeros(Bm, dtype=np.float32)
+        topk = np.zeros(Bm, dtype=np.int32)
+        topp = np.ones(Bm, dtype=np.float32)
+        seeds = np.zeros((Bm, 2), dtype=np.int32)
         for i, s in enumerate(self.slots):
             if s is None:
                 continue
             if s.state == "decode" and not s.aborted and not s.stop_after_enqueue and not s.paused:
                 active[i] = 1
-            temp[i] = s.params.temperature
-            topk[i] = s.params.top_k
-            topp[i] = s.params.top_p
-            sd = s.params.seed if s.params.seed is not None else (s.rid * 2654435761) & 0x7FFFFFFF
+            p = s.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k
+            topp[i] = p.top_p
+            sd = p.seed if p.seed is not None else (s.rid * 2654435761) & 0x7FFFFFFF
             seeds[i, 0] = sd & 0x7FFFFFFF
             seeds[i, 1] = (sd >> 31) & 0x7FFFFFFF
         bt_rows = {}
         for i in self._dirty_slots:
             s = self.slots[i]
             if s is not None and s.blocks:
-                row = torch.zeros(r.max_blocks, dtype=torch.int32)
-                row[: len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
-                bt_rows[i] = row
+                row = np.zeros(r.max_blocks, dtype=np.int32)
+                row[: len(s.blocks)] = s.blocks
+                bt_rows[i] = torch.from_numpy(row)
+        active, temp, topk, topp, seeds = (torch.from_numpy(a) for a in (active, temp, topk, topp, seeds))
         cuda = r.device.type == "cuda"
 
         def put(dst, src):
@@ -680,9 +686,12 @@ class LLMEngine:
         self._admit()
         if not self.waiting:
             self._compact()
+        t_a = time.perf_counter()
         row = self.ring_head % RING_SIZE
         chunks, prefill_done = self._schedule_prefill(self.step_no)
+        t_b = time.perf_counter()
         self._upload()
+        t_c = time.perf_counter()
         producers = []
         ran = False
         dec = [s for s in self.slots if s is not None and s.state == "decode" and not s.aborted
@@ -737,6 +746,9 @@ class LLMEngine:
             s.state = "decode"
             self._dirty_slots.add(s.slot)
         t_enq = time.perf_counter()
+        if self.enq_trace is not None and ran:  # host time from the step's start to its enqueue (bench_serving.py)
+            self.enq_trace.append(("mixed" if chunks and dec and mixed else ("prefill" if chunks else "decode"),
+                                   t_enq - t0, (t_a - t0, t_b - t_a, t_c - t_b, t_enq - t_c)))
         if ran:
             width = max(sl for sl, _ in producers) + 1 if producers else 1
             self.drain.issue(row, width)

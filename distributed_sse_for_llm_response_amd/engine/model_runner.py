@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -191,6 +192,7 @@ class ModelRunner:
         self.pf_graphs = {}   # row bucket -> captured prefill graph
         self.pf = None        # static prefill buffers (allocated by capture)
         self.mx_graphs = {}   # decode bucket B -> [(chunk rows C, captured mixed prefill + decode graph)], C ascending
+        self.host_trace = None  # a list: host seconds of each graph-replayed mixed step (upload, replay, sampling)
 
     # ------------------------------------------------------------------ decode
     def decode_forward(self, B: int) -> None:
@@ -714,9 +716,14 @@ class ModelRunner:
         T = sum(len(s.tokens) for s in seqs)
         entry = next(((c, g) for c, g in self.mx_graphs.get(B, ()) if c >= T), None)
         if entry is not None and len(seqs) <= PREFILL_GRAPH_SEQS:
+            t0 = time.perf_counter()
             q_start, q_len = self.pf.upload(seqs, entry[0], row0=B)
+            t1 = time.perf_counter()
             entry[1].replay()
+            t2 = time.perf_counter()
             self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)
+            if self.host_trace is not None:  # host seconds: metadata upload, graph launch, first-token sampling
+                self.host_trace.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
             return
         w, dev = self.w, self.device
         nh, nkv, F, H = w.nh, w.nkv, w.ffn, self.cfg.hidden_size

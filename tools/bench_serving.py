@@ -81,6 +81,21 @@ def ttft_split(trace):
     return out
 
 
+def enq_split(trace):
+    """p50 / p90 (ms) of the host time from a step's start to its enqueue, by step kind: the work the
+    just-in-time margin has to cover."""
+    out = {}
+    for kind in sorted({e[0] for e in trace or ()}):
+        v = sorted(e[1] * 1e3 for e in trace if e[0] == kind)
+        out[kind] = {"n": len(v), "p50": round(v[len(v) // 2], 3), "p90": round(v[int(len(v) * 0.9)], 3)}
+        phases = [e[2] for e in trace if e[0] == kind and len(e) > 2]
+        if phases:  # engine.step: admit / compact, chunk plan, slot upload, the runner's enqueue
+            for i, name in enumerate(("admit", "plan", "upload", "enqueue")):
+                u = sorted(p[i] * 1e3 for p in phases)
+                out[kind][name + "_p50"] = round(u[len(u) // 2], 3)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="mistral-7b-v0.3")
@@ -141,6 +156,8 @@ def main():
                     if a.long_every and not warm:
                         req.update(long_every=a.long_every, long_words=a.long_words)
                     app.engine.ttft_trace = []
+                    app.engine.enq_trace = []
+                    app.engine.r.host_trace = []
                     client.stdin.write(json.dumps(req) + "\n")
                     client.stdin.flush()
                     res = json.loads(client.stdout.readline())
@@ -152,6 +169,9 @@ def main():
                            "long_prompt_every": a.long_every, "long_prompt_tokens": a.long_words + 6 if a.long_every else 0,
                            **analyse(res["arrivals"], n, a.long_every, a.skip_s, a.max_tokens),
                            "server_ttft_split_ms": ttft_split(app.engine.ttft_trace),
+                           "host_enqueue_ms": enq_split(app.engine.enq_trace),
+                           "mixed_host_ms": enq_split([(k, t) for row in app.engine.r.host_trace or ()
+                                                       for k, t in zip(("upload", "replay", "sample"), row)]),
                            "client_errors": res.get("errors", [])[:3], "engine_stats_cumulative": {
                                k: app.engine.stats.get(k) for k in ("prefill_tokens", "decode_steps", "steps", "mixed_steps",
                                                                     "mixed_graph_rows", "preemptions", "compactions")},
