@@ -410,11 +410,11 @@ class LLMEngine:
         Bm = r.max_batch
         # built in numpy (one element write ~0.1 us; on torch CPU tensors ~1 us each: with ~130 live slots the
         # element loop cost ~1 ms of host time per step that changed a slot, on the JIT enqueue's critical path)
-        active = np.zeros(Bm, dtype=np.int32)
-        temp = np.zeros(Bm, dtype=np.float32)
-        topk = np.zeros(Bm, dtype=np.int32)
-        topp = np.ones(Bm, dtype=np.float32)
-        seeds = np.zeros((Bm, 2), dtype=np.int32)
+        meta = np.zeros(6 * Bm, dtype=np.int32)  # ModelRunner.slot_meta's layout
+        active, topk = meta[:Bm], meta[2 * Bm:3 * Bm]
+        temp, topp = meta[Bm:2 * Bm].view(np.float32), meta[3 * Bm:4 * Bm].view(np.float32)
+        seeds = meta[4 * Bm:].reshape(Bm, 2)
+        topp[:] = 1.0
         for i, s in enumerate(self.slots):
             if s is None:
                 continue
@@ -434,7 +434,6 @@ class LLMEngine:
                 row = np.zeros(r.max_blocks, dtype=np.int32)
                 row[: len(s.blocks)] = s.blocks
                 bt_rows[i] = torch.from_numpy(row)
-        active, temp, topk, topp, seeds = (torch.from_numpy(a) for a in (active, temp, topk, topp, seeds))
         cuda = r.device.type == "cuda"
 
         def put(dst, src):
@@ -443,11 +442,7 @@ class LLMEngine:
             else:
                 dst.copy_(src)
 
-        put(r.active, active)
-        put(r.temperature, temp)
-        put(r.top_k, topk)
-        put(r.top_p, topp)
-        put(r.seeds, seeds)
+        put(r.slot_meta, torch.from_numpy(meta))
         for i, row in bt_rows.items():
             put(r.block_tables[i], row)
         self._dirty_slots.clear()

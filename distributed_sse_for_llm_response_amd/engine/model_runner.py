@@ -141,7 +141,11 @@ class ModelRunner:
         # ---- decode state (slot-indexed, device resident) ----
         self.ids = torch.zeros(Bm, **i32)
         self.positions = torch.zeros(Bm, **i32)
-        self.active = torch.zeros(Bm, **i32)
+        # per-slot sampling state in ONE int32 buffer [active | temperature | top_k | top_p | seeds (Bm x 2)] (the
+        # float fields are views of their words): the engine uploads a changed slot set with one pinned copy
+        # (LLMEngine._upload)
+        self.slot_meta = torch.zeros(6 * Bm, **i32)
+        self.active = self.slot_meta[:Bm]
         self.block_tables = torch.zeros(Bm, self.max_blocks, **i32)
         self.slots = torch.full((Bm,), -1, **i32)
         self.ctx_len = torch.zeros(Bm, **i32)
@@ -149,10 +153,11 @@ class ModelRunner:
         self.q_start = torch.arange(Bm, **i32)
         self.work_seq = torch.arange(Bm, **i32)
         self.work_tile = torch.zeros(Bm, **i32)
-        self.temperature = torch.zeros(Bm, device=dev, dtype=torch.float32)
-        self.top_k = torch.zeros(Bm, **i32)
-        self.top_p = torch.ones(Bm, device=dev, dtype=torch.float32)
-        self.seeds = torch.zeros(Bm, 2, **i32)
+        self.temperature = self.slot_meta[Bm:2 * Bm].view(torch.float32)
+        self.top_k = self.slot_meta[2 * Bm:3 * Bm]
+        self.top_p = self.slot_meta[3 * Bm:4 * Bm].view(torch.float32)
+        self.top_p.fill_(1.0)
+        self.seeds = self.slot_meta[4 * Bm:].view(Bm, 2)
         self.ring = torch.zeros(RING_SIZE, Bm, **i32)
         self.ring_counter = torch.zeros(1, **i32)
         # ---- decode activations ----
