@@ -119,6 +119,10 @@ for s in "$@"; do
         step "jit15_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 &&
         DSSE_JIT_MARGIN_MS=1.1 step "jit11_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000
       done ;;
+    ratio_ab)  # mixed-step ITL ratio 2.0 vs the default 1.85, at 40 and 13 req/s
+      step r20_40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --itl-ratios 2.0 &&
+      step r185_40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 &&
+      step r20_13 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --itl-ratios 2.0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
