@@ -433,7 +433,21 @@ def test_paged_attention_decode(gpu, ctxs, part):
 def test_qkv_attention_decode_folded_epilogue(gpu, monkeypatch, cfg, M, part):
     """Attention mode 3 (QKV split-K reduce + RoPE + K/V write folded into the decode attention kernel) against
     the two-op path (gemm_qkv_rope + decode attention): same K/V cache bytes, same attention output."""
+    _folded_case(gpu, monkeypatch, cfg, M, part, None)
+
+
+@pytest.mark.parametrize("kwv", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("M,part", [(9, 512), (64, 128), (256, 8192)])
+def test_qkv_attention_decode_folded_key_split_waves(gpu, monkeypatch, kwv, M, part):
+    """The folded path with every key-split wave count (attn_kwv): each wave sums the slabs into its own LDS rows, and
+    the wave that attends over the newest key's page writes its K / V."""
+    _folded_case(gpu, monkeypatch, "auto", M, part, kwv)
+
+
+def _folded_case(gpu, monkeypatch, cfg, M, part, kwv):
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(**GEMM_CONFIGS[cfg]))
+    if kwv is not None:
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(attn_kwv=kwv))
     nh, nkv, H = 32, 8, 1024
     g = torch.Generator().manual_seed(M * 31 + part)
     ctxs = torch.randint(1, 700, (M,), generator=g).tolist()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Decode paged-attention microbenchmark: B sequences x ctx tokens, Mistral-7B heads (32 q / 8 kv, d 128).
 
-Usage (GPU box): python tools/bench_attn.py [--B 64] [--ctx 560] [--configs "KWV=4;KWV=1"]
+Usage (GPU box): python tools/bench_attn.py [--B 64] [--ctx 560] [--configs "KWV=4;KWV=1;KWV=1,PD=2"]
+(KWV / PD = the attn_kwv / attn_pd keys of DSSE_KERNEL_CFG.)
 Pages are randomly permuted over the cache and several layer caches are rotated (> 256 MiB Infinity
 Cache), so every call streams its K/V from HBM as in a decode step.  Times hipGraph replays; prints us and
 the achieved K/V bandwidth.
@@ -31,6 +32,7 @@ def main():
     ap.add_argument("--seq-pages", action="store_true", help="pages in cache order instead of a random permutation")
     args = ap.parse_args()
     ops.load_library(required=True)
+    base_cfg = os.environ.get("DSSE_KERNEL_CFG", "")
     dev = torch.device("cuda", 0)
     for B in [int(b) for b in args.B.split(",")]:
         for ctx in [int(c) for c in args.ctx.split(",")]:
@@ -53,9 +55,10 @@ def main():
                 part, nparts = decode_partitioning(B, args.hkv, ctx + 64, target_wgs=tw)
                 part_o = torch.empty(B * nparts * args.hkv * 16 * 128, device=dev)
                 part_ml = torch.empty(B * nparts * args.hkv * 16 * 2, device=dev)
-                for item in filter(None, cfg.split(",")):
-                    k, v = item.split("=")
-                    os.environ["DSSE_ATTN_" + k] = v
+                keys = {"KWV": "attn_kwv", "PD": "attn_pd"}  # DSSE_KERNEL_CFG keys (csrc/kernels/bindings.cpp)
+                os.environ["DSSE_KERNEL_CFG"] = base_cfg  # each config starts from the caller's environment
+                os.environ["DSSE_KERNEL_CFG"] = ops.kernel_cfg_env(
+                    **{keys[k]: v for k, v in (item.split("=") for item in filter(None, cfg.split(",")))})
                 ops.refresh_env()
 
                 def run(i):

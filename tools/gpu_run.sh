@@ -123,6 +123,19 @@ for s in "$@"; do
       step r20_40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --itl-ratios 2.0 &&
       step r185_40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 &&
       step r20_13 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --itl-ratios 2.0 ;;
+    attn_decode)  # decode attention alone (mode 0) at 64 / 256 sequences: key-split waves and pages in flight
+      step attn_decode 300 python -u tools/bench_attn.py --B 64,256 --ctx 560 --configs "KWV=1;KWV=1,PD=2;KWV=2;KWV=2,PD=2;KWV=4" ;;
+    kwv_ab)  # 256-stream step: decode attention key-split waves (folded QKV epilogue or not), alternating
+      for i in 1 2; do
+        step "kwv_def_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
+        DSSE_KERNEL_CFG=attn_kwv=4 step "kwv_4_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 &&
+        DSSE_KERNEL_CFG=attn_kwv=2 step "kwv_2_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256
+      done ;;
+    kwv64_ab)  # 64-stream step: decode attention key-split waves 2 (default) vs 4, alternating
+      for i in 1 2; do
+        step "kwv64_def_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 &&
+        DSSE_KERNEL_CFG=attn_kwv=4 step "kwv64_4_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
