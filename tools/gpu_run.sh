@@ -68,6 +68,7 @@ for s in "$@"; do
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
     kern_test) step kern_test 900 $PYT tests/test_kernels_gpu.py ;;
     attn_test) step attn_test 300 $PYT tests/test_kernels_gpu.py -k "prefill or rope_kv" ;;
+    folded_test) step folded_test 300 $PYT tests/test_kernels_gpu.py -k "folded" ;;
     flash_stamps) DSSE_FLASH_STAMPS="$out/fs.bin" step flash_stamps 300 python -u tools/bench_prefill_attn.py --T 8192
       python3 tools/flash_stamps.py "$out/fs.bin" > "$out/flash_stamps.md" 2>&1 ;;
     attn_bench) step attn_bench 300 python -u tools/bench_prefill_attn.py --T 8192,2048,512 --sdpa ;;
