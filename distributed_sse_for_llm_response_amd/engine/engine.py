@@ -314,6 +314,8 @@ class LLMEngine:
         # a prompt queued longer than this many steps gets the full prefill budget (TTFT guard, counted in steps:
         # identical on every TP rank)
         self.mixed_boost_steps = 40
+        # two or more prompts pending: mixed steps take the largest captured chunk (_mixed_budget)
+        self.mixed_queue_boost = True
         # adaptive prefill budget (separate passes while streams decode): DSSE_PREFILL_ITL_RATIO = r > 1 sizes each
         # pass so that a token gap spanning a decode step and a pass stays <= r x the occupied bucket's step
         # (PassCost), up to prefill_budget; a prompt that has waited DSSE_PREFILL_BOOST_STEPS steps gets the full
@@ -589,8 +591,12 @@ class LLMEngine:
             fit = self.cost.mixed_chunk(B, sizes)
             if fit is not None:
                 cap = max(cap, fit)
-        backlog = sum(len(s.prompt) - s.prefilled for s in self.slots
-                      if s is not None and s.state == "prefill" and not s.aborted)
+        pending = [s for s in self.slots if s is not None and s.state == "prefill" and not s.aborted]
+        backlog = sum(len(s.prompt) - s.prefilled for s in pending)
+        if self.mixed_queue_boost and sizes and len(pending) + len(self.waiting) >= 2:
+            # prompts queue: the largest captured chunk, so the weights stream once for more prompt rows (the
+            # step's length then matches a bucket-128 mixed step's, the ITL tail the serving mix already has)
+            cap = max(cap, max(sizes))
         if backlog > cap:
             n = -(-backlog // cap)  # steps the backlog needs at the cap
             per = -(-backlog // n)  # their even share

@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--skip-s", type=float, default=2.0)
     ap.add_argument("--warmup-requests", type=int, default=48)
     ap.add_argument("--engine", default="gpu", help="gpu | cpu (the tiny CPU model: a functional check of the tool)")
+    ap.add_argument("--no-queue-boost", action="store_true", help="mixed chunks stay at the ratio-sized cap when prompts queue")
     a = ap.parse_args()
 
     from distributed_sse_for_llm_response_amd.engine import bench_harness
@@ -131,6 +132,8 @@ def main():
                       temperature=1.0, first_token_timeout_ms=300000)
     t0 = time.time()
     app = ServingApp(cfg).start()
+    if a.no_queue_boost:
+        app.engine.mixed_queue_boost = False
     print(f"[bench_serving] engine up in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     port = app.port("edge")
     message = " ".join(f"w{i % 997}" for i in range(a.prompt_words))

@@ -137,6 +137,17 @@ for s in "$@"; do
         step "kwv64_def_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 &&
         DSSE_KERNEL_CFG=attn_kwv=4 step "kwv64_4_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
+    qboost_ab)  # serving at 40 / 13 req/s: largest mixed chunk when prompts queue (default) vs ratio-sized chunks
+      step qb40_on 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 &&
+      step qb40_off 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --no-queue-boost &&
+      step qb13_on 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 &&
+      step qb40_on2 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 &&
+      step qb40_off2 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --no-queue-boost ;;
+    qboost13_ab)  # serving at 13 req/s: queue boost on (default) vs off, alternating
+      for i in 1 2; do
+        step "qb13_on_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 &&
+        step "qb13_off_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --no-queue-boost
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
