@@ -1,6 +1,6 @@
 """Per-kernel breakdown of steady decode steps from a rocprofv3 kernel trace, one row per (kernel, grid).
 
-    python tools/step_kernels.py gpurun_out/prof/run_kernel_trace.csv [LAST]
+    python tools/step_kernels.py gpurun_out/prof/run_kernel_trace.csv [LAST] [tail | has=SUBSTRING]
 
 A step ends with the sampler's pick kernel.  The steps with the most common kernel count are steady (admission and
 finishing steps carry prefill or upload work); the last LAST (default 6) of them are averaged: calls, us per step and
@@ -15,6 +15,8 @@ import sys
 def main():
     path = sys.argv[1]
     last = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    tail = len(sys.argv) > 3 and sys.argv[3] == "tail"
+    has = sys.argv[3][4:] if len(sys.argv) > 3 and sys.argv[3].startswith("has=") else None
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -26,8 +28,19 @@ def main():
     spans = list(zip(ends[:-1], ends[1:]))
     if not spans:
         raise SystemExit("no decode steps (sample_pick) in the trace")
+    if has is not None:
+        def label(k):
+            return re.sub(r"\(.*", "", k[2]).replace("void ", "").replace("dsse::", "")[:55] + f" grid={k[3]}x{k[4]}"
+        spans = [(a, b) for a, b in spans if any(has in label(k) for k in rows[a + 1:b + 1])]
+        if not spans:
+            raise SystemExit(f"no step has a kernel matching {has!r}")
     mode = collections.Counter(b - a for a, b in spans).most_common(1)[0][0]
-    steady = [s for s in spans if s[1] - s[0] == mode][-last:]
+    if tail:
+        steady = spans[-last:]
+        mode = collections.Counter(b - a for a, b in steady).most_common(1)[0][0]
+        steady = [s for s in steady if s[1] - s[0] == mode]
+    else:
+        steady = [s for s in spans if s[1] - s[0] == mode][-last:]
     per = collections.defaultdict(lambda: [0, 0.0])
     wall = 0.0
     for a, b in steady:
