@@ -39,6 +39,7 @@ for s in "$@"; do
     bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     bench256b) step bench256b 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
+    prof256kwv4) DSSE_KERNEL_CFG=attn_kwv=4 step prof256kwv4 600 rocprofv3 --kernel-trace --stats -d "$out/prof256kwv4" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
     prof256) step prof256 600 rocprofv3 --kernel-trace --stats -d "$out/prof256" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     ttft512) step ttft512 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
