@@ -1,4 +1,4 @@
-// Prefill / wide GEMM, 256 (or 192) x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
+// Prefill / wide GEMM, 256 (or 192 / 128) x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
 // weight layout (api.h kTileChunk), M >= 256 (smaller M: split K, grid.z-style slices in the tile index).
 //
 // Why a new schedule (profiles/r4/pmc_gemm_r4.md): gemm_phased (gemm_tiled.hip cfg 4) issued the last A half of step
@@ -57,11 +57,11 @@ DEV int a_swz(int row) { return (row >> 1) & 5; }
 
 }  // namespace gp
 
-// BM: rows per workgroup tile, 256 or 192.  192 keeps the 256-row LDS image and schedule, and fills 48 of every
-// 64-row quadrant (the other 16 slot rows load as zeros, no traffic, and no MFMA reads them): 12 MFMAs per phase
-// instead of 16, for row counts that leave a 256-row block one-half to one-quarter empty (the mixed prefill + decode
-// steps' 320-384 rows, the 129-192-row decode bucket).  Slot row s of quadrant q, wave row wr holds X row
-// m0 + wr * BM / 2 + q * BM / 4 + s.
+// BM: rows per workgroup tile, 256, 192 or 128.  192 / 128 keep the 256-row LDS image and schedule and fill 48 / 32
+// of every 64-row quadrant (the other slot rows load as zeros, no traffic, and no MFMA reads them): 12 / 8 MFMAs per
+// phase instead of 16, for row counts that leave a 256-row block partly empty (the mixed prefill + decode steps'
+// 320-384 rows: 192; the 161-256-row decode buckets' qkv / down: 192 / 128).  Slot row s of quadrant q, wave row wr
+// holds X row m0 + wr * BM / 2 + q * BM / 4 + s.
 template <int MODE, int BM>
 __global__ void __launch_bounds__(512)
 gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
