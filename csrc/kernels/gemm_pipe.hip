@@ -1,5 +1,6 @@
-// Prefill / wide GEMM, 256 (or 192 / 128) x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the engine's tiled
-// weight layout (api.h kTileChunk), M >= 256 (smaller M: split K, grid.z-style slices in the tile index).
+// Prefill / wide GEMM, 256 (or 192 / 128) x 256 tile, deep LDS-DMA pipeline:  Y[M, N] = X[M, K] · W[N, K]ᵀ on the
+// engine's tiled weight layout (api.h kTileChunk), M >= 128 (few tiles: split K, grid.z-style slices in the tile
+// index).
 //
 // Why a new schedule (profiles/r4/pmc_gemm_r4.md): gemm_phased (gemm_tiled.hip cfg 4) issued the last A half of step
 // t+1 one phase before the counted wait that needed it, so every K step waited ~a full L2/HBM round trip -- 44 %
