@@ -259,14 +259,13 @@ TCfg pick_tiled(int M, int N, int K) {
     // for the weight-heavy 129-256-row shapes: gate_up 68.1 vs 73.9 us (256 rows) / 64.4 vs 66.2 (192), down
     // (K 14336) 42.9 vs 50.5 / 41.0 vs 42.0
     if (M > 128 && M <= 256 && (N > 8192 || K > 8192)) cfg = 5;
-    // round 5 (profiles/r5/pipe128_r5.log): the pipe schedule on 128 / 192-row tiles (cfg 10 / 9) for the decode
-    // buckets' qkv (N 6144) and down (K 14336): qkv 30.6 vs 33.1 us at 256 rows, 28.7 vs 30.4 at 192; down + norm
-    // 48.4 vs 52.1 at 256 (cfg 10), 43.8 vs 48.1 at 192 (cfg 9).  gate_up and o measured slower on them and keep
-    // cfg 5 / cfg 1
-    if (M > 160 && M <= 256 && N % 256 == 0 && N <= 8192 && env_int("t_small", 1)) {
-      if (K > 8192) cfg = M <= 192 ? 9 : 10;
-      else if (N > 4096) cfg = 10;
-    }
+    // round 5 (profiles/r5/pipe128_r5.log): the pipe schedule on the 128-row tile (cfg 10) for the 256-row
+    // bucket's qkv (N 6144) and down (K 14336): qkv 30.6 vs 33.1 us, down + norm 48.4 vs 52.1; 256-stream step
+    // 9.45-9.47 vs 9.54-9.55 ms alternating (small_ab_r5.log).  At 192 rows the kernels alone measured faster too
+    // (qkv 28.7 vs 30.4 us, down on cfg 9 43.8 vs 48.1) but the 192-stream step slower, 8.40-8.41 vs 8.31-8.37 ms
+    // (small192_ab_r5.log), so 129-192 rows keep the tiled kernels.  gate_up and o keep cfg 5 / cfg 1
+    if (M > 192 && M <= 256 && N % 256 == 0 && N <= 8192 && (K > 8192 || N > 4096) && env_int("t_small", 1))
+      cfg = 10;
     // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: 257-512 rows down
     // (K 14336) on the 256x256 tile split 8 ways (cfg 8: 69 vs 72 us on round 4's phased tile, vs 92 us on
     // 256x128), o on 256x128 (33 vs 38 us), qkv on cfg 8 (43 vs 46 us); 513-1024 rows N <= 4096 (o, down) on

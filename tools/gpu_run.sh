@@ -149,6 +149,13 @@ for s in "$@"; do
         step "qb13_on_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 &&
         step "qb13_off_$i" 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 --no-queue-boost
       done ;;
+    o512)  # o projection (+ norm) at 448-512 rows: default (256x128 split) vs the pipe tiles
+      step o512 300 python -u tools/bench_decode_gemm.py --shape o --M 448,512 --variants "split_norm,split_norm:t_cfg=10;t_split=4,split_norm:t_cfg=10;t_split=2,split_norm:t_cfg=8;t_split=4,split_norm:t_cfg=8;t_split=8,split_norm:t_cfg=1;t_split=2" ;;
+    small192_ab)  # 192-stream step: cfg 9 / 10 picks for qkv / down (default) vs t_small=0, alternating
+      for i in 1 2; do
+        step "s192_on_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 192 &&
+        DSSE_KERNEL_CFG=t_small=0 step "s192_off_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 192
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
