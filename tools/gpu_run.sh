@@ -37,6 +37,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench64) step bench64 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench256) step bench256 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
+    bench192) step bench192 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 192 ;;
     bench256b) step bench256b 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 256 ;;
     prof64) step prof64 600 rocprofv3 --kernel-trace --stats -d "$out/prof64" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 ;;
     prof256kwv4) DSSE_KERNEL_CFG=attn_kwv=4 step prof256kwv4 600 rocprofv3 --kernel-trace --stats -d "$out/prof256kwv4" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
