@@ -157,6 +157,9 @@ for s in "$@"; do
         step "s192_on_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 192 &&
         DSSE_KERNEL_CFG=t_small=0 step "s192_off_$i" 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --streams 192
       done ;;
+    m128)  # the 65-128-row bucket: default kernels (ring2 / gemm_wide) vs the tiled / pipe kernels forced
+      step m128_gu 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 96,128 --variants "silu,silu:gemm_impl=4;t_cfg=5,silu:gemm_impl=4;t_cfg=10,silu:gemm_impl=4;t_cfg=8" &&
+      step m128_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv,down --M 128 --variants "split_norm,split_norm:gemm_impl=4;t_cfg=10,split_norm:gemm_impl=4;t_cfg=5,split_norm:gemm_impl=4;t_cfg=1" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
