@@ -160,6 +160,8 @@ for s in "$@"; do
     m128)  # the 65-128-row bucket: default kernels (ring2 / gemm_wide) vs the tiled / pipe kernels forced
       step m128_gu 300 python -u tools/bench_decode_gemm.py --shape gate_up --M 96,128 --variants "silu,silu:gemm_impl=4;t_cfg=5,silu:gemm_impl=4;t_cfg=10,silu:gemm_impl=4;t_cfg=8" &&
       step m128_qkv 300 python -u tools/bench_decode_gemm.py --shape qkv,down --M 128 --variants "split_norm,split_norm:gemm_impl=4;t_cfg=10,split_norm:gemm_impl=4;t_cfg=5,split_norm:gemm_impl=4;t_cfg=1" ;;
+    m256bm)  # 256 rows: 256-row tiles (X re-read less) for o / qkv / down vs the defaults
+      step m256bm 300 python -u tools/bench_decode_gemm.py --shape o,qkv,down --M 256 --variants "split_norm,split_norm:t_cfg=0;t_split=4,split_norm:t_cfg=0;t_split=8,split_norm:t_cfg=8;t_split=8,split_norm:t_cfg=8;t_split=16" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
