@@ -76,3 +76,35 @@ def test_engine_mixed_steps_emit_the_same_streams():
     assert st_mix["mixed_steps"] > 0 and st_sep["mixed_steps"] == 0
     assert mix == sep
     assert all(v[-1][2] and len(v) == 10 for v in mix.values())
+
+
+def test_mixed_budget_queue_boost():
+    """LLMEngine._mixed_budget: one pending prompt is split into even chunks at the default cap (506 -> 2 x 256);
+    with two or more prompts pending the cap is the largest captured chunk (the queue drains faster: 40 req/s TTFT
+    p50 40 -> 32 ms, profiles/r5/serving_r5.md); mixed_queue_boost = False keeps the default cap."""
+    from distributed_sse_for_llm_response_amd.engine.engine import Sequence
+
+    os.environ["DSSE_MIXED"] = "1"
+    try:
+        e = LLMEngine(_runner(), eos_id=-1, prefill_budget=512)
+    finally:
+        os.environ.pop("DSSE_MIXED", None)
+    e.cost = None
+    e.r.mx_graphs = {64: [(128, None), (256, None), (384, None)]}
+    e.r.mixed_chunks = lambda B: [128, 256, 384]
+    e.r.mixed_chunk = lambda B: 256
+
+    def pending(n):
+        for i in range(len(e.slots)):
+            e.slots[i] = None
+        for i in range(n):
+            s = Sequence(rid=i, conversation_id=f"p{i}", prompt=list(range(506)), params=SamplingParams())
+            s.state = "prefill"
+            e.slots[i] = s
+
+    pending(1)
+    assert e._mixed_budget(64) == 256  # 506 tokens: two even 253-token shares, rounded up to 64
+    pending(2)
+    assert e._mixed_budget(64) == 384  # the boost: cap 384, 1012 tokens in three even shares of 338 -> 384
+    e.mixed_queue_boost = False
+    assert e._mixed_budget(64) == 256
