@@ -1842,6 +1842,7 @@ void InspectionGate::run(Worker& w) {
   const bool hybrid = cfg.inspection == InspectionMode::kHybrid;
   const int64_t window = (int64_t)cfg.inspection_buffer_ms * 1000000LL;
   std::unordered_map<std::string, Held> held;
+  int64_t next_age_scan = 0;  // the dead map's age-out scan runs at most once a second (a full-map walk)
   while (!stop_.load()) {
     std::deque<FramePtr> batch;
     {
@@ -1876,8 +1877,9 @@ void InspectionGate::run(Worker& w) {
         if (inline_frame(ri, f, out) && !f->done) w.dead.emplace(f->conversation_id, mono_ns());
       }
     }
-    if (w.dead.size() > 4096) {  // age out entries whose done frame never arrived (never a wholesale clear)
-      const int64_t now = mono_ns();
+    if (w.dead.size() > 4096 && mono_ns() >= next_age_scan) {  // age out entries whose done frame never arrived
+      const int64_t now = mono_ns();                            // (never a wholesale clear)
+      next_age_scan = now + 1000000000LL;
       for (auto it = w.dead.begin(); it != w.dead.end();) it = now - it->second > kDeadAgeNs ? w.dead.erase(it) : std::next(it);
     }
     if (hybrid) {  // buffer windows that ran out; forget conversations idle for 10 minutes

@@ -322,8 +322,11 @@ class LLMEngine:
         # budget (TTFT guard).  Unset / 0: the fixed prefill_budget.
         # Mixed steps (the default): the ratio is on by default (1.85: a mixed step within ~2x the bucket's step,
         # VERDICT r4 item 2's ITL p99 target, with margin) and sizes each step's prompt chunk.
+        # TP groups (deterministic): no PassCost -- its fit comes from this rank's own GPU event timings, so ranks
+        # would pick different chunk sizes and replay graphs of different row counts (mismatched collectives)
         ratio = float(os.environ.get("DSSE_PREFILL_ITL_RATIO", "1.85" if self.mixed else "0") or 0)
-        self.cost = PassCost(ratio) if ratio > 1.0 and runner.device.type == "cuda" else None
+        self.cost = PassCost(ratio) if ratio > 1.0 and runner.device.type == "cuda" and not self.deterministic \
+            else None
         self.boost_steps = int(os.environ.get("DSSE_PREFILL_BOOST_STEPS", "8"))
         self._jit = None  # (host time the newest step started, its expected ms): jit_delay
 
@@ -586,7 +589,7 @@ class LLMEngine:
         sizes = self.r.mixed_chunks(B) if hasattr(self.r, "mixed_chunks") and getattr(self.r, "mx_graphs", None) \
             else []
         cap = self.r.mixed_chunk(B)
-        if self.cost is not None and sizes:
+        if self.cost is not None and sizes and not self.deterministic:
             self.cost.poll()
             fit = self.cost.mixed_chunk(B, sizes)
             if fit is not None:
@@ -605,7 +608,8 @@ class LLMEngine:
 
     def set_itl_ratio(self, ratio: float) -> None:
         """Adaptive prefill budget on (ratio > 1) or off (bench_serving sweeps both in one process)."""
-        self.cost = PassCost(ratio) if ratio > 1.0 and self.r.device.type == "cuda" else None
+        self.cost = PassCost(ratio) if ratio > 1.0 and self.r.device.type == "cuda" and not self.deterministic \
+            else None
 
     def _oldest_prefill_step(self) -> int:
         oldest = min((s.enq_step for s in self.slots if s is not None and s.state == "prefill"), default=self.step_no)
@@ -616,7 +620,7 @@ class LLMEngine:
     def _schedule_prefill(self, t: int):
         running_decode = any(s is not None and s.state == "decode" for s in self.slots)
         budget = self.prefill_budget if running_decode else self.idle_prefill_budget
-        if running_decode and self.cost is not None and not self.mixed:
+        if running_decode and self.cost is not None and not self.mixed and not self.deterministic:
             self.cost.poll()
             adaptive = self.cost.budget(self._decode_bucket(), self.prefill_budget)
             if adaptive is not None and self.step_no - self._oldest_prefill_step() <= self.boost_steps:

@@ -156,14 +156,23 @@ class IpcAllReduce:
                 ok, why = False, f"open: {type(e).__name__}: {e}"
         elif ok:
             ok, why = False, "a peer could not allocate its buffer"
-        if ok:
-            why = ctx.self_test()
-            ok = not why
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
-        if dist.get_backend(comm.group) == "gloo":
-            flag = flag.cpu()
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
-        if int(flag.item()) == 0:
+
+        def vote(mine: bool) -> bool:
+            flag = torch.tensor([1 if mine else 0], dtype=torch.int32, device=device)
+            if dist.get_backend(comm.group) == "gloo":
+                flag = flag.cpu()
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
+            return int(flag.item()) == 1
+
+        # every rank opened every peer before any rank starts the self-test's kernels and collectives
+        if not vote(ok):
+            if ctx is not None:
+                ctx.close()
+            return None, why or "another rank of the TP group could not open the IPC buffers"
+        why = ctx.self_test()  # votes after every check: all ranks return from it at the same point
+        ok = not why
+        if not vote(ok):
+            ctx.close()
             return None, why or "another rank of the TP group failed the IPC all-reduce self-test"
         return ctx, ""
 
@@ -196,13 +205,24 @@ class IpcAllReduce:
         torch.ops.dsse.ar_gather(inp, out, self.peers, self.comm.rank, self.rows, self.hidden, self.gepoch, self.err)
 
     def self_test(self) -> str:
-        """Fused all-reduce of random partials vs RCCL/gloo sum + reference norm, at a few row counts; ""=ok."""
+        """Fused all-reduce of random partials vs RCCL/gloo sum + reference norm, and the candidate gather vs
+        all_gather, at a few row counts; ""=ok.  Every rank runs the same sequence of collectives whatever its own
+        checks find: after each check the ranks vote (MIN of an ok flag) and all stop together at the first failure
+        anywhere, so a rank that fails cannot leave its peers inside an IPC kernel or a collective it skipped."""
         from ..ops import reference as R
 
         gen = torch.Generator().manual_seed(1234 + self.comm.rank)
         H = self.hidden
+        gloo = dist.get_backend(self.comm.group) == "gloo"
+
+        def vote(why: str) -> bool:
+            flag = torch.tensor([0 if why else 1], dtype=torch.int32, device="cpu" if gloo else self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.comm.group)
+            return int(flag.item()) == 1
+
         for M in sorted({1, min(7, self.rows), self.rows}):
             for _ in range(3):  # both buffer parities, twice
+                why = ""
                 tmp = (torch.randn(M, H, generator=gen) * 0.5).bfloat16().to(self.device)
                 resid0 = torch.randn(M, H, generator=torch.Generator().manual_seed(M)).to(self.device)
                 w = (1 + 0.1 * torch.randn(H, generator=torch.Generator().manual_seed(7))).bfloat16().to(self.device)
@@ -216,16 +236,19 @@ class IpcAllReduce:
                 R.rmsnorm(r_ref.clone(), w.cpu(), y_ref, 1e-5)
                 torch.cuda.synchronize(self.device)
                 if int(self.err.item()) != 0:
-                    return "self-test: a peer wait timed out"
-                err_r = float((r.cpu() - r_ref).abs().max())
-                err_y = float((y.cpu().float() - y_ref.float()).abs().max())
-                if err_r > 1e-3 or err_y > 5e-2:
-                    return f"self-test: M={M} max |resid err| {err_r:.3g}, |y err| {err_y:.3g}"
+                    why = "self-test: a peer wait timed out"
+                else:
+                    err_r = float((r.cpu() - r_ref).abs().max())
+                    err_y = float((y.cpu().float() - y_ref.float()).abs().max())
+                    if err_r > 1e-3 or err_y > 5e-2:
+                        why = f"self-test: M={M} max |resid err| {err_r:.3g}, |y err| {err_y:.3g}"
+                if not vote(why):
+                    return why or "self-test: another rank's all-reduce check failed"
                 # the candidate gather: exact copies of every rank's rows, rank-major
                 cand = torch.randn(M, 16, 2, generator=gen).to(self.device)
                 got = torch.zeros(self.comm.size, M, 16, 2, device=self.device)
                 self.gather(cand, got)
-                if dist.get_backend(self.comm.group) == "gloo":
+                if gloo:
                     ref_all = torch.zeros(self.comm.size * cand.numel())
                     dist.all_gather_into_tensor(ref_all, cand.cpu().view(-1), group=self.comm.group)
                 else:
@@ -234,9 +257,11 @@ class IpcAllReduce:
                     ref_all = ref_dev.cpu()
                 torch.cuda.synchronize(self.device)
                 if int(self.err.item()) != 0:
-                    return "self-test: a peer gather wait timed out"
-                if not torch.equal(got.cpu().view(-1), ref_all):
-                    return f"self-test: M={M} candidate gather differs from all_gather"
+                    why = "self-test: a peer gather wait timed out"
+                elif not torch.equal(got.cpu().view(-1), ref_all):
+                    why = f"self-test: M={M} candidate gather differs from all_gather"
+                if not vote(why):
+                    return why or "self-test: another rank's gather check failed"
         return ""
 
 

@@ -75,6 +75,9 @@ class EngineLoop(threading.Thread):
         self.stop_flag = threading.Event()
         self.error = None
         self.halted = False  # set by the watchdog after it failed every stream: the loop must not touch the engine
+        # publish() and the watchdog's halt + [ERROR] publish serialise on this lock, so no token frame of the loop
+        # thread can follow a stream's terminal [ERROR] (the loop may be inside publish() when the watchdog fires)
+        self.pub_lock = threading.Lock()
         rt = rt_mod.load()
         self._rt = rt
         self._remote = hasattr(runtime, "observe")
@@ -117,9 +120,16 @@ class EngineLoop(threading.Thread):
             events = self.faults.filter_events(events)
         self.publish(events)
 
-    def publish(self, events):
+    def publish(self, events, final: bool = False):
+        """Hand events to the runtime.  After the watchdog halted the loop only its own `final` batch goes out."""
         if not events:
             return
+        with self.pub_lock:
+            if self.halted and not final:
+                return
+            self._publish(events)
+
+    def _publish(self, events):
         self.rt.publish_tokens([e.conversation_id for e in events], [e.token_id for e in events],
                                [e.sequence for e in events], [e.done for e in events], 0,
                                [e.text for e in events], [FINISH_CODES.get(e.finish, 0) for e in events],

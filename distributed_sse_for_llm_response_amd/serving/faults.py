@@ -120,11 +120,12 @@ class Watchdog(threading.Thread):
         The loop is halted first (on waking it publishes nothing and leaves its loop) and the [ERROR] events are built
         from a read-only view: only the loop thread ever mutates the engine, even if its wait completes later."""
         self.failed = True
-        self.loop.halted = True
+        with self.loop.pub_lock:  # wait out a publish() the loop thread is inside of; after this, none of its frames
+            self.loop.halted = True
         print(json.dumps({"level": "ERROR", "msg": "engine hung; failing every stream", "seconds": round(idle_for, 3)}),
               flush=True)
         try:
-            self.loop.publish(self.loop.engine.error_events())
+            self.loop.publish(self.loop.engine.error_events(), final=True)
         finally:
             self.set_ready(False)
             if os.environ.get("DSSE_STEP_FAIL_EXIT", "1") != "0":

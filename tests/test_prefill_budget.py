@@ -175,3 +175,71 @@ def test_mixed_backlog_split_into_even_chunks(monkeypatch):
     assert mixed_out == sep_out
     assert sep_sizes == []
     assert mixed_sizes == [192, 108]  # 300 rows over two steps: ceil(150 / 64) * 64 = 192, then the rest
+
+
+def test_tp_ranks_ignore_their_own_pass_costs(monkeypatch):
+    """TP groups run the scheduler on every rank (deterministic mode).  Two ranks whose PassCost fits differ (each
+    from its own GPU's event timings) must still pick identical chunk sizes, in mixed and in separate-pass mode:
+    different row counts would replay different graphs and mismatch the collectives (engine.py)."""
+    import torch
+
+    from distributed_sse_for_llm_response_amd.engine.engine import LLMEngine, SamplingParams
+    from distributed_sse_for_llm_response_amd.engine.model_runner import ModelRunner
+    from distributed_sse_for_llm_response_amd.engine.weights import convert_standard
+    from distributed_sse_for_llm_response_amd.models.mistral import TINY, init_standard_weights
+
+    w = convert_standard(TINY, init_standard_weights(TINY, seed=13))
+
+    def fake_cost(slope):
+        pc = PassCost(2.0)
+        for t in (64, 128, 256, 128):
+            pc.observe("prefill", t, 1.0 + slope * t)
+        pc.observe("decode", 1, 2.3)
+        pc.observe("decode", 64, 2.0)
+        for C in (128, 256, 384):
+            pc.observe("mixed", (64, C), 2.0 + slope * C)
+        return pc
+
+    # mixed steps: _mixed_budget with captured sizes; the two "ranks" see different fits
+    monkeypatch.setenv("DSSE_MIXED", "1")
+    budgets = {}
+    for det in (True, False):
+        for slope in (0.001, 0.02):
+            r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device="cpu", use_graphs=False)
+            e = LLMEngine(r, eos_id=-1, prefill_budget=512, deterministic=det)
+            e.cost = fake_cost(slope)
+            r.mx_graphs = {1: object()}
+            r.mixed_chunks = lambda B: [128, 256, 384]
+            r.mixed_chunk = lambda B: 128
+            budgets[(det, slope)] = e._mixed_budget(64)
+    assert budgets[(False, 0.001)] != budgets[(False, 0.02)]  # the fits do move the chunk when not in TP mode
+    assert budgets[(True, 0.001)] == budgets[(True, 0.02)] == 128
+
+    # separate prefill passes: the chunk list of a whole run is identical across the two ranks
+    monkeypatch.setenv("DSSE_MIXED", "0")
+
+    def run(slope):
+        r = ModelRunner(w, num_blocks=64, max_batch=4, max_model_len=512, device="cpu", use_graphs=False)
+        e = LLMEngine(r, eos_id=-1, prefill_budget=256, deterministic=True)
+        e.cost = fake_cost(slope)
+        chunks = []
+        orig = r.prefill
+
+        def spy(seqs, ring_row):
+            chunks.append(sum(len(s.tokens) for s in seqs))
+            return orig(seqs, ring_row=ring_row)
+
+        r.prefill = spy
+        g = torch.Generator().manual_seed(3)
+        e.add_request("a", torch.randint(3, TINY.vocab_size, (20,), generator=g).tolist(),
+                      SamplingParams(temperature=0.0, max_tokens=8))
+        long_prompt = torch.randint(3, TINY.vocab_size, (300,), generator=g).tolist()
+        for step in range(300):
+            if step == 2:
+                e.add_request("b", long_prompt, SamplingParams(temperature=0.0, max_tokens=4))
+            e.step()
+            if step > 2 and not e.has_work():
+                break
+        return chunks
+
+    assert run(0.001) == run(0.02)
