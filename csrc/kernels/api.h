@@ -29,7 +29,12 @@ struct GemmEpi {
   int nh, nkv;
   int num_slots;          // mode 4: KV slots in the cache (pages * kBS); checked build only
   int rope_len;           // mode 4: rows of the rope table; checked build only
+  // split-K fix-up inside the launch (gemm_pipe.hip, partial_only = 2): [4 + 2 * kFixTiles] ints -- word 0 counts
+  // timed-out waits, then the per-tile ticket and done counters (zero between launches: each tile's last arriver
+  // resets its pair); null when unused
+  int* fix_cnt;
 };
+constexpr int kFixTiles = 8192;  // tiles of one fix-up launch at most
 
 
 struct AttnParams {
@@ -100,6 +105,7 @@ hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const voi
                            int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M, const void* W,
                           int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
+size_t dsse_gemm_pipe_fix_floats(int bm, int S, int M, int N);
 hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);

@@ -222,7 +222,8 @@ WCfg pick_wide(int M, int N, int K) {
   return c;
 }
 
-// cfg 8 / 9 = the pipelined 256 x 256 / 192 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's configurations
+// cfg 8 / 9 / 10 = the pipelined 256 / 192 / 128 x 256 kernel of gemm_pipe.hip; 0, 1, 5 = gemm_tiled.hip's
+// configurations.  partial_only 2 (gemm_pipe only) = split-K slices combined inside the launch (run_pipe_fix).
 hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X, int ldx, int M, const void* W, int K,
                       int N, const dsse::GemmEpi* ep, float* part) {
   if (cfg == 8 || cfg == 9 || cfg == 10)
@@ -230,18 +231,99 @@ hipError_t tiled_call(int mode, int cfg, int S, int partial_only, const void* X,
   return dsse_gemm_tiled(mode, cfg, S, partial_only, X, ldx, M, W, K, N, ep, part, cur_stream());
 }
 
+// In-launch split-K fix-up state (gemm_pipe.hip FIX): per device, 2 * kFixTiles arrival counters + a timeout word,
+// zeroed once; every launch leaves the counters it used at zero (each tile's last arriver resets its pair), and
+// launches on one stream never overlap.  (Launches of one process on two streams at once would share them: the
+// engine issues every GEMM on its one compute stream.)
+using dsse::kFixTiles;
+#ifndef DSSE_PIPE_STAMPS
+#define DSSE_PIPE_STAMPS 0
+#endif
+constexpr int kStampWgs = 8192;  // stamps build: [workgroup][8] u64 after the counters
+at::Tensor& fix_state(const at::Device& dev) {
+  static std::unordered_map<int, at::Tensor> per_dev;
+  auto it = per_dev.find(dev.index());
+  if (it == per_dev.end()) {
+    const int64_t n = 4 + 2 * kFixTiles + (DSSE_PIPE_STAMPS ? kStampWgs * 16 : 0);
+    it = per_dev.emplace(dev.index(), at::zeros({n}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+  }
+  return it->second;
+}
+int* fix_counters(const at::Device& dev) { return fix_state(dev).data_ptr<int>(); }
+
 constexpr int kMaxDecodeM = 512;  // gemm_stream: one workgroup per tile group up to 256 rows, row blocks above
 
 // Tiled LDS-DMA GEMMs (gemm_tiled.hip, gemm_pipe.hip; prefill and wide batches).  DSSE_KERNEL_CFG overrides: t_cfg
-// (0 = 256x128, 1 = 128x128, 5 = 128x256, 8 = 256x256 gemm_pipe, 9 = 192x256 gemm_pipe), t_split.
+// (0 = 256x128, 1 = 128x128, 5 = 128x256, 8 / 9 / 10 = the 256 / 192 / 128 x 256 gemm_pipe tile), t_split, t_fix
+// (1 = split-K slices combined inside the launch, gemm_pipe only), t_model (0 = the round-5 row-range table).
 struct TCfg {
   int cfg, S;
   bool ok;
+  bool fix = false;    // S > 1 combined inside the launch (gemm_pipe FIX); else S > 1 = fp32 slabs
+  double est_us = 0;   // the cost model's estimate (pipe_plan), 0 for the table's choices
 };
-TCfg pick_tiled(int M, int N, int K) {
+
+// Cost model of one gemm_pipe launch (round 6, profiles/r6/gemm_model_r6.md), from the per-CU rates the pipe kernel
+// reaches on MI355X: a workgroup is bound by its LDS fill (X rows from L2 + weight rows, ~46 GB/s per CU when both
+// streams mix: tools/fillbench.hip, profiles/r6/fillbench_r6.log) or by its MFMA issue (~5.5 TFLOP/s per CU, the
+// kernel's 1.4 PFLOP/s at 8192 rows), plus ~3 us of pipeline fill and epilogue.  One 128 KiB workgroup per CU, so
+// the grid runs in ceil(WGs / 256) rounds of equal workgroups.  Split K costs the fp32 slabs: in-launch (fix) the
+// S - 1 slots of a tile are written by the first arrivers and read by the last (~60 GB/s per CU each way, on the
+// critical path once); left to a consumer (the norm / attention kernel) one slab write per workgroup plus the
+// consumer's read of S x M x N x 4 bytes at HBM rate.
+double pipe_est_us(int M, int N, int K, int bm, int S, bool fix) {
+  constexpr double kFill = 46e3, kMfma = 5.5e6, kT0 = 3.0, kSlot = 60e3, kHbm = 6.0e6, kCUs = 256;
+  const int nbm = (M + bm - 1) / bm, rows = std::min(bm, M), Kr = K / S;
+  const double wgs = (double)nbm * (N / 256) * S;
+  const double bytes = (double)(rows + 256) * Kr * 2, flops = 2.0 * bm * 256 * Kr;
+  const double t_wg = kT0 + std::max(bytes / kFill, flops / kMfma);
+  double t = std::ceil(wgs / kCUs) * t_wg;
+  if (S > 1) {
+    const double slot = (double)bm * 256 * 4;
+    t += fix ? S * slot / kSlot : slot / kSlot + (double)S * M * N * 4 / kHbm;
+  }
+  return t;
+}
+
+// Best gemm_pipe configuration by the model: tile 256 / 192 / 128 rows x split 1-16, combined in the launch or (when
+// `slab_consumer`, the caller reduces fp32 slabs in its next kernel) left as slabs.
+TCfg pipe_plan(int M, int N, int K, bool slab_consumer) {
+  TCfg best{};
+  best.ok = false;
+  for (int bm : {256, 192, 128}) {
+    const long tiles = (long)((M + bm - 1) / bm) * (N / 256);
+    for (int S = 1; S <= 16; S *= 2) {
+      if (K % (128 * S) != 0) break;
+      for (int fix = 0; fix < 2; ++fix) {
+        if (S == 1 && fix) continue;
+        if (S > 1 && !fix && !slab_consumer) continue;
+        if (fix && (tiles > dsse::kFixTiles || (double)tiles * (S - 1) * bm * 256 * 4 > (1u << 30))) continue;
+        const double t = pipe_est_us(M, N, K, bm, S, fix);
+        if (!best.ok || t < best.est_us * 0.98) {  // ties: the simpler (earlier) form
+          best.ok = true;
+          best.est_us = t;
+          best.cfg = bm == 256 ? 8 : bm == 192 ? 9 : 10;
+          best.S = S;
+          best.fix = fix;
+        }
+      }
+    }
+  }
+  return best;
+}
+
+constexpr int kModelMinM = 256;  // above this many rows every N % 256 == 0 projection is planned by pipe_plan
+
+TCfg pick_tiled(int M, int N, int K, bool slab_consumer = false) {
   TCfg c{};
   int cfg = env_int("t_cfg", -1);
-  if (cfg != 0 && cfg != 1 && cfg != 5 && cfg != 8 && cfg != 9 && cfg != 10) {
+  const bool forced = cfg == 0 || cfg == 1 || cfg == 5 || cfg == 8 || cfg == 9 || cfg == 10;
+  if (!forced && env_int("t_model", 1) && N % 256 == 0 && K % 128 == 0 && M > kModelMinM) {
+    c = pipe_plan(M, N, K, slab_consumer);
+    if (c.ok) return c;
+  }
+  if (!forced) {
+    // up to kModelMinM rows (and N % 256 != 0): the decode buckets' measured table
     // round 5 (profiles/r5/gemm_pipe_r5.md): the 256x256 tile of gemm_pipe.hip (cfg 8: 8 waves, every LDS-DMA
     // half-tile five phases ahead of its wait) once it yields >= ~160 workgroups -- 1.35-1.40 PFLOP/s at 8192 rows,
     // +5-7 % over round 4's phased cfg 4; below that the 256x128 tile (3-stage ring) fills more CUs; 128x128 for tiny M
@@ -261,25 +343,17 @@ TCfg pick_tiled(int M, int N, int K) {
     if (M > 128 && M <= 256 && (N > 8192 || K > 8192)) cfg = 5;
     // round 5 (profiles/r5/pipe128_r5.log): the pipe schedule on the 128-row tile (cfg 10) for the 256-row
     // bucket's qkv (N 6144) and down (K 14336): qkv 30.6 vs 33.1 us, down + norm 48.4 vs 52.1; 256-stream step
-    // 9.45-9.47 vs 9.54-9.55 ms alternating (small_ab_r5.log).  At 192 rows the kernels alone measured faster too
-    // (qkv 28.7 vs 30.4 us, down on cfg 9 43.8 vs 48.1) but the 192-stream step slower, 8.40-8.41 vs 8.31-8.37 ms
-    // (small192_ab_r5.log), so 129-192 rows keep the tiled kernels.  gate_up and o keep cfg 5 / cfg 1
+    // 9.45-9.47 vs 9.54-9.55 ms alternating (small_ab_r5.log).  129-192 rows keep the tiled kernels
+    // (small192_ab_r5.log).  gate_up and o keep cfg 5 / cfg 1
     if (M > 192 && M <= 256 && N % 256 == 0 && N <= 8192 && (K > 8192 || N > 4096) && env_int("t_small", 1))
       cfg = 10;
-    // prompt chunks of 257-1024 rows (the 512 / 1024-row prefill graphs), narrow projections: 257-512 rows down
-    // (K 14336) on the 256x256 tile split 8 ways (cfg 8: 69 vs 72 us on round 4's phased tile, vs 92 us on
-    // 256x128), o on 256x128 (33 vs 38 us), qkv on cfg 8 (43 vs 46 us); 513-1024 rows N <= 4096 (o, down) on
-    // 128x128 (50 / 153 vs 65 / 205 us; profiles/r3/prefill_chunk_gemm.md)
+    // t_model=0 (the round-5 table above 256 rows, for A/Bs): 257-512 rows cfg 8 / 9 / 0, 513-1024 narrow cfg 1
     if (N <= 8192 && M > 256 && M <= 512) cfg = (K > 8192 || N > 4096) ? 8 : 0;
     if (N <= 4096 && M > 512 && M <= 1024) cfg = 1;
-    // round 5 (profiles/r5/pipe192_r5.log): 257-384 rows -- the mixed prefill + decode steps' 320 / 384 rows -- leave
-    // the second 256-row block a quarter to three quarters empty; the 192-row pipe tile (cfg 9) fills it: gate_up
-    // 88.2 vs 99.1 us at 384 rows (87.6 vs 96.6 at 320), down + norm 58.0 vs 62.9 (54.4 vs 61.2), qkv 37.1 vs 41.5
-    // (34.2 vs 38.2); o (cfg 0) even, so it stays
     if (cfg == 8 && M > 256 && M <= 384) cfg = 9;
   }
-  constexpr int min_wgs = 160;  // split K until this many workgroups (M <= 512)
-  // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8, 9)
+  constexpr int min_wgs = 160;  // split K until this many workgroups (table choices, M <= 512)
+  // tile shapes by cfg (gemm_tiled.hip launch_t_mode: 0, 1, 5; gemm_pipe.hip: 8, 9, 10)
   const int BM = cfg == 1 || cfg == 5 || cfg == 10 ? 128 : cfg == 9 ? 192 : 256, BN = cfg == 0 || cfg == 1 ? 128 : 256;
   c.cfg = cfg;
   c.S = 1;
@@ -294,7 +368,26 @@ TCfg pick_tiled(int M, int N, int K) {
     while (M <= kMaxDecodeM && tiles * S < min_wgs && K % (kq * S * 2) == 0 && K / (S * 2) >= 512) S *= 2;
   }
   c.S = S;
+  // t_fix=1: combine the slices inside the launch (gemm_pipe only, and only when the tile count fits the counters)
+  c.fix = pipe && S > 1 && env_int("t_fix", 0) == 1 && (long)((M + BM - 1) / BM) * (N / 256) <= dsse::kFixTiles;
+  if (pipe) c.est_us = pipe_est_us(M, N, K, BM, S, c.fix);
   return c;
+}
+
+// One tiled / pipe launch for a plain epilogue (no slabs left for a consumer): S > 1 is combined in the launch (fix)
+// or by launch_splitk_reduce.
+void run_tiled(int mode, const TCfg& c, const Tensor& x, const Tensor& w, int M, int N, int K, dsse::GemmEpi& ep) {
+  at::Tensor part;
+  if (c.S > 1 && c.fix) {
+    const int bm = c.cfg == 10 ? 128 : c.cfg == 9 ? 192 : 256;
+    part = at::empty({(int64_t)dsse_gemm_pipe_fix_floats(bm, c.S, M, N)}, x.options().dtype(at::kFloat));
+    ep.fix_cnt = fix_counters(x.device());
+    DSSE_CHECK_HIP(tiled_call(mode, c.cfg, c.S, 2, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep, part.data_ptr<float>()));
+    return;
+  }
+  if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
+  DSSE_CHECK_HIP(tiled_call(mode, c.cfg, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                            c.S > 1 ? part.data_ptr<float>() : nullptr));
 }
 
 // 0 = register-streaming (gemm_skinny.hip; tiny batches, X re-reads are cheap), 2 = X streamed through LDS
@@ -351,11 +444,7 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   const int impl = gemm_impl(M, N, K);
   TORCH_CHECK(impl >= 0, "no GEMM kernel for M=", M, " N=", N, " K=", K, " (tiled path needs N % 128, K % 64)");
   if (impl == 4) {
-    const TCfg c = pick_tiled(M, N, K);
-    at::Tensor part;
-    if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
-    DSSE_CHECK_HIP(tiled_call(mode, c.cfg, c.S, 0, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
-                              c.S > 1 ? part.data_ptr<float>() : nullptr));
+    run_tiled(mode, pick_tiled(M, N, K), x, w, M, N, K, ep);
     return;
   }
   TORCH_CHECK(M <= 64 || impl >= 2, "M > 64 needs the X-streaming kernel shape contract (K % 512, N % 64)");
@@ -418,8 +507,8 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
   const bool shape_ok = M >= 1 && K % 128 == 0 && N % 16 == 0 && w.size(1) == K;
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
   if (impl == 4) {
-    const TCfg c = pick_tiled(M, N, K);
-    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+    const TCfg c = pick_tiled(M, N, K, true);
+    if (c.S > 1 && !c.fix && part.numel() >= (int64_t)c.S * M * N) {
       check_dtype(x, at::kBFloat16, "x");
       check_dtype(w, at::kBFloat16, "w");
       dsse::GemmEpi ep{};
@@ -694,7 +783,10 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
                         N == (nh + 2 * nkv) * 128;
   const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
   int S = 0;
-  if (impl == 4) S = pick_tiled(M, N, K).S;
+  if (impl == 4) {
+    const TCfg c = pick_tiled(M, N, K, true);
+    S = c.fix ? 0 : c.S;  // combined in the launch: the unfused path (gemm_qkv_rope's FIX launch + attention)
+  }
   else if (impl == 3) S = pick_wide(M, N, K).S;
   else if (impl == 2) {
     S = pick_stream(M, N, K, dsse::kQkvRope).S;
@@ -730,7 +822,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   const void* X = x.data_ptr();
   float* sl = slabs.data_ptr<float>();
   if (impl == 4) {
-    const TCfg c = pick_tiled(M, N, K);
+    const TCfg c = pick_tiled(M, N, K, true);
     DSSE_CHECK_HIP(tiled_call(dsse::kQkvRope, c.cfg, S, 1, X, K, M, w.data_ptr(), K, N, &ep, sl));
   } else if (impl == 3) {
     const WCfg c = pick_wide(M, N, K);
@@ -902,7 +994,31 @@ void ar_gather(const Tensor& cand, Tensor& out, const Tensor& peers, int64_t ran
                                 reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 14; }
+int64_t kernels_abi_version() { return 15; }
+
+// The dispatch's choice for an (M, N, K) projection: (impl, tiled cfg, split, fix, model estimate in us) -- impl as
+// gemm_impl (4 = tiled / pipe); cfg / split / fix / estimate only for impl 4 (tools/bench_decode_gemm.py --plan).
+std::tuple<int64_t, int64_t, int64_t, bool, double> gemm_plan(int64_t M, int64_t N, int64_t K, bool slab_consumer) {
+  const int impl = gemm_impl((int)M, (int)N, (int)K);
+  if (impl != 4) return {impl, -1, 0, false, 0.0};
+  const TCfg c = pick_tiled((int)M, (int)N, (int)K, slab_consumer);
+  return {impl, c.cfg, c.S, c.fix, c.est_us};
+}
+
+// Stamps build: the last fix-up launch's per-workgroup phase stamps ([kStampWgs, 8] int64; empty otherwise).
+at::Tensor gemm_fix_stamps(int64_t device) {
+  const at::Device dev(at::kCUDA, (c10::DeviceIndex)device);
+  if (!DSSE_PIPE_STAMPS) return at::empty({0}, at::kLong);
+  return fix_state(dev).narrow(0, 4 + 2 * kFixTiles, kStampWgs * 16).view(at::kLong).view({kStampWgs, 8}).cpu();
+}
+
+// Timed-out waits of the in-launch split-K fix-up on `device` since load (0 unless a writer never counted itself).
+int64_t gemm_fix_timeouts(int64_t device) {
+  const at::Device dev(at::kCUDA, (c10::DeviceIndex)device);
+  int v = 0;
+  DSSE_CHECK_HIP(hipMemcpy(&v, fix_counters(dev), sizeof(int), hipMemcpyDeviceToHost));
+  return v;
+}
 
 #if DSSE_KERNEL_CHECKS
 bool kernels_checked() { return true; }
@@ -968,6 +1084,9 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_gather(Tensor cand, Tensor(a!) out, Tensor peers, int rank, int rows, int H, Tensor(b!) gepoch, "
         "Tensor(c!) err) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
+  m.def("gemm_plan(int M, int N, int K, bool slab_consumer=False) -> (int, int, int, bool, float)", &gemm_plan);
+  m.def("gemm_fix_timeouts(int device=0) -> int", &gemm_fix_timeouts);
+  m.def("gemm_fix_stamps(int device=0) -> Tensor", &gemm_fix_stamps);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
   m.def("kernel_check_files() -> str", &kernel_check_files);

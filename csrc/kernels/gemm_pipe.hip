@@ -37,8 +37,22 @@
 //     split-K partial slabs through gemm_epilogue.h.
 #include "gemm_epilogue.h"
 
+#ifndef DSSE_PIPE_STAMPS
+#define DSSE_PIPE_STAMPS 0
+#endif
+
 namespace dsse {
 namespace gp {
+
+// Diagnostic build only (_build.py variant "stamps"): workgroup-level s_memrealtime stamps (100 MHz, one clock for
+// every CU) of the FIX path's phases after the fix-up counters: [wg][8] u64 (tools/pipe_stamps.py)
+DEV void stamp(const GemmEpi& ep, int k, unsigned long long v) {
+  if constexpr (DSSE_PIPE_STAMPS) {
+    if (threadIdx.x == 0 && ep.fix_cnt)
+      reinterpret_cast<unsigned long long*>(ep.fix_cnt + 4 + 2 * kFixTiles)[(size_t)blockIdx.x * 8 + k] = v;
+  }
+}
+DEV unsigned long long now() { return DSSE_PIPE_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull; }
 
 constexpr int kA = 256 * 128;     // A image of one K step: 256 rows x 64 bf16, swizzled 16-byte pieces
 constexpr int kB = 16 * 2048;     // B image: 16 column tiles x two 1 KiB k-step blocks
@@ -63,7 +77,15 @@ DEV int a_swz(int row) { return (row >> 1) & 5; }
 // phase instead of 16, for row counts that leave a 256-row block partly empty (the mixed prefill + decode steps'
 // 320-384 rows: 192; the 161-256-row decode buckets' qkv / down: 192 / 128).  Slot row s of quadrant q, wave row wr
 // holds X row m0 + wr * BM / 2 + q * BM / 4 + s.
-template <int MODE, int BM>
+// FIX (round 6): split-K with the slices of a tile combined inside the launch, no reduce kernel and no slabs for the
+// consumer.  Ticket first: after its K loop every workgroup takes a ticket on the tile's arrival counter; the
+// first S - 1 store their fp32 accumulators (16-byte stores in the MFMA register order, 1 KiB per wave instruction,
+// read back by the same lanes) into slot `ticket` of the tile's workspace, drain, release, and count themselves
+// done (a tile's slices are adjacent in the remapped order, so they share an XCD and its L2); the workgroup that draws ticket S - 1 waits (bounded) until the others are done -- they are
+// running already and wait for nothing, so this cannot deadlock whatever the residency -- adds their slots into
+// its registers and runs the normal epilogue.  The slab round trip costs (S - 1) x the tile's fp32 bytes once, on
+// the tile's last arriver (profiles/r6/gemm_fix_r6.md).
+template <int MODE, int BM, bool FIX = false>
 __global__ void __launch_bounds__(512)
 gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
                  GemmEpi ep, float* __restrict__ part) {
@@ -72,6 +94,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int wm = w >> 2, wn = w & 3;
+  if constexpr (FIX) stamp(ep, 0, now());
 
   // ---- tile order: bijective XCD remap, then groups of 8 row blocks swept column by column (L2 panel reuse)
   constexpr int QR = BM / 4, QI = QR / 16;  // X rows per quadrant, MFMA row tiles per quadrant
@@ -80,7 +103,11 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   const int nwg = gridDim.x;
   const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rem = nwg % 8;
   const int lid = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + bid / 8;
-  const int ks = lid / ntile, tl = lid % ntile;
+  // split slices: FIX keeps a tile's S slices adjacent in the remapped order, so they run on one XCD and the last
+  // arriver reads the other slices' plain-stored slots from its own L2; the slab form (consumer-reduced) keeps
+  // them ntile apart
+  const int S_ = nwg / ntile;
+  const int ks = FIX ? lid % S_ : lid / ntile, tl = FIX ? lid / S_ : lid % ntile;
   constexpr int GM = 8;
   const int grp = tl / (GM * nbn), first = grp * GM, gsz = min(GM, nbm - first);
   const int bm = first + (tl % (GM * nbn)) % gsz, bn = (tl % (GM * nbn)) / gsz;
@@ -227,6 +254,93 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   // balance the barrier count of the two rows
   if (wm == 0) asm volatile("s_barrier" ::: "memory");
 
+  if constexpr (FIX) {
+    const int S = S_;
+    if (S > 1) {
+      constexpr int kSlotF4 = 8 * 8 * QI * 64;  // f32x4 per slot: [wave][qm][i < QI][nt][lane]
+      typedef __attribute__((address_space(1))) int gint;  // shared words: global agent-scope accesses, never flat
+      gint* cnt = (gint*)(ep.fix_cnt) + 4;   // tickets [tl], done [kFixTiles + tl]; timeouts at [0]
+      __syncthreads();  // every wave past its last LDS read: word 0 of the LDS carries the ticket
+      stamp(ep, 1, now());
+      int* sflag = reinterpret_cast<int*>(smem);
+      if (threadIdx.x == 0) sflag[0] = __hip_atomic_fetch_add(cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int ticket = __builtin_amdgcn_readfirstlane(sflag[0]);  // wave-uniform: no waterfall around the rsrc
+      stamp(ep, 2, now());
+      if constexpr (DSSE_PIPE_STAMPS) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        stamp(ep, 6, ((unsigned long long)ticket << 32) | (xcc & 0xF));
+      }
+      f32x4* slots = reinterpret_cast<f32x4*>(part) + (size_t)tl * (S - 1) * kSlotF4;
+      const int lane_off = w * (8 * QI * 64) + lane;
+      if (ticket < S - 1) {
+        // plain stores (they stay in this XCD's L2 for the same-XCD reader), every wave drained, then ONE agent-scope
+        // release and the done count (the CDNA guide's split-K recipe: fence before the count, wait after the fence)
+        f32x4* dst = slots + (size_t)ticket * kSlotF4 + lane_off;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int i = 0; i < QI; ++i)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) dst[((qm * QI + i) * 4 + nt) * 64] = acc[4 * qm + i][nt];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(ep, 3, now());
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(cnt + kFixTiles + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        stamp(ep, 4, now());
+        return;
+      }
+      if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt + kFixTiles + tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 22)) {  // ~0.1 s: a writer never counted itself (cannot happen); flag, do not hang
+            __hip_atomic_fetch_add(cnt - 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // every other slice already took its ticket and counted itself: nothing touches this pair again in
+        // this launch, so the last arriver leaves it zero for the next one
+        __hip_atomic_store(cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + kFixTiles + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stamp(ep, 3, now());
+      for (int s = 0; s < S - 1; ++s) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(slots + (size_t)s * kSlotF4, kSlotF4 * 16);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          // 2 QI accumulators in flight at once (quadrant row h / 2, column pair h % 2), then the adds
+          const int qm = h >> 1, n0 = 2 * (h & 1);
+          f32x4 t[QI][2];
+#pragma unroll
+          for (int i = 0; i < QI; ++i)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+              t[i][nt] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rs, (uint32_t)((lane_off + ((qm * QI + i) * 4 + n0 + nt) * 64) * 16), 0, 0));
+#pragma unroll
+          for (int i = 0; i < QI; ++i)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[4 * qm + i][n0 + nt] += t[i][nt];
+        }
+      }
+      if constexpr (DSSE_PIPE_STAMPS) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(ep, 4, now());
+      }
+    }
+  }
+
   // acc[4 qm + i] holds X rows row0 + QR qm + 16 i (i < QI)
   const int row0 = m0 + wm * (BM / 2), tile0 = n0 / 16 + wn * 4;
   auto mrow = [&](int mt) { return row0 + QR * (mt >> 2) + 16 * (mt & 3); };
@@ -255,6 +369,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
       const int m = row0 + QR * (rr >> 6) + (rr & 63);
       if (m < M) *reinterpret_cast<bf16x8*>(out + (size_t)m * ep.ldo + n0 + wn * 64 + ch * 8) = v;
     }
+    if constexpr (FIX) stamp(ep, 5, now());
     return;
   }
   if constexpr (MODE == kSiluMul) {
@@ -263,6 +378,7 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         if ((mt & 3) < QI) silu_epilogue4(ep, M, mrow(mt) + 4 * g, tile0 + nt, r, acc[mt][nt]);
+    if constexpr (FIX) stamp(ep, 5, now());
     return;
   }
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
@@ -280,33 +396,34 @@ gemm_pipe_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   }
 }
 
-template <int MODE, int BM>
+template <int MODE, int BM, bool FIX>
 static hipError_t launch_pipe_bm(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                                  float* part, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<MODE, BM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pipe_kernel<MODE, BM, FIX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)gp::kLDS);
     attr_set = true;
   }
   const int nbm = (M + BM - 1) / BM, nbn = N / 256;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, BM>), dim3(nbm * nbn * S), dim3(512), gp::kLDS, st, X, ldx, M, W, K, N,
-                     K / S, ep, part);
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, BM, FIX>), dim3(nbm * nbn * S), dim3(512), gp::kLDS, st, X, ldx, M, W, K,
+                     N, K / S, ep, part);
   return hipGetLastError();
 }
-template <int MODE>
+template <int MODE, bool FIX = false>
 static hipError_t launch_pipe(int bm, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
                               const GemmEpi& ep, float* part, hipStream_t st) {
-  if (bm == 128) return launch_pipe_bm<MODE, 128>(X, ldx, M, W, K, N, S, ep, part, st);
-  return bm == 192 ? launch_pipe_bm<MODE, 192>(X, ldx, M, W, K, N, S, ep, part, st)
-                   : launch_pipe_bm<MODE, 256>(X, ldx, M, W, K, N, S, ep, part, st);
+  if (bm == 128) return launch_pipe_bm<MODE, 128, FIX>(X, ldx, M, W, K, N, S, ep, part, st);
+  return bm == 192 ? launch_pipe_bm<MODE, 192, FIX>(X, ldx, M, W, K, N, S, ep, part, st)
+                   : launch_pipe_bm<MODE, 256, FIX>(X, ldx, M, W, K, N, S, ep, part, st);
 }
 
 }  // namespace dsse
 
 // Shape contract (checked here): N % 256 == 0, K % (128 S) == 0 (>= 2 K steps of 64 per slice), the tiled weight
-// layout (api.h), X rows of ldx >= K elements.  S > 1: fp32 slabs [S, M, N] into `part`, reduced by
-// launch_splitk_reduce unless partial_only.
+// layout (api.h), X rows of ldx >= K elements.  S > 1: partial_only 0 = fp32 slabs [S, M, N] into `part` reduced by
+// launch_splitk_reduce, 1 = the slabs only (the consumer reduces them), 2 = in-launch fix-up (FIX above): `part`
+// holds dsse_gemm_pipe_fix_floats() floats and ep->fix_cnt the counters (api.h), tiles <= kFixTiles.
 extern "C" hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M,
                                      const void* W, int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st) {
   using namespace dsse;
@@ -324,7 +441,24 @@ extern "C" hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, 
     }
     return hipErrorInvalidValue;
   }
+  if (partial_only == 2) {
+    if (ep->fix_cnt == nullptr || (size_t)((M + bm - 1) / bm) * (N / 256) > (size_t)kFixTiles) return hipErrorInvalidValue;
+    switch (mode) {
+      case kStoreBf16: return launch_pipe<kStoreBf16, true>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
+      case kStoreF32: return launch_pipe<kStoreF32, true>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
+      case kResidAdd: return launch_pipe<kResidAdd, true>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
+      case kSiluMul: return launch_pipe<kSiluMul, true>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
+      case kQkvRope: return launch_pipe<kQkvRope, true>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
+    }
+    return hipErrorInvalidValue;
+  }
   hipError_t e = launch_pipe<kPartial>(bm, x, ldx, M, w, K, N, S, *ep, part, st);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
+}
+
+// Workspace floats of the in-launch fix-up (partial_only = 2): S - 1 register-order slots per tile.
+extern "C" size_t dsse_gemm_pipe_fix_floats(int bm, int S, int M, int N) {
+  const int nbm = (M + bm - 1) / bm, qi = bm / 64;
+  return (size_t)nbm * (N / 256) * (S - 1) * (8 * 8 * qi * 64) * 4;
 }

@@ -71,6 +71,7 @@ def _parallel(jobs, verbose):
 KERNEL_VARIANTS = {
     "checked": ["-DDSSE_KERNEL_CHECKS=1"],  # device index-check debug build (tools/check_kernels.py)
     "burst": ["-DDSSE_TILED_BURST=1"],  # A/B build: gemm_tiled issues each stage's DMA in one burst
+    "stamps": ["-DDSSE_PIPE_STAMPS=1"],  # diagnostic build: gemm_pipe FIX phase stamps (tools/pipe_stamps.py)
 }  # libdsse_kernels_<variant>.so, selected at import with DSSE_KERNELS_VARIANT
 
 

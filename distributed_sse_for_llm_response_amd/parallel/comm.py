@@ -64,6 +64,33 @@ class TPComm:
         else:
             out.copy_(inp.view(-1)[: out.numel()].view_as(out))
 
+    def reduce_scatter_rows(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out = rows [rank * n, (rank + 1) * n) of the sum over ranks of inp ([size * n, ...] -> [n, ...]): the
+        first half of a ring all-reduce, so the caller can normalise only its own rows (TP prefill)."""
+        if self.size == 1:
+            out.copy_(inp)
+            return
+        if self._host_staged(inp):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.reduce_scatter_tensor(h, inp.contiguous().cpu(), group=self.group)
+            out.copy_(h)
+            return
+        dist.reduce_scatter_tensor(out, inp.contiguous(), group=self.group)
+
+    def all_gather_rows(self, out: torch.Tensor, own: torch.Tensor) -> None:
+        """out ([size * n, ...], contiguous) = every rank's `own` rows in rank order; `own` may be this rank's slice
+        of `out` itself (in place)."""
+        if self.size == 1:
+            if own.data_ptr() != out.data_ptr():
+                out.copy_(own)
+            return
+        if self._host_staged(out):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(h, own.contiguous().cpu(), group=self.group)
+            out.copy_(h)
+            return
+        dist.all_gather_into_tensor(out, own.contiguous(), group=self.group)
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         if self.size > 1:
             dist.broadcast(t, src=src, group=self.group)

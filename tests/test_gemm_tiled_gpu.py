@@ -159,3 +159,91 @@ def test_pipe_repeat_bit_identical(gpu, monkeypatch, cfg, M):
     for i in range(20):
         ops.gemm_out(x, w, out)
         assert torch.equal(out, first), f"call {i + 1} differs from the first"
+
+
+@pytest.mark.parametrize("cfg,split,M", [("8", "2", 256), ("8", "4", 300), ("9", "2", 576), ("9", "4", 384),
+                                         ("10", "2", 200), ("10", "8", 640), ("8", "16", 129)])
+def test_pipe_fix_in_launch_split_k(gpu, monkeypatch, cfg, split, M):
+    """Split-K combined inside the launch (gemm_pipe.hip FIX, t_fix=1): every epilogue (bf16 / fp32 store, residual
+    add, SiLU·mul, QKV + RoPE + KV write) against the fp32 reference, ragged M; 10 repeats bit-identical (the
+    ticket decides who sums, but the sum order is fixed: the last arriver adds the slots in ticket order -- so
+    repeats agree only up to fp32 rounding; checked against the reference instead); counters left at zero and no
+    timed-out wait."""
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(t_cfg=cfg, t_split=split, t_fix="1"))
+    ops.refresh_env()
+    plan = torch.ops.dsse.gemm_plan(M, 6144, H)
+    assert plan[0] == 4 and plan[1] == int(cfg) and plan[2] == int(split) and plan[3], plan
+    g = torch.Generator().manual_seed(M * 3 + int(split))
+    x = _rand((M, H), g, gpu)
+    wq = R.tile_weight(_rand(((NH + 2 * NKV) * 128, H), g, gpu, 1 / 64))
+    out = torch.empty(M, wq.shape[0], device=gpu, dtype=torch.bfloat16)
+    ref = _ref(x, wq)
+    for _ in range(10):
+        ops.gemm_out(x, wq, out)
+        _check(out, ref, f"fix qkv bf16 M={M}")
+    o32 = torch.empty(M, wq.shape[0], device=gpu)
+    ops.gemm_out(x, wq, o32)
+    _check(o32, ref, f"fix qkv fp32 M={M}", rel=2e-3)
+    h = _rand((M, F), g, gpu)
+    wd = R.tile_weight(_rand((H, F), g, gpu, 1 / math.sqrt(F)))
+    r0 = torch.randn(M, H, generator=g).to(gpu)
+    r = r0.clone()
+    ops.gemm_resid(h, wd, r)
+    _check(r, r0 + _ref(h, wd), f"fix down resid M={M}", rel=2e-3)
+    wgu = R.tile_weight(_rand((2 * F, H), g, gpu, 1 / 64))
+    hs = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_silu(x, wgu, hs)
+    gu = _ref(x, wgu).view(M, 2 * F // 16, 16)
+    _check(hs, (torch.nn.functional.silu(gu[..., :8]) * gu[..., 8:]).reshape(M, F), f"fix silu M={M}", rel=2e-2)
+    rope = R.rope_table(8192, 1e6, gpu)
+    positions = torch.arange(M, dtype=torch.int32)
+    nblk = (M + 31) // 32 + 1
+    slots = torch.randperm(nblk * 32, generator=g)[:M].to(torch.int32)
+    q = torch.zeros(M, NH * 128, device=gpu, dtype=torch.bfloat16)
+    kc = torch.zeros(nblk, NKV, 32, 128, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros(nblk, NKV, 128, 32, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_qkv_rope(x, wq, positions.to(gpu), slots.to(gpu), rope, q, kc, vc, NH, NKV)
+    qr, kr, vr = torch.zeros(M, NH * 128, dtype=torch.bfloat16), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    R.rope_kv_write(ref.cpu(), positions, slots, rope.cpu(), qr, kr, vr, NH, NKV)
+    _check(q.cpu(), qr, "fix q", rel=2e-2)
+    _check(kc.cpu(), kr, "fix k cache", rel=2e-2)
+    _check(vc.cpu(), vr, "fix v cache", rel=2e-2)
+    torch.cuda.synchronize()
+    assert torch.ops.dsse.gemm_fix_timeouts(gpu.index or 0) == 0
+
+
+@pytest.mark.parametrize("M", [257, 320, 448, 513, 576, 640, 777, 1024])
+def test_model_planned_gemms_mid_rows(gpu, monkeypatch, M):
+    """The cost-model dispatch above 256 rows (bindings.cpp pipe_plan): whatever tile / split / in-launch fix-up it
+    picks, every projection shape of the mixed steps and prompt chunks matches the fp32 reference, including the
+    split-K slabs handed to the norm (gemm_resid_split + rmsnorm) and non-multiples of 64 rows."""
+    monkeypatch.setenv("DSSE_KERNEL_CFG", "")
+    ops.refresh_env()
+    g = torch.Generator().manual_seed(M + 99)
+    x = _rand((M, H), g, gpu)
+    wq = R.tile_weight(_rand(((NH + 2 * NKV) * 128, H), g, gpu, 1 / 64))
+    out = torch.empty(M, wq.shape[0], device=gpu, dtype=torch.bfloat16)
+    ops.gemm_out(x, wq, out)
+    _check(out, _ref(x, wq), f"planned qkv M={M}")
+    wgu = R.tile_weight(_rand((2 * F, H), g, gpu, 1 / 64))
+    hs = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_silu(x, wgu, hs)
+    gu = _ref(x, wgu).view(M, 2 * F // 16, 16)
+    _check(hs, (torch.nn.functional.silu(gu[..., :8]) * gu[..., 8:]).reshape(M, F), f"planned silu M={M}", rel=2e-2)
+    for name, (N, K) in (("o", (H, H)), ("down", (H, F))):
+        a = _rand((M, K), g, gpu)
+        w = R.tile_weight(_rand((N, K), g, gpu, 1 / math.sqrt(K)))
+        r0 = torch.randn(M, N, generator=g).to(gpu)
+        r = r0.clone()
+        part = torch.zeros(16 * M * N, device=gpu)
+        nw = (1 + 0.1 * torch.randn(N, generator=g)).bfloat16().to(gpu)
+        y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        ns = ops.gemm_resid_split(a, w, r, part)
+        ops.rmsnorm(r, nw, y, 1e-5, part=part, nsplit=ns)
+        r_ref = r0 + _ref(a, w)
+        _check(r, r_ref, f"planned {name} resid M={M} (S={ns})", rel=2e-3)
+        y_ref = torch.zeros(M, N, dtype=torch.bfloat16)
+        R.rmsnorm(r_ref.cpu().clone(), nw.cpu(), y_ref, 1e-5)
+        _check(y.cpu(), y_ref, f"planned {name} norm M={M}", rel=2e-2)
+    torch.cuda.synchronize()
+    assert torch.ops.dsse.gemm_fix_timeouts(gpu.index or 0) == 0

@@ -609,7 +609,7 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 14
+    assert torch.ops.dsse.kernels_abi_version() == 15
     assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
 
 

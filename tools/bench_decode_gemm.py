@@ -95,8 +95,11 @@ def main():
                         e1.record()
                         torch.cuda.synchronize()
                         best = min(best, e0.elapsed_time(e1) * 1e3 / ncopy)
+                    impl, cfg_, S_, fix_, est = torch.ops.dsse.gemm_plan(M, N, K, op == "split_norm")
+                    plan = f"impl {impl} cfg {cfg_} S {S_}{' fix' if fix_ else ''} est {est:6.1f}" if impl == 4 else \
+                        f"impl {impl}"
                     print(f"{shape:8s} M={M:4d} {var:40s} {best:8.2f} us/call  {N * K * 2 / best / 1e6:6.2f} TB/s "
-                          f"{2 * M * N * K / best / 1e6:7.1f} TF/s", flush=True)
+                          f"{2 * M * N * K / best / 1e6:7.1f} TF/s  [{plan}]", flush=True)
                     del graph
                 except Exception as e:  # noqa: BLE001 - report and go on with the next variant
                     print(f"{shape:8s} M={M:4d} {var:40s} FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)

@@ -1,4 +1,6 @@
-// Per-CU fill-rate microbenchmark (round 3): how many bytes per second one CU can bring on chip, by path.
+// Per-CU fill-rate microbenchmark (round 3; round 6: 4 or 8 waves per workgroup, up to 32 KiB in flight per wave,
+// X footprints of 2 MiB (one XCD's L2) and 8 MiB (spills the 4 MiB L2 into the Infinity Cache)): how many bytes
+// per second one CU can bring on chip, by path.
 //
 // The decode GEMMs at 64-256 rows all measured ~35-39 GB/s of LDS-DMA fill per CU (gemm_ring at 64 rows,
 // gemm_tiled at 256 rows and at 8192 rows alike: profiles/r3/fillbench.md), which bounds them whatever the
@@ -36,31 +38,35 @@ __device__ __forceinline__ void glds(const void* src, char* lds) {
 
 template <int D>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (D >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  if constexpr (D >= 32) asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
+  else if constexpr (D >= 24) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+  else if constexpr (D >= 16) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  else if constexpr (D >= 12) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
   else if constexpr (D == 8) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
   else if constexpr (D == 4) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   else if constexpr (D == 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// iters: 1-KiB pieces per loading wave
-template <int MODE, int D>
-__global__ void __launch_bounds__(256) fill_kernel(const char* __restrict__ x, const char* __restrict__ w,
-                                                   size_t w_per_wg, int iters, unsigned* __restrict__ sink) {
+// iters: 1-KiB pieces per loading wave.  NW waves per workgroup; in the mixed modes the first half of the waves load
+// X, the second half W.  XB: the X buffer's bytes (every workgroup sweeps all of it, so it stays cached).
+template <int MODE, int D, int NW>
+__global__ void __launch_bounds__(512) fill_kernel(const char* __restrict__ x, const char* __restrict__ w,
+                                                   size_t w_per_wg, int iters, size_t xb, unsigned* __restrict__ sink) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool x_role = MODE == 0 || ((MODE == 3 || MODE == 4) && wave < 2);
-  const bool w_vgpr = MODE == 1 || (MODE == 3 && wave >= 2);
-  const bool w_lds = MODE == 2 || (MODE == 4 && wave >= 2);
-  const int nw = (MODE >= 3) ? 2 : 4;  // waves per role
-  const int rw = (MODE >= 3) ? (wave & 1) : wave;
+  const bool mixed = MODE == 3 || MODE == 4;
+  const bool x_role = MODE == 0 || (mixed && wave < NW / 2);
+  const bool w_vgpr = MODE == 1 || (MODE == 3 && wave >= NW / 2);
+  const bool w_lds = MODE == 2 || (MODE == 4 && wave >= NW / 2);
+  const int nw = mixed ? NW / 2 : NW;  // waves per role
+  const int rw = mixed ? (wave % (NW / 2)) : wave;
   unsigned acc = 0;
   char* ring = smem + wave * (D * 1024);
   if (x_role) {
-    // 2 MiB source: pieces spread over it by workgroup and wave (L2-resident after the first pass)
-    const size_t start = ((size_t)blockIdx.x * 4 + wave) * 4096;
+    const size_t start = ((size_t)blockIdx.x * NW + wave) * 4096;
     for (int i = 0; i < iters; ++i) {
-      const size_t off = (start + (size_t)i * 1024) % (2u << 20);  // 1-KiB aligned, inside the 2 MiB buffer
+      const size_t off = (start + (size_t)i * 1024) % xb;  // 1-KiB aligned, inside the X buffer
       glds(x + off + lane * 16, ring + (i % D) * 1024);
       wait_vm<D>();
     }
@@ -93,62 +99,67 @@ __global__ void __launch_bounds__(256) fill_kernel(const char* __restrict__ x, c
   if (acc == 0x12345678u) sink[0] = acc;  // keeps the loads
 }
 
-template <int MODE, int D>
-double run(const char* x, const char* w, int iters, unsigned* sink, int reps, double* bytes_out) {
+template <int MODE, int D, int NW>
+double run(const char* x, const char* w, int iters, size_t xb, unsigned* sink, int reps, double* bytes_out) {
   const int grid = 256;
-  const size_t lds = 4 * D * 1024;
-  const int nw = MODE >= 3 ? 2 : 4;
+  const size_t lds = (size_t)NW * D * 1024;
+  const int nw = (MODE == 3 || MODE == 4) ? NW / 2 : NW;
   const size_t w_per_wg = (size_t)iters * nw * 1024;
-  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fill_kernel<MODE, D>),
+  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fill_kernel<MODE, D, NW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  fill_kernel<MODE, D><<<grid, 256, lds>>>(x, w, w_per_wg, iters, sink);  // warm
+  fill_kernel<MODE, D, NW><<<grid, NW * 64, lds>>>(x, w, w_per_wg, iters, xb, sink);  // warm
   CHECK(hipDeviceSynchronize());
   CHECK(hipEventRecord(a));
-  for (int r = 0; r < reps; ++r) fill_kernel<MODE, D><<<grid, 256, lds>>>(x, w, w_per_wg, iters, sink);
+  for (int r = 0; r < reps; ++r) fill_kernel<MODE, D, NW><<<grid, NW * 64, lds>>>(x, w, w_per_wg, iters, xb, sink);
   CHECK(hipEventRecord(b));
   CHECK(hipEventSynchronize(b));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, a, b));
-  // bytes per kernel: every wave moves iters KiB
-  *bytes_out = (double)grid * 4 * iters * 1024;
+  *bytes_out = (double)grid * NW * iters * 1024;  // every wave moves iters KiB
   return ms / reps;
 }
 
-template <int MODE, int D>
-void report(const char* name, const char* x, const char* w, int iters, unsigned* sink) {
+template <int MODE, int D, int NW>
+void report(const char* name, const char* x, const char* w, size_t xb, unsigned* sink) {
+  static_assert((size_t)NW * D <= 160, "LDS");
   double bytes = 0;
-  const double ms = run<MODE, D>(x, w, iters, sink, 10, &bytes);
+  // the W modes stream 2 GiB per kernel: 256 WG x NW waves x iters KiB
+  const int iters = 8192 / NW;
+  const double ms = run<MODE, D, NW>(x, w, iters, xb, sink, 10, &bytes);
   const double gbs = bytes / (ms * 1e-3) / 1e9;
-  printf("%-44s D=%2d  %8.3f ms  chip %7.1f GB/s  per CU %6.1f GB/s\n", name, D, ms, gbs, gbs / 256);
+  printf("%-44s NW=%d D=%2d X=%zu MiB  %8.3f ms  chip %7.1f GB/s  per CU %6.1f GB/s\n", name, NW, D, xb >> 20, ms, gbs,
+         gbs / 256);
   fflush(stdout);
 }
 
 int main() {
   char *x = nullptr, *w = nullptr;
   unsigned* sink = nullptr;
-  const size_t wbytes = (size_t)2 << 30;
-  CHECK(hipMalloc(&x, 2u << 20));
+  const size_t wbytes = (size_t)2 << 30, xmax = (size_t)8 << 20;
+  CHECK(hipMalloc(&x, xmax));
   CHECK(hipMalloc(&w, wbytes));
   CHECK(hipMalloc(&sink, 64));
-  CHECK(hipMemset(x, 1, 2u << 20));
+  CHECK(hipMemset(x, 1, xmax));
   CHECK(hipMemset(w, 2, wbytes));
-  // iters so that the W modes stream 2 GiB / (4 waves) per kernel: 256 WG x 4 waves x iters KiB = 2 GiB -> 2048
-  const int iters = 2048;
-  report<0, 4>("X  LDS-DMA, L2-resident", x, w, iters, sink);
-  report<0, 8>("X  LDS-DMA, L2-resident", x, w, iters, sink);
-  report<0, 16>("X  LDS-DMA, L2-resident", x, w, iters, sink);
-  report<1, 4>("W  global_load->VGPR nt, HBM", x, w, iters, sink);
-  report<1, 8>("W  global_load->VGPR nt, HBM", x, w, iters, sink);
-  report<1, 16>("W  global_load->VGPR nt, HBM", x, w, iters, sink);
-  report<2, 4>("W  buffer_load lds nt, HBM", x, w, iters, sink);
-  report<2, 8>("W  buffer_load lds nt, HBM", x, w, iters, sink);
-  report<2, 16>("W  buffer_load lds nt, HBM", x, w, iters, sink);
-  report<3, 8>("X LDS-DMA (2 waves) + W->VGPR (2 waves)", x, w, iters, sink);
-  report<3, 16>("X LDS-DMA (2 waves) + W->VGPR (2 waves)", x, w, iters, sink);
-  report<4, 8>("X LDS-DMA (2 waves) + W LDS-DMA (2 waves)", x, w, iters, sink);
-  report<4, 16>("X LDS-DMA (2 waves) + W LDS-DMA (2 waves)", x, w, iters, sink);
+  const size_t x2 = 2u << 20, x8 = xmax;
+  report<0, 4, 4>("X  LDS-DMA", x, w, x2, sink);
+  report<0, 16, 4>("X  LDS-DMA", x, w, x2, sink);
+  report<0, 8, 8>("X  LDS-DMA", x, w, x2, sink);
+  report<0, 16, 8>("X  LDS-DMA", x, w, x2, sink);
+  report<0, 16, 8>("X  LDS-DMA", x, w, x8, sink);
+  report<2, 8, 4>("W  buffer_load lds nt, HBM", x, w, x2, sink);
+  report<2, 16, 4>("W  buffer_load lds nt, HBM", x, w, x2, sink);
+  report<2, 8, 8>("W  buffer_load lds nt, HBM", x, w, x2, sink);
+  report<2, 16, 8>("W  buffer_load lds nt, HBM", x, w, x2, sink);
+  report<1, 16, 4>("W  global_load->VGPR nt, HBM", x, w, x2, sink);
+  report<4, 16, 4>("X LDS-DMA + W LDS-DMA (half the waves each)", x, w, x2, sink);
+  report<4, 8, 8>("X LDS-DMA + W LDS-DMA (half the waves each)", x, w, x2, sink);
+  report<4, 16, 8>("X LDS-DMA + W LDS-DMA (half the waves each)", x, w, x2, sink);
+  report<4, 20, 8>("X LDS-DMA + W LDS-DMA (half the waves each)", x, w, x2, sink);
+  report<4, 16, 8>("X LDS-DMA + W LDS-DMA (half the waves each)", x, w, x8, sink);
+  report<3, 16, 8>("X LDS-DMA + W->VGPR (half the waves each)", x, w, x2, sink);
   return 0;
 }
