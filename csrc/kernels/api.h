@@ -111,6 +111,10 @@ hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);
 hipError_t dsse_sample_pick(int B, int world, const void* cand, const dsse::SampleParams* p,
                             hipStream_t st);
+hipError_t dsse_prefill_sample_gather(const void* x, int T, int H, const int* meta, int NS, const int* slot_meta, int Bm,
+                                      void* xl, int* smeta, hipStream_t st);
+hipError_t dsse_prefill_sample_commit(const int* meta, int NS, const int* new_ids, int* ids, int Bm, int* ring, int R,
+                                      int* positions, hipStream_t st);
 hipError_t dsse_rmsnorm(int mode, int M, float* resid, int H, const void* delta, const void* embed,
                         const int* ids, const void* w, void* y, float eps, const float* part, int nsplit,
                         int vocab, hipStream_t st);

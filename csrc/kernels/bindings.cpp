@@ -263,30 +263,34 @@ struct TCfg {
   double est_us = 0;   // the cost model's estimate (pipe_plan), 0 for the table's choices
 };
 
-// Cost model of one gemm_pipe launch (round 6, profiles/r6/gemm_model_r6.md), from the per-CU rates the pipe kernel
-// reaches on MI355X: a workgroup is bound by its LDS fill (X rows from L2 + weight rows, ~46 GB/s per CU when both
-// streams mix: tools/fillbench.hip, profiles/r6/fillbench_r6.log) or by its MFMA issue (~5.5 TFLOP/s per CU, the
-// kernel's 1.4 PFLOP/s at 8192 rows), plus ~3 us of pipeline fill and epilogue.  One 128 KiB workgroup per CU, so
-// the grid runs in ceil(WGs / 256) rounds of equal workgroups.  Split K costs the fp32 slabs: in-launch (fix) the
-// S - 1 slots of a tile are written by the first arrivers and read by the last (~60 GB/s per CU each way, on the
-// critical path once); left to a consumer (the norm / attention kernel) one slab write per workgroup plus the
-// consumer's read of S x M x N x 4 bytes at HBM rate.
-double pipe_est_us(int M, int N, int K, int bm, int S, bool fix) {
-  constexpr double kFill = 46e3, kMfma = 5.5e6, kT0 = 3.0, kSlot = 60e3, kHbm = 6.0e6, kCUs = 256;
-  const int nbm = (M + bm - 1) / bm, rows = std::min(bm, M), Kr = K / S;
-  const double wgs = (double)nbm * (N / 256) * S;
-  const double bytes = (double)(rows + 256) * Kr * 2, flops = 2.0 * bm * 256 * Kr;
-  const double t_wg = kT0 + std::max(bytes / kFill, flops / kMfma);
-  double t = std::ceil(wgs / kCUs) * t_wg;
+// Cost model of one gemm_pipe launch (round 6, profiles/r6/gemm_model_r6.md).  A workgroup is bound by its LDS
+// fill (X rows + weight rows through LDS-DMA: ~44 GB/s per CU when the L2 and HBM streams mix -- the 8-wave,
+// 32 KiB-in-flight fillbench tops out there too, profiles/r6/fillbench_r6.log) or by its MFMA issue (~5.0 TFLOP/s
+// per CU, the kernel's rate at 8192 rows), plus ~3.3 us of pipeline fill and epilogue; one 128 KiB workgroup per CU,
+// so the grid runs in rounds of 256, a partial last round at 0.67 + 0.33 x its fill of a full one's time.  Split K
+// costs the fp32 partial tiles: combined in the launch (FIX) ~7 us of store / release / wait plus the last arriver
+// reading S - 1 slots at ~26 GB/s (the stamps of profiles/r6/pipe_fix_stamps_r6.log), or left as slabs for the
+// next kernel (the norm or attention consumer, else splitk_reduce) that reads S x M x N x 4 bytes at ~4.5 TB/s
+// after ~5.7 us.  Constants least-squares fitted to 238 measured launches at 192-1024 rows (12 % rms error).
+double pipe_est_us(int M, int N, int K, int bm, int S, bool fix, int out_bytes = 0) {
+  constexpr double kFill = 43.76e3, kMfma = 5.006e6, kT0 = 3.35, kPartial = 0.666, kSlotRead = 26.48e3,
+                   kFixSync = 7.06, kNext = 5.68, kHbm = 4.458e6, kCUs = 256;
+  const int nbm = (M + bm - 1) / bm, rows = std::min(bm, M);
+  const double Kr = (double)K / S;
+  const long wgs = (long)nbm * (N / 256) * S;
+  const long full = wgs / (long)kCUs, rem = wgs - full * (long)kCUs;
+  const double t_wg = kT0 + std::max((double)(rows + 256) * Kr * 2 / kFill, 2.0 * bm * 256 * Kr / kMfma);
+  double t = full * t_wg + (rem ? t_wg * (kPartial + (1 - kPartial) * rem / kCUs) : 0.0);
   if (S > 1) {
     const double slot = (double)bm * 256 * 4;
-    t += fix ? S * slot / kSlot : slot / kSlot + (double)S * M * N * 4 / kHbm;
+    t += fix ? kFixSync + (S - 1) * slot / kSlotRead : kNext + ((double)S * M * N * 4 + (double)M * N * out_bytes) / kHbm;
   }
   return t;
 }
 
-// Best gemm_pipe configuration by the model: tile 256 / 192 / 128 rows x split 1-16, combined in the launch or (when
-// `slab_consumer`, the caller reduces fp32 slabs in its next kernel) left as slabs.
+// Best gemm_pipe configuration by the model: tile 256 / 192 / 128 rows x split 1-16, slices combined in the launch
+// (fix) or left as fp32 slabs -- for the caller's next kernel when `slab_consumer` (norm, attention), else for
+// splitk_reduce (which also writes the bf16 output: counted).
 TCfg pipe_plan(int M, int N, int K, bool slab_consumer) {
   TCfg best{};
   best.ok = false;
@@ -296,9 +300,8 @@ TCfg pipe_plan(int M, int N, int K, bool slab_consumer) {
       if (K % (128 * S) != 0) break;
       for (int fix = 0; fix < 2; ++fix) {
         if (S == 1 && fix) continue;
-        if (S > 1 && !fix && !slab_consumer) continue;
         if (fix && (tiles > dsse::kFixTiles || (double)tiles * (S - 1) * bm * 256 * 4 > (1u << 30))) continue;
-        const double t = pipe_est_us(M, N, K, bm, S, fix);
+        const double t = pipe_est_us(M, N, K, bm, S, fix, slab_consumer ? 0 : 2);
         if (!best.ok || t < best.est_us * 0.98) {  // ties: the simpler (earlier) form
           best.ok = true;
           best.est_us = t;
@@ -926,6 +929,36 @@ void sample_pick(const Tensor& cand_all, const c10::optional<Tensor>& active, Te
   DSSE_CHECK_HIP(dsse_sample_pick(B, world, cand_all.data_ptr(), &p, cur_stream()));
 }
 
+// First-token sampling inside the captured prefill / mixed graphs (sampler.hip prefill_sample_*): gather the
+// finishing prompts' last rows + their slots' sampling parameters, then (after the LM head, candidates and pick)
+// commit ids / ring / positions.  meta: int32 [3 NS + 2]; smeta: int32 [7 NS]; slot_meta: the runner's [6 Bm].
+void prefill_sample_gather(const Tensor& x, const Tensor& meta, const Tensor& slot_meta, Tensor& xl, Tensor& smeta) {
+  for (const Tensor* t : {&x, &meta, &slot_meta, (const Tensor*)&xl, (const Tensor*)&smeta})
+    check_gpu(*t, "prefill_sample_gather operand");
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(xl, at::kBFloat16, "xl");
+  for (const Tensor* t : {&meta, &slot_meta, (const Tensor*)&smeta}) check_dtype(*t, at::kInt, "metadata");
+  TORCH_CHECK(x.dim() == 2 && xl.dim() == 2 && xl.size(1) == x.size(1) && x.size(1) % 8 == 0, "x / xl shapes");
+  const int NS = (int)xl.size(0), Bm = (int)(slot_meta.numel() / 6);
+  TORCH_CHECK(meta.numel() >= 3 * NS + 2 && smeta.numel() >= 7 * NS && slot_meta.numel() == 6 * Bm, "metadata sizes");
+  DSSE_CHECK_HIP(dsse_prefill_sample_gather(x.data_ptr(), (int)x.size(0), (int)x.size(1), meta.data_ptr<int>(), NS,
+                                            slot_meta.data_ptr<int>(), Bm, xl.data_ptr(), smeta.data_ptr<int>(),
+                                            cur_stream()));
+}
+
+void prefill_sample_commit(const Tensor& meta, const Tensor& new_ids, Tensor& ids, Tensor& ring, Tensor& positions) {
+  for (const Tensor* t : {&meta, &new_ids, (const Tensor*)&ids, (const Tensor*)&ring, (const Tensor*)&positions}) {
+    check_gpu(*t, "prefill_sample_commit operand");
+    check_dtype(*t, at::kInt, "int32 operand");
+  }
+  const int NS = (int)new_ids.numel(), Bm = (int)ids.numel();
+  TORCH_CHECK(NS <= 64 && meta.numel() >= 3 * NS + 2, "meta too short / NS > 64");
+  TORCH_CHECK(ring.dim() == 2 && ring.size(1) == Bm && positions.numel() == Bm, "ring must be [R, Bm], positions [Bm]");
+  DSSE_CHECK_HIP(dsse_prefill_sample_commit(meta.data_ptr<int>(), NS, new_ids.data_ptr<int>(), ids.data_ptr<int>(), Bm,
+                                            ring.data_ptr<int>(), (int)ring.size(0), positions.data_ptr<int>(),
+                                            cur_stream()));
+}
+
 // ---- TP all-reduce over IPC peer buffers (allreduce.hip) ------------------------------------------------------
 // ar_alloc: this rank's zeroed buffer for `rows` decode rows of width H -> (64-byte IPC handle as uint8 [64],
 // device pointer, uncached flag).  ar_open: a peer's handle -> its pointer in this process.  The buffers live
@@ -1076,6 +1109,8 @@ TORCH_LIBRARY(dsse, m) {
         "Tensor positions, Tensor? active, Tensor(a!) cand, int vocab_offset=0) -> ()");
   m.def("sample_pick(Tensor cand_all, Tensor? active, Tensor(a!) next_ids, Tensor(b!)? ring=None, "
         "Tensor? ring_counter=None, Tensor(c!)? positions_inc=None, int vocab=2147483647) -> ()");
+  m.def("prefill_sample_gather(Tensor x, Tensor meta, Tensor slot_meta, Tensor(a!) xl, Tensor(b!) smeta) -> ()");
+  m.def("prefill_sample_commit(Tensor meta, Tensor new_ids, Tensor(a!) ids, Tensor(b!) ring, Tensor(c!) positions) -> ()");
   m.def("ar_alloc(int rows, int H) -> (Tensor, int, int)", &ar_alloc);
   m.def("ar_open(Tensor handle) -> int", &ar_open);
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
@@ -1107,6 +1142,8 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);
+  m.impl("prefill_sample_gather", &prefill_sample_gather);
+  m.impl("prefill_sample_commit", &prefill_sample_commit);
   m.impl("ar_rmsnorm", &ar_rmsnorm);
   m.impl("ar_gather", &ar_gather);
 }

@@ -185,7 +185,67 @@ __global__ void sample_pick_kernel(const float2* __restrict__ cand, int world, i
   if (p.positions_inc) p.positions_inc[b] += 1;
 }
 
+// First-token sampling of the prompts a captured prefill / mixed graph finishes (round 6: inside the graph, no torch
+// index kernels).  meta = [rows[NS] | slots[NS] | last_pos[NS] | n | ring_row] (uploaded with the graph's other
+// metadata); slot_meta = the runner's per-slot sampling state [active | temperature | top_k | top_p | seeds x 2]
+// (Bm each).  Gather: row i < n of xl = x[rows[i]] (zeros for i >= n) and the sampling parameters of slots[i] into
+// smeta = [active | temperature | top_k | top_p | seeds x 2 | position] (NS each; active = i < n).
+__global__ void __launch_bounds__(256)
+prefill_sample_gather_kernel(const bf16* __restrict__ x, int T, int H, const int* __restrict__ meta, int NS,
+                             const int* __restrict__ slot_meta, int Bm, bf16* __restrict__ xl, int* __restrict__ smeta) {
+  const int i = blockIdx.x;
+  const int n = meta[3 * NS];
+  const bool on = i < n;
+  const int row = on ? DSSE_IDX(meta[i], T, 0) : 0;
+  const int H8 = H / 8;
+  for (int c = threadIdx.x; c < H8; c += blockDim.x) {
+    const bf16x8 v = on ? *reinterpret_cast<const bf16x8*>(x + (size_t)row * H + 8 * c) : zero_bf16x8();
+    *reinterpret_cast<bf16x8*>(xl + (size_t)i * H + 8 * c) = v;
+  }
+  if (threadIdx.x == 0) {
+    const int slot = on ? DSSE_IDX(meta[NS + i], Bm, 0) : 0;
+    smeta[i] = on ? 1 : 0;
+    smeta[NS + i] = slot_meta[Bm + slot];          // temperature (bits)
+    smeta[2 * NS + i] = slot_meta[2 * Bm + slot];  // top_k
+    smeta[3 * NS + i] = slot_meta[3 * Bm + slot];  // top_p (bits)
+    smeta[4 * NS + 2 * i] = slot_meta[4 * Bm + 2 * slot];
+    smeta[4 * NS + 2 * i + 1] = slot_meta[4 * Bm + 2 * slot + 1];
+    smeta[6 * NS + i] = on ? meta[2 * NS + i] : 0;  // the sampled token's predecessor position (RNG counter)
+  }
+}
+
+// Commit the picked first tokens: ids[slot], ring[ring_row][slot], positions[slot] = last_pos + 1.
+__global__ void prefill_sample_commit_kernel(const int* __restrict__ meta, int NS, const int* __restrict__ new_ids,
+                                             int* __restrict__ ids, int Bm, int* __restrict__ ring, int R,
+                                             int* __restrict__ positions) {
+  const int i = threadIdx.x;
+  if (i >= NS || i >= meta[3 * NS]) return;
+  const int slot = DSSE_IDX(meta[NS + i], Bm, -1);
+  if (slot < 0) return;
+  const int row = DSSE_IDX(meta[3 * NS + 1], R, 0);
+  ids[slot] = new_ids[i];
+  ring[(size_t)row * Bm + slot] = new_ids[i];
+  positions[slot] = meta[2 * NS + i] + 1;
+}
+
 }  // namespace dsse
+
+extern "C" hipError_t dsse_prefill_sample_gather(const void* x, int T, int H, const int* meta, int NS,
+                                                 const int* slot_meta, int Bm, void* xl, int* smeta, hipStream_t st) {
+  if (NS <= 0 || H % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dsse::prefill_sample_gather_kernel, dim3(NS), dim3(256), 0, st,
+                     reinterpret_cast<const bf16*>(x), T, H, meta, NS, slot_meta, Bm, reinterpret_cast<bf16*>(xl),
+                     smeta);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dsse_prefill_sample_commit(const int* meta, int NS, const int* new_ids, int* ids, int Bm,
+                                                 int* ring, int R, int* positions, hipStream_t st) {
+  if (NS <= 0 || NS > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dsse::prefill_sample_commit_kernel, dim3(1), dim3(64), 0, st, meta, NS, new_ids, ids, Bm, ring,
+                     R, positions);
+  return hipGetLastError();
+}
 
 // Per-rank candidate pass: fills p->cand[B, nchunks].
 extern "C" hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st) {

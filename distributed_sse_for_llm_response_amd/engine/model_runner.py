@@ -426,12 +426,14 @@ class ModelRunner:
         with torch.cuda.stream(s):
             for tb in buckets:
                 self._prefill_layers(tb, self.pf.views(tb))
+                self._graph_sample()  # padding metadata: no prompt finishes, nothing is committed
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         for tb in sorted(buckets, reverse=True):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
                 self._prefill_layers(tb, self.pf.views(tb))
+                self._graph_sample()
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
             self.pf_graphs[tb] = g
@@ -469,12 +471,14 @@ class ModelRunner:
         with torch.cuda.stream(s):
             for B, C in pairs:  # eager warm-up of every shape (kernel attributes, library state)
                 self._mixed_layers(B, C)
+                self._graph_sample()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         for B, C in sorted(pairs, reverse=True):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
                 self._mixed_layers(B, C)
+                self._graph_sample()
             self.mx_graphs.setdefault(B, []).insert(0, (C, g))
         torch.cuda.synchronize(self.device)
         self._restore_state(saved)
@@ -697,9 +701,8 @@ class ModelRunner:
         T = sum(len(s.tokens) for s in seqs)
         tb = next((t for t in sorted(self.pf_graphs) if t >= T), None) if len(seqs) <= PREFILL_GRAPH_SEQS else None
         if tb is not None:
-            q_start, q_len = self.pf.upload(seqs, tb)
-            self.pf_graphs[tb].replay()
-            self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)
+            self.pf.upload(seqs, tb, ring_row=ring_row)
+            self.pf_graphs[tb].replay()  # first tokens sampled inside the graph (_graph_sample)
             return
         w, dev = self.w, self.device
         nh, nkv, F, H = w.nh, w.nkv, w.ffn, self.cfg.hidden_size
@@ -732,6 +735,29 @@ class ModelRunner:
             self._prefill_post_attention(T, attn.view(T, nh * 128), L, w_next, resid, x, h, tmp)
 
     # ------------------------------------------------------------------ mixed prefill + decode
+    def _graph_sample(self) -> None:
+        """The first-token sampling of the prompts a captured prefill / mixed batch finishes, inside the graph
+        (VERDICT r5 item 5): gather their last rows of the static x and their slots' sampling parameters
+        (prefill_sample_gather), LM head, candidates (TP: all-gathered), pick, commit ids / ring row / positions
+        (prefill_sample_commit) -- static shapes of PREFILL_GRAPH_SEQS rows, rows past the batch's count inactive.
+        Replaces _prefill_sample's torch index kernels and per-call index upload on the graph paths."""
+        pf, w, cfg, comm = self.pf, self.w, self.cfg, self.comm
+        ns = pf.ns
+        meta, sm = pf.samp_meta(), pf.s_meta
+        ops.prefill_sample_gather(pf.x, meta, self.slot_meta, pf.s_xl, sm)
+        ops.gemm_out(pf.s_xl, w.lm_head_t, pf.s_logits)
+        active = sm[:ns]
+        ops.sample_candidates(pf.s_logits, sm[ns:2 * ns].view(torch.float32), sm[2 * ns:3 * ns],
+                              sm[3 * ns:4 * ns].view(torch.float32), sm[4 * ns:6 * ns].view(ns, 2), sm[6 * ns:7 * ns],
+                              active, pf.s_cand, w.vocab_offset)
+        if comm.size == 1:
+            cand_all = pf.s_cand.unsqueeze(0)
+        else:
+            cand_all = pf.s_cand_all
+            comm.all_gather_into(cand_all, pf.s_cand)
+        ops.sample_pick(cand_all, active, pf.s_new, vocab=cfg.vocab_size)
+        ops.prefill_sample_commit(meta, pf.s_new, self.ids, self.ring, self.positions)
+
     def mixed(self, B: int, seqs: list, ring_row: int) -> None:
         """ONE forward over the decode slots [0, B) and the prefill chunks `seqs` (rows B .. B+T-1): every weight
         byte streams once for both, so prompt tokens absorbed while streams decode cost the in-flight streams a
@@ -747,12 +773,11 @@ class ModelRunner:
         entry = next(((c, g) for c, g in self.mx_graphs.get(B, ()) if c >= T), None)
         if entry is not None and len(seqs) <= PREFILL_GRAPH_SEQS:
             t0 = time.perf_counter()
-            q_start, q_len = self.pf.upload(seqs, entry[0], row0=B)
+            self.pf.upload(seqs, entry[0], row0=B, ring_row=ring_row)
             t1 = time.perf_counter()
-            entry[1].replay()
+            entry[1].replay()  # the finishing prompts' first tokens are sampled inside (_graph_sample)
             t2 = time.perf_counter()
-            self._prefill_sample(seqs, self.pf.x, q_start, q_len, ring_row)
-            if self.host_trace is not None:  # host seconds: metadata upload, graph launch, first-token sampling
+            if self.host_trace is not None:  # host seconds: metadata upload, graph launch, (in-graph sampling: 0)
                 self.host_trace.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
             return
         w, dev = self.w, self.device
@@ -836,7 +861,7 @@ class _PrefillStatic:
         self.off = {}
         o = 0
         for name, k in (("ids", tmax), ("pos", tmax), ("slots", tmax), ("qs", n1), ("ql", n1), ("ctx", n1),
-                        ("ws", self.nw), ("wt", self.nw), ("bt", n1 * self.mb)):
+                        ("ws", self.nw), ("wt", self.nw), ("bt", n1 * self.mb), ("samp", 3 * self.ns + 2)):
             self.off[name] = (o, k)
             o += k
         self.words = o
@@ -859,10 +884,24 @@ class _PrefillStatic:
         # mixed steps: ids / positions / slots of the B decode rows followed by the chunk rows
         i32 = dict(device=dev, dtype=torch.int32)
         self.mx_ids, self.mx_pos, self.mx_slots = (torch.zeros(tmax, **i32) for _ in range(3))
+        # first-token sampling inside the graph (ModelRunner._graph_sample): the finishing prompts' last rows, their
+        # sampling parameters, logits, candidates and picks, ns rows each
+        ns, V = self.ns, w.vocab_local
+        nch = SAMPLE_CHUNKS if dev.type == "cuda" else 1
+        self.s_xl = torch.zeros(ns, H, **bf)
+        self.s_meta = torch.zeros(7 * ns, **i32)
+        self.s_logits = torch.zeros(ns, V, **f32)
+        self.s_cand = torch.zeros(ns, nch, 2, **f32)
+        self.s_cand_all = torch.zeros(runner.comm.size, ns, nch, 2, **f32)
+        self.s_new = torch.zeros(ns, **i32)
 
     def _meta(self, name):
         o, k = self.off[name]
         return self.dev_meta[o:o + k]
+
+    def samp_meta(self):
+        """[rows | slots | last_pos (ns each) | n | ring_row] of the prompts the uploaded batch finishes."""
+        return self._meta("samp")
 
     def views(self, tb: int) -> dict:
         nwb = tb // PREFILL_TILE + self.ns
@@ -874,10 +913,19 @@ class _PrefillStatic:
                  tmp=self.tmp[:tb], qkv=self.qkv[:tb])
         return d
 
-    def _fill(self, buf: torch.Tensor, seqs: list, tb: int, row0: int = 0):
+    def _fill(self, buf: torch.Tensor, seqs: list, tb: int, row0: int = 0, ring_row: int = 0):
         a = buf.numpy()
         a[:] = 0
         o = self.off
+        sm = a[o["samp"][0]:o["samp"][0] + o["samp"][1]]
+        ns, row = self.ns, row0
+        n = 0
+        for s in seqs:
+            row += len(s.tokens)
+            if s.last_chunk:  # the chunk's last row samples the prompt's first token (as _prefill_sample)
+                sm[n], sm[ns + n], sm[2 * ns + n] = row - 1, s.slot, s.start_pos + len(s.tokens) - 1
+                n += 1
+        sm[3 * ns], sm[3 * ns + 1] = n, ring_row
         ids, pos, slots = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("ids", "pos", "slots"))
         qs, ql, ctx = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("qs", "ql", "ctx"))
         ws, wt = (a[o[k][0]:o[k][0] + o[k][1]] for k in ("ws", "wt"))
@@ -906,14 +954,15 @@ class _PrefillStatic:
             ws[k], wt[k] = i, t
         return q_start, q_len
 
-    def upload(self, seqs: list, tb: int, row0: int = 0):
+    def upload(self, seqs: list, tb: int, row0: int = 0, ring_row: int = 0):
         """Metadata of `seqs` into the static buffers (stream-ordered before the replay that follows); the rows of
-        the chunks start at `row0` of the activations (a mixed step: after the B decode rows)."""
+        the chunks start at `row0` of the activations (a mixed step: after the B decode rows); the prompts finishing
+        in this batch commit their first token to ring row `ring_row` inside the graph."""
         k = self.flip
         self.flip ^= 1
         if self.events[k] is not None:
             self.events[k].synchronize()  # that pinned buffer's previous copy has been consumed
-        q_start, q_len = self._fill(self.host[k], seqs, tb, row0)
+        q_start, q_len = self._fill(self.host[k], seqs, tb, row0, ring_row)
         self.dev_meta.copy_(self.host[k], non_blocking=True)
         if self.dev_meta.is_cuda:
             ev = torch.cuda.Event()

@@ -207,6 +207,23 @@ def sample_pick(cand_all, active, next_ids, ring=None, ring_counter=None, positi
         ref.sample_pick(cand_all, active, next_ids, ring, ring_counter, positions_inc)
 
 
+def prefill_sample_gather(x, meta, slot_meta, xl, smeta):
+    """First-token sampling inside the prefill / mixed graphs: xl = the finishing prompts' last rows of x, smeta =
+    their slots' sampling parameters (sampler.hip prefill_sample_gather_kernel has the layouts)."""
+    if _hip(x):
+        torch.ops.dsse.prefill_sample_gather(x, meta, slot_meta, xl, smeta)
+    else:
+        ref.prefill_sample_gather(x, meta, slot_meta, xl, smeta)
+
+
+def prefill_sample_commit(meta, new_ids, ids, ring, positions):
+    """ids[slot] = ring[ring_row][slot] = new_ids[i], positions[slot] = last_pos[i] + 1 for the n finishing prompts."""
+    if _hip(new_ids):
+        torch.ops.dsse.prefill_sample_commit(meta, new_ids, ids, ring, positions)
+    else:
+        ref.prefill_sample_commit(meta, new_ids, ids, ring, positions)
+
+
 def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids, ring=None, ring_counter=None,
            positions_inc=None, nchunks: int = 16):
     """Single-rank convenience: candidates + pick."""

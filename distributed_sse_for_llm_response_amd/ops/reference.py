@@ -305,3 +305,35 @@ def sample(logits, temperature, top_k, top_p, seeds, positions, active, next_ids
     cand = torch.empty(logits.shape[0], 1, 2)
     sample_candidates(logits, temperature, top_k, top_p, seeds, positions, active, cand)
     sample_pick(cand.unsqueeze(0), active, next_ids, ring, ring_counter, positions_inc)
+
+
+def prefill_sample_gather(x, meta, slot_meta, xl, smeta):
+    """CPU twin of sampler.hip prefill_sample_gather_kernel: meta = [rows | slots | last_pos (NS each) | n | ring_row],
+    slot_meta = [active | temperature | top_k | top_p | seeds x 2] (Bm each) -> xl rows, smeta = [active | temperature |
+    top_k | top_p | seeds x 2 | position] (NS each)."""
+    NS, Bm = xl.shape[0], slot_meta.numel() // 6
+    n = int(meta[3 * NS])
+    xl.zero_()
+    smeta.zero_()
+    for i in range(NS):
+        on = i < n
+        slot = int(meta[NS + i]) if on else 0
+        if on:
+            xl[i] = x[int(meta[i])]
+        smeta[i] = 1 if on else 0
+        smeta[NS + i] = slot_meta[Bm + slot]
+        smeta[2 * NS + i] = slot_meta[2 * Bm + slot]
+        smeta[3 * NS + i] = slot_meta[3 * Bm + slot]
+        smeta[4 * NS + 2 * i] = slot_meta[4 * Bm + 2 * slot]
+        smeta[4 * NS + 2 * i + 1] = slot_meta[4 * Bm + 2 * slot + 1]
+        smeta[6 * NS + i] = int(meta[2 * NS + i]) if on else 0
+
+
+def prefill_sample_commit(meta, new_ids, ids, ring, positions):
+    NS = new_ids.numel()
+    n, row = int(meta[3 * NS]), int(meta[3 * NS + 1])
+    for i in range(min(n, NS)):
+        slot = int(meta[NS + i])
+        ids[slot] = new_ids[i]
+        ring[row, slot] = new_ids[i]
+        positions[slot] = int(meta[2 * NS + i]) + 1

@@ -171,7 +171,14 @@ def test_prefill_graph_matches_eager(model, gpu):
     batches = [[PrefillSeq(i, p, 0, tables[i], True) for i, p in enumerate(prompts) if i != 1],
                [PrefillSeq(1, prompts[1][:20], 0, tables[1], False)],
                [PrefillSeq(1, prompts[1][20:], 20, tables[1], True)]]
+    # greedy rows and sampled rows (temperature / top-k / top-p): the graph samples the first tokens inside
+    # (_graph_sample) and must commit the same ids, ring row and positions as the eager _prefill_sample
     r.temperature.zero_()
+    r.temperature[2:4] = 0.8
+    r.top_k[3] = 40
+    r.top_p[4] = 0.9
+    r.temperature[4] = 1.0
+    r.seeds[:len(lens), 0] = torch.arange(11, 11 + len(lens), dtype=torch.int32)
     blocks = torch.tensor([b for t in tables for b in t], device=gpu)
     out = {}
     saved = dict(r.pf_graphs)
@@ -181,15 +188,23 @@ def test_prefill_graph_matches_eager(model, gpu):
             r.kv.k[li].index_fill_(0, blocks, 0)
             r.kv.v[li].index_fill_(0, blocks, 0)
         r.ids.zero_()
+        r.positions.zero_()
+        r.ring[3].fill_(-1)
         for b in batches:
-            r.prefill(b, ring_row=0)
+            r.prefill(b, ring_row=3)
         torch.cuda.synchronize()
         out[mode] = ([r.kv.k[li].index_select(0, blocks).float() for li in range(CFG.num_layers)],
                      [r.kv.v[li].index_select(0, blocks).float() for li in range(CFG.num_layers)],
-                     r.ids[:len(lens)].cpu().tolist())
+                     r.ids[:len(lens)].cpu().tolist(), r.positions[:len(lens)].cpu().tolist(),
+                     r.ring[3, :len(lens)].cpu().tolist())
+    r.temperature.zero_()
+    r.top_k.zero_()
+    r.top_p.fill_(1.0)
     r.pf_graphs = saved
     for li in range(CFG.num_layers):
         for kind, a, b in (("k", out["graph"][0][li], out["eager"][0][li]), ("v", out["graph"][1][li], out["eager"][1][li])):
             err = (a - b).abs().max().item()
             assert err <= 0.02 * max(1.0, b.abs().max().item()), f"layer {li} {kind}: max err {err}"
     assert out["graph"][2] == out["eager"][2]
+    assert out["graph"][3] == out["eager"][3] == lens  # positions = prompt length (next token's position)
+    assert out["graph"][4] == out["eager"][4] == out["eager"][2]

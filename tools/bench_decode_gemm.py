@@ -22,7 +22,10 @@ import torch  # noqa: E402
 from distributed_sse_for_llm_response_amd import ops  # noqa: E402
 from distributed_sse_for_llm_response_amd.ops import reference as R  # noqa: E402
 
-SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          # one rank's shard at TP = 8 (tools/bench_tp_rank.py): column-parallel N / 8, row-parallel K / 8
+          "qkv_tp8": (768, 4096), "o_tp8": (4096, 512), "gate_up_tp8": (3584, 4096), "down_tp8": (4096, 1792),
+          "lm_tp8": (4096, 4096)}
 
 
 def main():
