@@ -69,6 +69,9 @@ class EngineLoop(threading.Thread):
     publish_tokens / set_ready.  A DP worker ships its engine metrics to the router (``observe``).
     """
 
+    halted = False
+    pub_lock = threading.Lock()  # class default (a loop built without __init__); each loop sets its own
+
     def __init__(self, runtime, engine: LLMEngine, tokenizer, cfg: ServeConfig):
         super().__init__(daemon=True, name="engine-loop")
         self.rt, self.engine, self.tok, self.cfg = runtime, engine, tokenizer, cfg
