@@ -47,10 +47,14 @@ __host__ __device__ inline size_t ar_data_off(int rows) { return ((size_t)2 * kA
 __host__ __device__ inline size_t ar_gdata_off(int rows, int H) { return ar_data_off(rows) + (size_t)2 * rows * H * 2; }
 
 // H / 8 threads per workgroup (16 bytes of bf16 per lane), H <= 8192.
+// part != null (round 6): this rank's partial row is the sum of `nsplit` fp32 split-K slabs [nsplit, M, H] of the O /
+// down GEMM, rounded to bf16 -- the bits splitk_reduce_kernel<kStoreBf16> would have written to tmp, without that
+// launch.
 __global__ void __launch_bounds__(1024)
 ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const bf16* __restrict__ w,
                   bf16* __restrict__ y, int H, float eps, const unsigned long long* __restrict__ peers, int rank,
-                  int world, int rows, unsigned int* __restrict__ epoch, unsigned int* __restrict__ err) {
+                  int world, int rows, unsigned int* __restrict__ epoch, unsigned int* __restrict__ err,
+                  const float* __restrict__ part, int nsplit, int M) {
   const int b = blockIdx.x, tid = threadIdx.x;
   __shared__ unsigned int e_s;
   __shared__ float red[16];
@@ -65,7 +69,22 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
       reinterpret_cast<const void*>(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(mine_u >> 32)) << 32) |
                                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mine_u)), 0x7FFFFFFF);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = *reinterpret_cast<const u32x4*>(tmp + (size_t)b * H + tid * 8);
+  u32x4 v;
+  if (part) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sidx = 0; sidx < nsplit; ++sidx) {  // slab order = splitk_reduce's summation order
+      const float* sp = part + ((size_t)sidx * M + b) * H + tid * 8;
+      const float4 p0 = *reinterpret_cast<const float4*>(sp), p1 = *reinterpret_cast<const float4*>(sp + 4);
+      a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
+      a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
+    }
+    bf16x8 hv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = f2bf(a[j]);
+    v = __builtin_bit_cast(u32x4, hv);
+  } else {
+    v = *reinterpret_cast<const u32x4*>(tmp + (size_t)b * H + tid * 8);
+  }
   __builtin_amdgcn_raw_buffer_store_b128(v, mrs, (uint32_t)doff, 0, kAuxSys);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -208,13 +227,15 @@ extern "C" hipError_t dsse_ar_close(void* ptr, int opened) { return opened ? hip
 
 extern "C" hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, const void* w, void* y, int H, float eps,
                                       const unsigned long long* peers, int rank, int world, int rows,
-                                      unsigned int* epoch, unsigned int* err, hipStream_t st) {
+                                      unsigned int* epoch, unsigned int* err, const float* part, int nsplit,
+                                      hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  if (M > rows || world > kArMaxRanks || world < 1 || rank < 0 || rank >= world || H % 512 != 0 || H / 8 > 1024)
+  if (M > rows || world > kArMaxRanks || world < 1 || rank < 0 || rank >= world || H % 512 != 0 || H / 8 > 1024 ||
+      (part != nullptr && nsplit < 1) || (part == nullptr && tmp == nullptr))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(ar_rmsnorm_kernel, dim3(M), dim3(H / 8), 0, st, reinterpret_cast<const bf16*>(tmp), resid,
                      reinterpret_cast<const bf16*>(w), reinterpret_cast<bf16*>(y), H, eps, peers, rank, world, rows,
-                     epoch, err);
+                     epoch, err, part, nsplit, M);
   return hipGetLastError();
 }
 

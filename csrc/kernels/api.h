@@ -53,7 +53,7 @@ struct AttnParams {
   float* part_o;            // [num_work, Hkv, nparts, QW, 16, 128]
   float2* part_ml;          // [num_work, Hkv, nparts, QW, 16]
   int hq, hkv, group;       // group = hq / hkv; 16 % group == 0
-  int part;                 // keys per partition (multiple of 32 * KWV)
+  int part;                 // keys per partition (multiple of 32 * KWV); 0 = each item's keys split evenly over nparts
   int nparts;               // grid.z
   float scale_log2;         // log2(e) / sqrt(128)
   int kwv;                  // decode: waves per workgroup splitting the keys (0 = by grid size)
@@ -106,6 +106,7 @@ hipError_t dsse_gemm_tiled(int mode, int cfg, int S, int partial_only, const voi
 hipError_t dsse_gemm_pipe(int mode, int bm, int S, int partial_only, const void* X, int ldx, int M, const void* W,
                           int K, int N, const dsse::GemmEpi* ep, float* part, hipStream_t st);
 size_t dsse_gemm_pipe_fix_floats(int bm, int S, int M, int N);
+size_t dsse_gemm_ring_fix_floats(int nw, int S, int M, int N);
 hipError_t dsse_paged_attention(int mode, int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st);
 hipError_t dsse_sample(int B, const dsse::SampleParams* p, hipStream_t st);
@@ -132,7 +133,7 @@ hipError_t dsse_ar_open(const void* handle64, void** ptr);
 hipError_t dsse_ar_close(void* ptr, int opened);
 hipError_t dsse_ar_rmsnorm(int M, const void* tmp, float* resid, const void* w, void* y, int H, float eps,
                            const unsigned long long* peers, int rank, int world, int rows, unsigned int* epoch,
-                           unsigned int* err, hipStream_t st);
+                           unsigned int* err, const float* part, int nsplit, hipStream_t st);
 hipError_t dsse_ar_gather(int M, const void* in, void* out, const unsigned long long* peers, int rank, int world,
                           int rows, int H, unsigned int* gepoch, unsigned int* err, hipStream_t st);
 // Checked build: first out-of-range index per kernel file (line, value, bound, count); zeros otherwise.

@@ -37,6 +37,16 @@ constexpr int kD = 128;
 // PD: KV pages in flight per wave (a register ring of PD pages, each wave's next PD-1 pages issued before the
 // current one is computed).  One-wave workgroups with PD > 1 are held to 2 waves per SIMD (256 VGPRs): the
 // 2048-workgroup grid they serve (256 streams x 8 kv heads) puts 2 waves on each SIMD anyway.
+// Keys per flash-decoding partition: p.part, or (p.part == 0, round 6) this work item's own key range split evenly
+// over the nparts partitions in whole pages -- a graph captured for max_model_len then keeps every partition busy at
+// the contexts actually served (one KV head per rank at TP = 8: 64 streams = 64 (sequence, head) pairs, all of whose
+// work sat in the first partition of a max_model_len / nparts split).
+DEV int part_keys(const AttnParams& p, int kmax) {
+  if (p.part > 0) return p.part;
+  const int per = (kmax + p.nparts - 1) / p.nparts;
+  return max(kPage, (per + kPage - 1) / kPage * kPage);
+}
+
 template <int QW, int KWV, int PD = 1, int FQG = 0>
 __global__ void __launch_bounds__(64 * QW * KWV, QW * KWV == 1 ? (PD > 1 ? 2 : 4) : 1)
 paged_attention_kernel(AttnParams p) {
@@ -62,8 +72,9 @@ paged_attention_kernel(AttnParams p) {
   // Key range needed by the whole workgroup (all QW tiles): up to the last live query.
   const int last_q = min(qlen, (p.work_tile[item] + 1) * QW * QT) - 1;
   const int kmax = (qlen > 0 && last_q >= 0) ? (ctx - qlen + last_q + 1) : 0;
-  const int kbeg = pz * p.part;
-  const int kend = min(kmax, kbeg + p.part);
+  const int part = part_keys(p, kmax);
+  const int kbeg = pz * part;
+  const int kend = min(kmax, kbeg + part);
   if (kbeg >= kend) return;  // uniform for the whole workgroup
 
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
@@ -127,7 +138,7 @@ paged_attention_kernel(AttnParams p) {
     const int kn_page = (ctx - 1) & ~(kPage - 1);
     const int sl = p.slots[m];
     // wave-uniform: this partition holds the newest key, and the key-split wave visiting its page is this one
-    const bool owner = pz == (ctx - 1) / p.part && sl >= 0 && ((kn_page - kbeg) / kPage) % KWV == kw;
+    const bool owner = pz == (ctx - 1) / part && sl >= 0 && ((kn_page - kbeg) / kPage) % KWV == kw;
     const int t = lane >> 3, j = lane & 7;
     const float* base = p.qkv_part + (size_t)m * N + 16 * t + j;
     // Slabs 0 and 1 (slab 0 again when S == 1, masked below) are loaded unconditionally -- a guarded load is a
@@ -391,7 +402,8 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p) {
   if (qi >= qlen) return;
   const int last_q = min(qlen, (p.work_tile[item] + 1) * QW * QT) - 1;
   const int kmax = ctx - qlen + last_q + 1;
-  const int np = min(p.nparts, (kmax + p.part - 1) / p.part);
+  const int part = part_keys(p, kmax);
+  const int np = min(p.nparts, (kmax + part - 1) / part);
   float mm = -1e30f;
   for (int z = 0; z < np; ++z) {
     const size_t base = (((size_t)item * p.hkv + h) * p.nparts + z) * QW + qw;

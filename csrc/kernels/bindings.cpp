@@ -116,6 +116,7 @@ struct SCfg {
   int mt, nt, nw, rd, S;
   bool ok;
   int ring_nw = 0;  // waves per workgroup of the LDS-DMA ring form (0 = stream_launch's default rule)
+  bool ring_only = false;  // only the ring kernel's K contract holds (K % 128, not K % 512)
 };
 // 64 < M <= 256: one workgroup holds all rows (mt 8 / 16, X slices of 256 / 128 columns); M > 256: row
 // blocks of 64 (mt 4, L2-shared weights).
@@ -142,8 +143,15 @@ SCfg pick_stream(int M, int N, int K, int mode = -1) {
   if (c.nt == 2 || c.rd != 2 || M > 64 || (c.nw != 4 && c.nw != 8)) c.rd = 1;
   if (c.mt == 8) c.rd = 2;
   if (c.mt == 16) c.rd = c.nt == 2 ? 2 : 4;  // ring of 4 chunks (2 with two tiles per wave: VGPR budget)
-  const int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
+  int cps = c.mt <= 4 ? 4 : (c.mt == 8 ? 2 : 1);  // gemm_stream.hip stream_cps
   c.ok = K % (128 * cps) == 0 && N % (16 * c.nt) == 0 && (N / (16 * c.nt)) % c.nw == 0;
+  // 17-64 rows with K a multiple of 128 but not of 512 (a TP = 8 rank's down projection, K = 1792): the LDS-DMA ring
+  // kernel (stream_launch) only needs K % (128 S) == 0 -- before round 6 these fell to a 128-row tiled tile
+  if (!c.ok && M > 16 && M <= 64 && c.nt == 1 && K % 128 == 0 && (N / 16) % c.nw == 0 && env_int("s_ring", 1) > 0) {
+    c.ok = true;
+    c.ring_only = true;
+    cps = 1;
+  }
   if (!c.ok) return c;
   const int wgs = N / (16 * c.nt) / c.nw * (M > 16 * c.mt ? (M + 63) / 64 : 1), slices = K / (128 * cps);
   int S = env_int("s_split", 0);
@@ -179,6 +187,10 @@ hipError_t stream_launch(int mode, const SCfg& c, int S, int partial_only, const
   // 17-64 rows (32-stream step 3.99 vs 4.04 ms; at 9-16 rows the ring measured 4.02 vs 3.99: gemm_stream kept)
   const bool ring_rows = (c.mt == 4 && M > 32 && M <= 64) || (c.mt == 2 && M > 16 && M <= 32) ||
                          (c.mt == 8 && M > 64 && M <= 128 && c.nw == 4);
+  // partial_only 2 = split K combined in the launch: only the 17-64-row ring kernel has that form (else the caller
+  // falls back to slabs + splitk_reduce)
+  if (partial_only == 2 && !(ring > 0 && ring_rows && M <= 64 && c.nt == 1 && K % (128 * S) == 0 && S > 1))
+    return hipErrorNotSupported;
   if (ring > 0 && ring_rows && c.nt == 1 && K % (128 * S) == 0) {
     int nw = c.nw >= 7 ? c.nw : 4;
     if (c.ring_nw > 0 && (N / 16) % c.ring_nw == 0 && M <= 64)
@@ -461,6 +473,17 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   }
   if (impl == 2) {
     const SCfg c = pick_stream(M, N, K, mode);
+    // SiLU·mul split over K (a TP rank's gate_up at 17-64 rows): slices combined inside the ring kernel (round 6)
+    // instead of slabs + a splitk_reduce launch; s_fix=0 (DSSE_KERNEL_CFG) keeps the reduce launch
+    if (c.S > 1 && mode == dsse::kSiluMul && M <= 64 && env_int("s_fix", 1)) {
+      at::Tensor ws = at::empty({(int64_t)dsse_gemm_ring_fix_floats(1, c.S, M, N)}, x.options().dtype(at::kFloat));
+      ep.fix_cnt = fix_counters(x.device());
+      const hipError_t e = stream_launch(mode, c, c.S, 2, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
+                                         ws.data_ptr<float>());
+      if (e == hipSuccess) return;
+      TORCH_CHECK(e == hipErrorNotSupported, "dsse kernel launch failed: ", hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
     at::Tensor part;
     if (c.S > 1) part = at::empty({(int64_t)c.S * M * N}, x.options().dtype(at::kFloat));
     DSSE_CHECK_HIP(stream_launch(mode, c, c.S, 0, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
@@ -548,6 +571,40 @@ int64_t gemm_resid_split(const Tensor& x, const Tensor& w, Tensor& resid, Tensor
     }
   }
   gemm_resid(x, w, resid);
+  return 0;
+}
+
+// bf16 projection whose split-K reduction is left to the consumer (the TP decode step's IPC all-reduce, ar_rmsnorm
+// with `part`): returns S > 0 when fp32 slabs [S, M, N] went to `part` (out untouched), else 0 after writing out.
+int64_t gemm_out_split(const Tensor& x, const Tensor& w, Tensor& out, Tensor& part) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(part, "part");
+  check_dtype(part, at::kFloat, "part");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  const bool shape_ok = M >= 1 && K % 128 == 0 && N % 16 == 0 && w.size(1) == K;
+  const int impl = shape_ok ? gemm_impl(M, N, K) : 0;
+  dsse::GemmEpi ep{};
+  if (impl == 2) {
+    const SCfg c = pick_stream(M, N, K);
+    if (c.S > 1 && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      DSSE_CHECK_HIP(stream_launch(dsse::kStoreBf16, c, c.S, 1, x.data_ptr(), M, w.data_ptr(), K, N, &ep,
+                                   part.data_ptr<float>()));
+      return c.S;
+    }
+  } else if (impl == 4) {
+    const TCfg c = pick_tiled(M, N, K, true);
+    if (c.S > 1 && !c.fix && part.numel() >= (int64_t)c.S * M * N) {
+      check_dtype(x, at::kBFloat16, "x");
+      check_dtype(w, at::kBFloat16, "w");
+      DSSE_CHECK_HIP(tiled_call(dsse::kStoreBf16, c.cfg, c.S, 1, x.data_ptr(), K, M, w.data_ptr(), K, N, &ep,
+                                part.data_ptr<float>()));
+      return c.S;
+    }
+  }
+  gemm_out(x, w, out);
   return 0;
 }
 
@@ -711,7 +768,8 @@ dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cach
   TORCH_CHECK(out.dim() == 3 && out.size(1) == hq && out.size(2) == 128, "out must be [T, Hq, 128]");
   const int num_work = (int)work_seq.numel();
   TORCH_CHECK(work_tile.numel() == num_work, "work lists differ in length");
-  TORCH_CHECK(part % (32 * kwv) == 0 && part > 0, "partition size must be a multiple of ", 32 * kwv);
+  TORCH_CHECK((part % (32 * kwv) == 0 && part > 0) || (part == 0 && nparts > 1),
+              "partition size must be a multiple of ", 32 * kwv, " (or 0: even split of each sequence's keys)");
   TORCH_CHECK(nparts >= 1, "nparts >= 1");
   if (nparts > 1) {
     check_gpu(part_o, "part_o");
@@ -984,7 +1042,8 @@ void ar_close(int64_t ptr, bool opened) { DSSE_CHECK_HIP(dsse_ar_close(reinterpr
 // peers: int64 device tensor [world] of buffer pointers in THIS process (own at index rank); epoch: int32 [rows],
 // zero-initialised, owned by this all-reduce context; err: int32 [1] (set on a timed-out peer wait).
 void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, double eps, const Tensor& peers,
-                int64_t rank, int64_t rows, Tensor& epoch, Tensor& err) {
+                int64_t rank, int64_t rows, Tensor& epoch, Tensor& err, const c10::optional<Tensor>& part,
+                int64_t nsplit) {
   for (const Tensor* t : {&tmp, (const Tensor*)&resid, &w, (const Tensor*)&y, &peers, (const Tensor*)&epoch,
                           (const Tensor*)&err})
     check_gpu(*t, "ar_rmsnorm tensor");
@@ -999,10 +1058,18 @@ void ar_rmsnorm(const Tensor& tmp, Tensor& resid, const Tensor& w, Tensor& y, do
   TORCH_CHECK(tmp.dim() == 2 && resid.size(0) >= M && resid.size(1) == H && y.size(0) >= M && y.size(1) == H &&
                   w.numel() == H, "ar_rmsnorm: shape mismatch");
   TORCH_CHECK(M <= rows && epoch.numel() >= rows, "ar_rmsnorm: more rows than the buffers hold");
+  const float* pp = nullptr;
+  if (part.has_value() && nsplit > 0) {  // the partial row = sum of the GEMM's split-K slabs (tmp unused)
+    check_gpu(*part, "part");
+    check_dtype(*part, at::kFloat, "part");
+    TORCH_CHECK(part->numel() >= nsplit * M * H, "part too small for ", nsplit, " slabs");
+    pp = part->data_ptr<float>();
+  }
   DSSE_CHECK_HIP(dsse_ar_rmsnorm(M, tmp.data_ptr(), resid.data_ptr<float>(), w.data_ptr(), y.data_ptr(), H, (float)eps,
                                  reinterpret_cast<const unsigned long long*>(peers.data_ptr<int64_t>()), (int)rank,
                                  (int)peers.numel(), (int)rows, reinterpret_cast<unsigned int*>(epoch.data_ptr<int>()),
-                                 reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
+                                 reinterpret_cast<unsigned int*>(err.data_ptr<int>()), pp, (int)(pp ? nsplit : 0),
+                                 cur_stream()));
 }
 
 // C3 over the same IPC buffers: out[q] = rank q's `cand` rows (every rank's sampling candidates, [M, 16, 2] fp32 =
@@ -1091,6 +1158,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("rmsnorm(Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor? delta=None, Tensor? embed=None, "
         "Tensor? ids=None, Tensor? part=None, int nsplit=0) -> ()");
   m.def("gemm_resid_split(Tensor x, Tensor w, Tensor(a!) resid, Tensor(b!) part) -> int");
+  m.def("gemm_out_split(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) part) -> int");
   m.def("refresh_env() -> ()", &refresh_env);
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv) -> ()");
@@ -1115,7 +1183,7 @@ TORCH_LIBRARY(dsse, m) {
   m.def("ar_open(Tensor handle) -> int", &ar_open);
   m.def("ar_close(int ptr, bool opened) -> ()", &ar_close);
   m.def("ar_rmsnorm(Tensor tmp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, Tensor peers, int rank, int rows, "
-        "Tensor(c!) epoch, Tensor(d!) err) -> ()");
+        "Tensor(c!) epoch, Tensor(d!) err, Tensor? part=None, int nsplit=0) -> ()");
   m.def("ar_gather(Tensor cand, Tensor(a!) out, Tensor peers, int rank, int rows, int H, Tensor(b!) gepoch, "
         "Tensor(c!) err) -> ()");
   m.def("kernels_abi_version() -> int", &kernels_abi_version);
@@ -1131,6 +1199,7 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("gemm_out", &gemm_out);
   m.impl("gemm_resid", &gemm_resid);
   m.impl("gemm_resid_split", &gemm_resid_split);
+  m.impl("gemm_out_split", &gemm_out_split);
   m.impl("gemm_silu", &gemm_silu);
   m.impl("gemm_qkv_rope", &gemm_qkv_rope);
   m.impl("rmsnorm", &rmsnorm);

@@ -316,7 +316,12 @@ DEV void glds16_s(const void* src, char* lds_base) {
                                    16, 0, 0);
 }
 
-template <int MT, int NW, int D, int MODE>
+// FIX (round 6, the gemm_pipe.hip protocol on this kernel's small tiles): split-K slices of a column group combined
+// inside the launch -- ticket first, the first S - 1 slices store their MT x 16 x 16 fp32 accumulators per wave
+// (NW x MT KiB per workgroup) and count themselves done, the last waits for them (they wait for nothing), adds and
+// runs the epilogue.  Used for the SiLU·mul projection of TP ranks at 17-64 rows (gate_up, N = 28672 / t), whose
+// split-K otherwise needs a splitk_reduce launch.
+template <int MT, int NW, int D, int MODE, bool FIX = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restrict__ W, int K, int N, int Kr,
                  GemmEpi ep, float* __restrict__ part) {
@@ -402,6 +407,58 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   // no LDS-DMA may still be landing when the workgroup's LDS is handed to the next workgroup
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if constexpr (FIX) {
+    const int S = gridDim.y;
+    if (S > 1) {
+      typedef __attribute__((address_space(1))) int gint;  // shared words: global agent-scope accesses
+      gint* cnt = (gint*)(ep.fix_cnt) + 4;                 // tickets [wg], done [kFixTiles + wg]; timeouts at [0]
+      constexpr int kSlotF4 = NW * MT * 64;                // [wave][mt][lane]
+      __syncthreads();  // every wave past its last LDS read: word 0 of the LDS carries the ticket
+      int* sflag = reinterpret_cast<int*>(smem);
+      if (threadIdx.x == 0) sflag[0] = __hip_atomic_fetch_add(cnt + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int ticket = __builtin_amdgcn_readfirstlane(sflag[0]);
+      f32x4* slots = reinterpret_cast<f32x4*>(part) + (size_t)wg * (S - 1) * kSlotF4;
+      const int off = w * MT * 64 + lane;
+      if (ticket < S - 1) {
+        f32x4* dst = slots + (size_t)ticket * kSlotF4 + off;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) dst[mt * 64] = acc[mt];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(cnt + kFixTiles + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+      if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt + kFixTiles + wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 22)) {
+            __hip_atomic_fetch_add(cnt - 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(cnt + wg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + kFixTiles + wg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int sl = 0; sl < S - 1; ++sl) {
+        const f32x4* src = slots + (size_t)sl * kSlotF4 + off;
+        f32x4 t[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) t[mt] = src[mt * 64];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] += t[mt];
+      }
+    }
+  }
+
   float* part_ks = part ? part + (size_t)ks * M * N : nullptr;
   if constexpr (MODE == kSiluMul) {
 #pragma unroll
@@ -418,20 +475,23 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
     }
 }
 
-template <int MT, int NW, int D, int MODE>
+template <int MT, int NW, int D, int MODE, bool FIX = false>
 static hipError_t launch_r(const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S, const GemmEpi& ep,
                            float* part, hipStream_t st) {
   const size_t lds = RingGeom<MT, NW, D>::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<MT, NW, D, MODE>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_ring_kernel<MT, NW, D, MODE, FIX>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   dim3 grid(N / 16 / NW, S), block(64 * NW);
-  hipLaunchKernelGGL((gemm_ring_kernel<MT, NW, D, MODE>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep, part);
+  hipLaunchKernelGGL((gemm_ring_kernel<MT, NW, D, MODE, FIX>), grid, block, lds, st, X, ldx, M, W, K, N, K / S, ep,
+                     part);
   return hipGetLastError();
 }
+
+
 
 // Ring depth per (rows, waves): as many 128-column chunks as the LDS holds (slot = 16 MT rows x 256 B of X +
 // NW x 4 KiB of weights, <= 160 KiB in all).
@@ -451,6 +511,18 @@ static hipError_t launch_r_mode(int nw, const bf16* X, int ldx, int M, const bf1
   K_R_CASE(4, 3) K_R_CASE(4, 4) K_R_CASE(4, 6) K_R_CASE(4, 7) K_R_CASE(4, 8)
   K_R_CASE(2, 4) K_R_CASE(2, 7) K_R_CASE(2, 8)
 #undef K_R_CASE
+  return hipErrorInvalidValue;
+}
+
+// The in-launch fix-up form (SiLU·mul only; 17-64 rows, 4 / 7 / 8 waves).
+static hipError_t launch_r_fix(int nw, const bf16* X, int ldx, int M, const bf16* W, int K, int N, int S,
+                               const GemmEpi& ep, float* part, hipStream_t st) {
+  const int mt = M <= 32 ? 2 : 4;
+  if (M > 64 || N / 16 / nw > kFixTiles) return hipErrorInvalidValue;
+#define K_RF_CASE(MT_, NW_) \
+  if (mt == MT_ && nw == NW_) return launch_r<MT_, NW_, ring_depth(MT_, NW_), kSiluMul, true>(X, ldx, M, W, K, N, S, ep, part, st);
+  K_RF_CASE(4, 4) K_RF_CASE(4, 7) K_RF_CASE(4, 8) K_RF_CASE(2, 4) K_RF_CASE(2, 7) K_RF_CASE(2, 8)
+#undef K_RF_CASE
   return hipErrorInvalidValue;
 }
 
@@ -670,6 +742,10 @@ extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, 
   const bf16* x = reinterpret_cast<const bf16*>(X);
   const bf16* w = reinterpret_cast<const bf16*>(W);
   if (M > 128 || M < 17 || (M > 64 && nw != 4) || K % (128 * S) != 0 || (N / 16) % nw != 0) return hipErrorInvalidValue;
+  if (partial_only == 2) {  // split-K combined in the launch (SiLU·mul; `part` = dsse_gemm_ring_fix_floats)
+    if (mode != kSiluMul || S < 2 || ep->fix_cnt == nullptr) return hipErrorInvalidValue;
+    return launch_r_fix(nw, x, ldx, M, w, K, N, S, *ep, part, st);
+  }
   // ring2: the decoupled-weight-look-ahead kernel (the single-ring kernel is the fallback for shapes it is not
   // instantiated for); chosen by the caller (bindings.cpp ring2_for)
   const bool r2 = ring2 != 0;
@@ -696,6 +772,12 @@ extern "C" hipError_t dsse_gemm_ring(int mode, int nw, int S, int partial_only, 
   hipError_t e = run(std::integral_constant<int, kPartial>{}, S, ep, part);
   if (e != hipSuccess || partial_only) return e;
   return launch_splitk_reduce(mode, part, S, M, N, *ep, st);
+}
+
+// Workspace floats of the ring kernel's in-launch fix-up: S - 1 register-order slots per column group.
+extern "C" size_t dsse_gemm_ring_fix_floats(int nw, int S, int M, int N) {
+  const int mt = M <= 32 ? 2 : 4;
+  return (size_t)(N / 16 / nw) * (S - 1) * nw * mt * 64 * 4;
 }
 
 DSSE_CHECK_READER(dsse_check_gemm_stream)

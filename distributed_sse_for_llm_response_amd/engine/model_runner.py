@@ -108,7 +108,10 @@ def decode_partitioning(B: int, nkv: int, max_ctx: int, target_wgs: int = 512, m
     want = max(1, min(max_parts, math.ceil(target_wgs / max(1, B * nkv))))
     part = max(128, math.ceil(max_ctx / want / 128) * 128)
     nparts = math.ceil(max_ctx / part)
-    return part, nparts
+    # several partitions: part 0 = each sequence's keys split evenly over them (attention.hip part_keys), so the
+    # partitions stay busy at the served contexts, not only at max_ctx (TP = 8, 64 streams: 19 -> ~? us per layer,
+    # profiles/r6/tp8_rank_decode_kernels_r6.md)
+    return (0 if nparts > 1 else part), nparts
 
 
 @dataclass
@@ -280,6 +283,10 @@ class ModelRunner:
         if self.comm.size == 1:
             ns = ops.gemm_resid_split(a, wt, resid, self.split_part)
             ops.rmsnorm(resid, norm_w, x, eps, part=self.split_part, nsplit=ns)
+        elif self.comm.ipc_rows(a.shape[0]) and a.is_cuda:
+            # the IPC all-reduce kernel sums the GEMM's split-K slabs itself (no splitk_reduce launch)
+            ns = ops.gemm_out_split(a, wt, tmp, self.split_part)
+            self.comm.all_reduce_rmsnorm(tmp, resid, norm_w, x, eps, part=self.split_part, nsplit=ns)
         else:
             ops.gemm_out(a, wt, tmp)
             self.comm.all_reduce_rmsnorm(tmp, resid, norm_w, x, eps)
@@ -453,7 +460,7 @@ class ModelRunner:
         tmax = self.pf.tmax if self.pf is not None else 0
         if fixed > 0:
             return [c for c in [self.mixed_chunk(B)] if B + c <= tmax]
-        top = (MIXED_MAX_ROWS - B) // PREFILL_TILE * PREFILL_TILE
+        top = (int(os.environ.get("DSSE_MIXED_MAX_ROWS_AB", MIXED_MAX_ROWS)) - B) // PREFILL_TILE * PREFILL_TILE
         sizes = sorted({c for c in MIXED_CHUNKS if c <= top} | ({top} if top >= MIXED_CHUNKS[0] else set()))
         return [c for c in sizes if B + c <= tmax]
 

@@ -102,6 +102,15 @@ def gemm_resid_split(x, w, resid, part) -> int:
     return 0
 
 
+def gemm_out_split(x, w, out, part) -> int:
+    """out = x · wᵀ (bf16), or (when the chosen kernel splits K) fp32 slabs [S, M, N] into `part` and return S for a
+    consumer that sums them (the TP decode step's IPC all-reduce, comm.all_reduce_rmsnorm(part=..., nsplit=S))."""
+    if _hip(x):
+        return int(torch.ops.dsse.gemm_out_split(x, w, out, part))
+    ref.gemm_out(x, w, out)
+    return 0
+
+
 def kernel_cfg_env(**overrides) -> str:
     """The DSSE_KERNEL_CFG string (the kernel library's one configuration override: "key=value,..."; keys in
     csrc/kernels/bindings.cpp env_int, e.g. gemm_impl, t_cfg, s_nw) with `overrides` merged into the current value.

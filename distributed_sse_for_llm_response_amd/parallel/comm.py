@@ -127,15 +127,22 @@ class TPComm:
         self.fast_ar = ar
         return why
 
-    def all_reduce_rmsnorm(self, tmp, resid, norm_w, y, eps: float) -> None:
-        """resid += all_reduce(tmp); y = rmsnorm(resid) * norm_w (the TP decode residual step)."""
+    def all_reduce_rmsnorm(self, tmp, resid, norm_w, y, eps: float, part=None, nsplit: int = 0) -> None:
+        """resid += all_reduce(tmp); y = rmsnorm(resid) * norm_w (the TP decode residual step).  part / nsplit: this
+        rank's partial product is still `nsplit` fp32 split-K slabs (gemm_out_split), summed by the IPC kernel
+        itself; only valid when the IPC context serves these rows (ipc_rows)."""
         from .. import ops
 
         if self.fast_ar is not None and tmp.shape[0] <= self.fast_ar.rows:
-            self.fast_ar(tmp, resid, norm_w, y, eps)
+            self.fast_ar(tmp, resid, norm_w, y, eps, part, nsplit)
             return
+        assert nsplit == 0, "split-K slabs need the IPC all-reduce"
         self.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, y, eps, delta=tmp)
+
+    def ipc_rows(self, rows: int) -> bool:
+        """The IPC all-reduce serves `rows` rows (so the O / down GEMM may leave its split-K slabs to it)."""
+        return self.size > 1 and self.fast_ar is not None and rows <= self.fast_ar.rows
 
 
 class IpcAllReduce:
@@ -215,9 +222,9 @@ class IpcAllReduce:
             torch.ops.dsse.ar_close(int(self.own_ptr), False)
         self.peer_ptrs, self.own_ptr = [], 0
 
-    def __call__(self, tmp, resid, norm_w, y, eps: float) -> None:
+    def __call__(self, tmp, resid, norm_w, y, eps: float, part=None, nsplit: int = 0) -> None:
         torch.ops.dsse.ar_rmsnorm(tmp, resid, norm_w, y, eps, self.peers, self.comm.rank, self.rows, self.epoch,
-                                  self.err)
+                                  self.err, part if nsplit > 0 else None, nsplit)
 
     GATHER_ROW_FLOATS = 32  # allreduce.hip kGatherRowBytes / 4: 16 vocab chunks x (score, index)
 

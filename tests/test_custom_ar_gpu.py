@@ -200,3 +200,40 @@ def test_ipc_allreduce_graph_replay_multiprocess(gpu, world, buckets):
         assert r["bad"] == [], r["bad"][:5]
         assert r["closed"]
     assert all(r["digest"] == res[0]["digest"] for r in res)
+
+
+@pytest.mark.parametrize("M,S", [(1, 2), (37, 2), (64, 4), (64, 7)])
+def test_ar_rmsnorm_sums_split_k_slabs(gpu, M, S):
+    """Round 6: the IPC all-reduce + RMSNorm kernel takes the O / down GEMM's fp32 split-K slabs directly (part /
+    nsplit) -- bit for bit what the splitk_reduce_kernel -> bf16 tmp -> ar_rmsnorm chain gives (one rank, its own
+    buffer as the only peer: the kernel, the flags and the epochs run as in a TP group)."""
+    from distributed_sse_for_llm_response_amd import ops
+
+    ops.load_library(required=True)
+    rows, H = 64, 4096
+    _, ptr, _ = torch.ops.dsse.ar_alloc(rows, H)
+    try:
+        peers = torch.tensor([ptr], dtype=torch.int64, device=gpu)
+        epoch = torch.zeros(rows, dtype=torch.int32, device=gpu)
+        err = torch.zeros(1, dtype=torch.int32, device=gpu)
+        g = torch.Generator().manual_seed(M * 10 + S)
+        slabs = torch.randn(S, M, H, generator=g).to(gpu)
+        acc = torch.zeros(M, H, device=gpu)
+        for s in range(S):  # the kernel's summation order
+            acc += slabs[s]
+        tmp = acc.bfloat16()
+        resid = torch.randn(M, H, generator=g).to(gpu)
+        w = (1 + 0.1 * torch.randn(H, generator=g)).bfloat16().to(gpu)
+        r1, r2 = resid.clone(), resid.clone()
+        y1 = torch.empty(M, H, device=gpu, dtype=torch.bfloat16)
+        y2 = torch.empty_like(y1)
+        torch.ops.dsse.ar_rmsnorm(tmp, r1, w, y1, 1e-5, peers, 0, rows, epoch, err)
+        torch.ops.dsse.ar_rmsnorm(torch.zeros_like(tmp), r2, w, y2, 1e-5, peers, 0, rows, epoch, err,
+                                  slabs.view(-1), S)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert torch.equal(r1, r2) and torch.equal(y1, y2)
+        assert torch.allclose(r1, resid + tmp.float(), atol=0, rtol=0)
+    finally:
+        torch.cuda.synchronize()
+        torch.ops.dsse.ar_close(int(ptr), False)

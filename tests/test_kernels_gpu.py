@@ -427,6 +427,37 @@ def test_paged_attention_decode(gpu, ctxs, part):
     _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention")
 
 
+@pytest.mark.parametrize("ctxs", [[1, 31, 32, 33, 300], [2000, 4096, 77], [1, 1, 1], [560] * 8])
+@pytest.mark.parametrize("nparts", [2, 4, 8])
+def test_paged_attention_decode_even_partitions(gpu, ctxs, nparts):
+    """part = 0 (round 6): every sequence's keys split evenly over the nparts flash-decoding partitions in whole
+    pages (attention.hip part_keys) instead of fixed max-context partitions; against the fp32 reference."""
+    g = torch.Generator().manual_seed(sum(ctxs) + nparts)
+    B = len(ctxs)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, [1] * B, gen=g)
+    qlen = torch.ones(B, dtype=torch.int32)
+    qlen[-1] = 0 if B > 3 else 1  # an inactive slot
+    ctx = torch.tensor(ctxs, dtype=torch.int32)
+    ws, wt = torch.arange(B, dtype=torch.int32), torch.zeros(B, dtype=torch.int32)
+    out = torch.zeros_like(q)
+    out_g = torch.zeros_like(q).to(gpu)
+    po = torch.zeros(B * 8 * nparts * 16 * 128, device=gpu)
+    pml = torch.zeros(B * 8 * nparts * 16 * 2, device=gpu)
+    ops.paged_attention(0, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
+                        ws.to(gpu), wt.to(gpu), out_g, po, pml, 0, nparts)
+    R.paged_attention(0, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
+    live = qlen.bool()
+    _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention, even partitions")
+
+
+@pytest.mark.parametrize("kwv", ["1", "2", "4"])
+@pytest.mark.parametrize("M,nparts", [(9, 4), (64, 8)])
+def test_qkv_attention_decode_folded_even_partitions(gpu, monkeypatch, kwv, M, nparts):
+    """The folded QKV path with even per-sequence partitions (part = 0): the partition holding the newest key (and
+    its key-split wave) writes that token's K / V, the others attend over their share."""
+    _folded_case(gpu, monkeypatch, "auto", M, 0, kwv, nparts=nparts)
+
+
 @pytest.mark.parametrize("cfg", ["auto", "stream-nw4-split4", "wide-split2-rd", "tiled-default", "tiled-128-split2",
                                  "skinny-default"])
 @pytest.mark.parametrize("M,part", [(1, 128), (9, 512), (64, 128), (64, 8192), (200, 256), (256, 8192)])
@@ -444,7 +475,7 @@ def test_qkv_attention_decode_folded_key_split_waves(gpu, monkeypatch, kwv, M, p
     _folded_case(gpu, monkeypatch, "auto", M, part, kwv)
 
 
-def _folded_case(gpu, monkeypatch, cfg, M, part, kwv):
+def _folded_case(gpu, monkeypatch, cfg, M, part, kwv, nparts=None):
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(**GEMM_CONFIGS[cfg]))
     if kwv is not None:
         monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(attn_kwv=kwv))
@@ -461,7 +492,7 @@ def _folded_case(gpu, monkeypatch, cfg, M, part, kwv):
     x = _rand(M, H, dev=gpu, gen=g)
     w = R.tile_weight(_rand((nh + 2 * nkv) * 128, H, dev=gpu, scale=1 / 32, gen=g))
     rope = R.rope_table(1024, 1e6, gpu)
-    nparts = math.ceil(int(ctx.max()) / part)
+    nparts = nparts or math.ceil(int(ctx.max()) / part)
     dev = {k: t.to(gpu) for k, t in dict(bt=bt, ctx=ctx, qlen=qlen, pos=pos, slots=slots,
                                          qs=torch.arange(M, dtype=torch.int32), ws=torch.arange(M, dtype=torch.int32),
                                          wt=torch.zeros(M, dtype=torch.int32)).items()}
@@ -668,3 +699,50 @@ def test_decode_gemms_at_tp_shard_shapes(gpu, tp, M):
             ops.gemm_out(x, w, out)
             R.gemm_out(x, w, ref)
             _close(out, ref, 1e-3, 1e-2, f"{name} tp={tp} M={M}")
+
+
+@pytest.mark.parametrize("M", [17, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 1792), (4096, 512), (768, 4096), (3584, 4096)])
+def test_tp8_shard_shapes_out_and_split_slabs(gpu, M, N, K):
+    """A TP = 8 rank's decode projections (qkv N 768, o K 512, gate_up N 3584, down K 1792): gemm_out against the fp32
+    reference, and gemm_out_split's fp32 slabs (when it splits; the IPC all-reduce sums them) against the same.  K =
+    1792 runs the LDS-DMA ring kernel since round 6 (K % 128, not K % 512)."""
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / math.sqrt(K), gen=g))
+    ref = x.float() @ R.untile_weight(w).float().t()
+    out = torch.zeros(M, N, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_out(x, w, out)
+    _close(out, ref, 2e-2, 1e-2, "gemm_out")
+    if K == 1792:
+        impl = torch.ops.dsse.gemm_plan(M, N, K)[0]
+        assert impl == 2, f"K = 1792 at {M} rows should take the ring kernel, got impl {impl}"
+    part = torch.full((16 * M * N,), float("nan"), device=gpu)
+    out2 = torch.zeros(M, N, device=gpu, dtype=torch.bfloat16)
+    ns = ops.gemm_out_split(x, w, out2, part)
+    if ns > 0:
+        s = part[: ns * M * N].view(ns, M, N).sum(0)
+        _close(s, ref, 1e-3, 1e-3, f"{ns} slabs")
+    else:
+        _close(out2, ref, 2e-2, 1e-2, "gemm_out_split (no split)")
+
+
+@pytest.mark.parametrize("M", [17, 33, 64])
+@pytest.mark.parametrize("fix", ["1", "0"])
+def test_ring_silu_split_k_fix_up(gpu, monkeypatch, M, fix):
+    """gate_up of a TP = 8 rank (N 3584) at decode rows: the ring kernel splits K and (s_fix=1, the default since
+    round 6) combines the slices inside the launch, else slabs + splitk_reduce; both against the fp32 reference."""
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(s_fix=fix))
+    ops.refresh_env()
+    g = torch.Generator().manual_seed(M + int(fix))
+    N, K = 3584, 4096
+    x = _rand(M, K, dev=gpu, gen=g)
+    w = R.tile_weight(_rand(N, K, dev=gpu, scale=1 / 64, gen=g))
+    out = torch.zeros(M, N // 2, device=gpu, dtype=torch.bfloat16)
+    for _ in range(3):
+        ops.gemm_silu(x, w, out)
+    gu = (x.float() @ R.untile_weight(w).float().t()).view(M, N // 16, 16)
+    ref = (torch.nn.functional.silu(gu[..., :8]) * gu[..., 8:]).reshape(M, N // 2)
+    _close(out, ref, 2e-2, 2e-2, f"ring silu s_fix={fix}")
+    torch.cuda.synchronize()
+    assert torch.ops.dsse.gemm_fix_timeouts(gpu.index or 0) == 0

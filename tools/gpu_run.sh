@@ -65,6 +65,10 @@ for s in "$@"; do
     sdef40j08) DSSE_JIT_MARGIN_MS=0.8 step sdef40j08 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
     sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
+    sdef40_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef40_768 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
+    sdef13_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef13_768 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
+    tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
+    r6_tests) step r6_tests 900 $PYT tests/test_kernels_gpu.py -k "tp8_shard or even_partitions or paged_attention_decode or folded" tests/test_custom_ar_gpu.py tests/test_gemm_tiled_gpu.py tests/test_model_full_dims_gpu.py tests/test_tp_graph_gpu.py ;;
     soak) step soak 900 python3 tools/bench_serving.py --rates 40 --requests 2000 --max-tokens 200 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
     gemm_test) step gemm_test 600 $PYT tests/test_gemm_tiled_gpu.py ;;
