@@ -820,6 +820,11 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
                                    out, part_o, part_ml, part, nparts, mode == 0 ? 1 : 4, mode == 0 ? 4 : 1);
   p.q = reinterpret_cast<const bf16*>(q.data_ptr());
   const int num_work = (int)work_seq.numel();
+  if (mode == 2) {
+    // flash prefill: q heads per workgroup (flash_hg in DSSE_KERNEL_CFG; 0 = the launcher's rule)
+    const int hg = env_int("flash_hg", 0);
+    p.kwv = (hg == 1 || hg == 2 || hg == 4) && (hq / hkv) % hg == 0 ? hg : 0;
+  }
   if (mode == 2) DSSE_CHECK_HIP(dsse_flash_prefill(num_work, &p, cur_stream()));
   else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
 }

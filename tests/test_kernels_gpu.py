@@ -548,6 +548,34 @@ def test_paged_attention_prefill(gpu, case, mode, hq):
     _close(out_g, out, 1e-2, 2e-2, f"prefill attention mode {mode}")
 
 
+@pytest.mark.parametrize("hg", ["auto", "1", "2", "4"])
+@pytest.mark.parametrize("case", [([4096], [4096]), ([4800, 300], [4096, 300]), ([200], [200])])
+def test_flash_prefill_one_kv_head_head_split(gpu, monkeypatch, case, hg):
+    """A TP = 8 rank's prompt attention (4 q heads on ONE kv head): the flash kernel with the group's q heads split
+    over 1 / 2 / 4 workgroups (flash_hg; auto = 2 from 64 query tiles when fewer than 256 workgroups, round 6)."""
+    if hg != "auto":
+        monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(flash_hg=hg))
+        ops.refresh_env()
+    ctxs, qlens = case
+    g = torch.Generator().manual_seed(sum(ctxs) + len(hg))
+    B = len(ctxs)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, qlens, hq=4, hkv=1, gen=g)
+    qlen, ctx = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
+    ws, wt = [], []
+    for b in range(B):
+        for t in reversed(range(math.ceil(qlens[b] / 64))):
+            ws.append(b)
+            wt.append(t)
+    ws, wt = torch.tensor(ws, dtype=torch.int32), torch.tensor(wt, dtype=torch.int32)
+    out = torch.zeros_like(q)
+    out_g = torch.zeros_like(q).to(gpu)
+    dummy = torch.zeros(1, device=gpu)
+    ops.paged_attention(2, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
+                        ws.to(gpu), wt.to(gpu), out_g, dummy, dummy, math.ceil(max(ctxs) / 32) * 32, 1)
+    R.paged_attention(2, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
+    _close(out_g, out, 1e-2, 2e-2, f"flash prefill, one kv head, hg {hg}")
+
+
 def _sampler_inputs(B, V, gen, temps, topk, topp):
     logits = torch.randn(B, V, generator=gen) * 3
     t = torch.tensor(temps, dtype=torch.float32)

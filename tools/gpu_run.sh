@@ -68,6 +68,15 @@ for s in "$@"; do
     sdef40_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef40_768 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
     sdef13_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef13_768 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
+    r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
+    flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
+      for hg in 4 2 1; do DSSE_KERNEL_CFG=flash_hg=$hg step "flash_tp8_hg$hg" 300 python -u tools/bench_prefill_attn.py --T 8192,2048 --hq 4 --hkv 1; done ;;
+    prof_tp8)  # kernel traces of one TP = 8 rank: 64-stream decode step and 8k prefill
+      step prof_tp8_dec 300 rocprofv3 --kernel-trace -d "$out/prof_tp8_dec" -o run --output-format csv -- python3 tools/bench_tp_rank.py --tp 8 --phase decode --steps 20 --profile-marker
+      python3 tools/trace_sum.py "$(ls "$out"/prof_tp8_dec/*/run_kernel_trace.csv "$out"/prof_tp8_dec/run_kernel_trace.csv 2>/dev/null | head -1)" --div 20 --after-kernel bitwise_not --title "TP=8 rank 0, 64-stream decode step (20 replays)" > "$out/prof_tp8_dec.md" 2>&1
+      step prof_tp8_pf 300 rocprofv3 --kernel-trace -d "$out/prof_tp8_pf" -o run --output-format csv -- python3 tools/bench_tp_rank.py --tp 8 --phase prefill --iters 3 --profile-marker
+      python3 tools/trace_sum.py "$(ls "$out"/prof_tp8_pf/*/run_kernel_trace.csv "$out"/prof_tp8_pf/run_kernel_trace.csv 2>/dev/null | head -1)" --div 3 --after-kernel bitwise_not --title "TP=8 rank 0, 8192-token prefill (3 prompts)" > "$out/prof_tp8_pf.md" 2>&1 ;;
+    r6_tests3) step r6_tests3 900 $PYT tests/test_kernels_gpu.py -k "one_kv_head or ring_silu or paged_attention_prefill" ;;
     r6_tests) step r6_tests 900 $PYT tests/test_kernels_gpu.py -k "tp8_shard or even_partitions or paged_attention_decode or folded" tests/test_custom_ar_gpu.py tests/test_gemm_tiled_gpu.py tests/test_model_full_dims_gpu.py tests/test_tp_graph_gpu.py ;;
     soak) step soak 900 python3 tools/bench_serving.py --rates 40 --requests 2000 --max-tokens 200 ;;
     serving40) step serving40 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 --prefill-budget 256,512 --itl-ratios 0,2 ;;
