@@ -144,4 +144,7 @@ hipError_t dsse_check_attention_prefill(int* out, int clear);
 hipError_t dsse_check_elementwise(int* out, int clear);
 hipError_t dsse_check_sampler(int* out, int clear);
 hipError_t dsse_check_gemm_tiled(int* out, int clear);
+// Stamps build: bind the step-anatomy record buffer (common.h stamps::) of a kernel file; no-ops otherwise.
+hipError_t dsse_stamps_bind_gemm_stream(void* rec);
+hipError_t dsse_stamps_bind_elementwise(void* rec);
 }

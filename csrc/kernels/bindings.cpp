@@ -1146,6 +1146,40 @@ Tensor kernel_checks(bool clear) {
   for (int i = 0; i < 7; ++i) DSSE_CHECK_HIP(readers[i](out.data_ptr<int>() + 4 * i, clear ? 1 : 0));
   return out;
 }
+// Stamps build: step-anatomy records (common.h stamps::record) of the ring GEMMs and RMSNorms.  step_stamps_arm
+// (re)binds an empty buffer of `cap` records on `device` (cap 0 unbinds); step_stamps_read returns the records so
+// far as [n, 8] int64 (tag, grid, block, t0..t3, wave).  Both synchronise the device; empty in the default build.
+std::unordered_map<int, Tensor>& stamp_bufs() {
+  static std::unordered_map<int, Tensor> m;
+  return m;
+}
+bool step_stamps_arm(int64_t device, int64_t cap) {
+  if (!DSSE_PIPE_STAMPS) return false;
+  const at::Device dev(at::kCUDA, (c10::DeviceIndex)device);
+  DSSE_CHECK_HIP(hipDeviceSynchronize());
+  void* p = nullptr;
+  if (cap > 0) {
+    Tensor buf = at::zeros({8 + 8 * cap}, at::TensorOptions().dtype(at::kLong).device(dev));
+    const int64_t hdr[2] = {0, cap};
+    DSSE_CHECK_HIP(hipMemcpy(buf.data_ptr(), hdr, sizeof hdr, hipMemcpyHostToDevice));
+    stamp_bufs()[dev.index()] = buf;
+    p = buf.data_ptr();
+  } else {
+    stamp_bufs().erase(dev.index());
+  }
+  DSSE_CHECK_HIP(dsse_stamps_bind_gemm_stream(p));
+  DSSE_CHECK_HIP(dsse_stamps_bind_elementwise(p));
+  return true;
+}
+Tensor step_stamps_read(int64_t device) {
+  auto it = stamp_bufs().find((int)device);
+  if (!DSSE_PIPE_STAMPS || it == stamp_bufs().end()) return at::empty({0, 8}, at::kLong);
+  DSSE_CHECK_HIP(hipDeviceSynchronize());
+  Tensor h = it->second.cpu();
+  const int64_t n = std::min(h[0].item<int64_t>(), h[1].item<int64_t>());
+  return h.narrow(0, 8, 8 * n).view({n, 8}).clone();
+}
+
 std::string kernel_check_files() {
   std::string s;
   for (const char* f : kCheckFiles) s += std::string(s.empty() ? "" : ",") + f;
@@ -1195,6 +1229,8 @@ TORCH_LIBRARY(dsse, m) {
   m.def("gemm_plan(int M, int N, int K, bool slab_consumer=False) -> (int, int, int, bool, float)", &gemm_plan);
   m.def("gemm_fix_timeouts(int device=0) -> int", &gemm_fix_timeouts);
   m.def("gemm_fix_stamps(int device=0) -> Tensor", &gemm_fix_stamps);
+  m.def("step_stamps_arm(int device=0, int cap=0) -> bool", &step_stamps_arm);
+  m.def("step_stamps_read(int device=0) -> Tensor", &step_stamps_read);
   m.def("kernels_checked() -> bool", &kernels_checked);
   m.def("kernel_checks(bool clear=True) -> Tensor", &kernel_checks);
   m.def("kernel_check_files() -> str", &kernel_check_files);

@@ -149,4 +149,57 @@ DEV int check_index(int v, int bound, int line, int fallback) {
   }
 #endif
 
+// ---- Step anatomy stamps (diagnostic `stamps` build only, DSSE_PIPE_STAMPS; tools/step_stamps.py).  Workgroup
+// 0-thread records of s_memrealtime (100 MHz, one clock for every CU): [tag, grid x | grid y << 32, block x |
+// block y << 32, t0 entry, t1 first operands landed, t2 main loop done, t3 stores drained, 0] appended to a
+// per-translation-unit device buffer that the host binds (torch.ops.dsse.step_stamps_*): word 0 counts records,
+// word 1 is the capacity.  In the default build every call below compiles to nothing.
+#ifndef DSSE_PIPE_STAMPS
+#define DSSE_PIPE_STAMPS 0
+#endif
+namespace stamps {
+enum Tag { kRing = 1, kNorm = 2, kAttn = 3, kPipe = 4 };
+DEV unsigned long long now() {
+#if DSSE_PIPE_STAMPS
+  return __builtin_amdgcn_s_memrealtime();
+#else
+  return 0ull;
+#endif
+}
+#if DSSE_PIPE_STAMPS
+static __device__ unsigned long long* g_rec;
+#endif
+// t3 is taken here, after this wave's stores drained (vmcnt(0)); call from one wave, after its last store
+DEV void record(int tag, unsigned long long t0, unsigned long long t1, unsigned long long t2) {
+#if DSSE_PIPE_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t3 = now();
+  unsigned long long* rec = g_rec;
+  if ((threadIdx.x & 63) == 0 && rec) {
+    const unsigned long long n = atomicAdd(rec, 1ull);
+    if (n < rec[1]) {
+      unsigned long long* r = rec + 8 + 8 * n;
+      r[0] = (unsigned long long)tag;
+      r[1] = gridDim.x | ((unsigned long long)gridDim.y << 32);
+      r[2] = blockIdx.x | ((unsigned long long)blockIdx.y << 32);
+      r[3] = t0;
+      r[4] = t1;
+      r[5] = t2;
+      r[6] = t3;
+      r[7] = threadIdx.x >> 6;
+    }
+  }
+#endif
+}
+}  // namespace stamps
+#if DSSE_PIPE_STAMPS
+#define DSSE_STAMPS_BINDER(fn)                                                                  \
+  extern "C" hipError_t fn(void* p) {                                                            \
+    return hipMemcpyToSymbol(HIP_SYMBOL(::dsse::stamps::g_rec), &p, sizeof(p));                 \
+  }
+#else
+#define DSSE_STAMPS_BINDER(fn) \
+  extern "C" hipError_t fn(void*) { return hipSuccess; }
+#endif
+
 }  // namespace dsse

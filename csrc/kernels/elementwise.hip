@@ -24,6 +24,7 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
                const bf16* __restrict__ w, bf16* __restrict__ y, float eps,
                const float* __restrict__ part = nullptr, int nsplit = 0, int M = 0, int vocab = 0) {
   const int m = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const unsigned long long st0 = stamps::now();
   float* rrow = resid + (size_t)m * H;
   constexpr int kMaxIt = 2;  // H <= 8192
   float4 v[kMaxIt];
@@ -73,6 +74,8 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
       ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
     }
   }
+  if (DSSE_PIPE_STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long st1 = stamps::now();  // the row's values (and slab sums) landed
   ss = wave_sum(ss);
   __shared__ float red[16];
   if ((tid & 63) == 0) red[tid >> 6] = ss;
@@ -80,6 +83,7 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
   float tot = 0.f;
   for (int i = 0; i < (nt >> 6); ++i) tot += red[i];
   const float inv = rsqrtf(tot / (float)H + eps);
+  const unsigned long long st2 = stamps::now();
 #pragma unroll
   for (int it = 0; it < kMaxIt; ++it) {
     if (it < nit) {
@@ -92,6 +96,7 @@ rmsnorm_kernel(float* __restrict__ resid, int H, const bf16* __restrict__ delta,
       *reinterpret_cast<bf16x4*>(y + (size_t)m * H + i) = o;
     }
   }
+  stamps::record(stamps::kNorm | MODE << 8, st0, st1, st2);
 }
 
 // ---- K4 (prefill side): RoPE on q/k + paged KV write from a library-GEMM QKV output ----------
@@ -302,3 +307,4 @@ extern "C" hipError_t dsse_ring_advance(int* counter, hipStream_t st) {
 }
 
 DSSE_CHECK_READER(dsse_check_elementwise)
+DSSE_STAMPS_BINDER(dsse_stamps_bind_elementwise)

@@ -334,6 +334,8 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   constexpr int PER = XI + 4;             // VMEM instructions per wave per chunk
   constexpr int WAUX = kAuxNT;  // weights streamed once: non-temporal
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const unsigned long long st0 = stamps::now();
+  unsigned long long st1 = 0;
 
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -387,6 +389,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
       if (u > 0 && c0 + u >= nch) break;
       // chunk c0 + u landed for every wave, chunks up to c0 + u + D - 2 still in flight
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((D - 2) * PER) : "memory");
+      if (DSSE_PIPE_STAMPS && c0 + u == 0) st1 = stamps::now();
       const char* xb = smem + u * G::SLOT;
       const char* wb = xb + G::SLOTX + w * 4096 + lane * 16;
 #pragma unroll
@@ -406,6 +409,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   }
   // no LDS-DMA may still be landing when the workgroup's LDS is handed to the next workgroup
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long st2 = stamps::now();
 
   if constexpr (FIX) {
     const int S = gridDim.y;
@@ -431,6 +435,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_fetch_add(cnt + kFixTiles + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        stamps::record(stamps::kRing | MODE << 8 | FIX << 12, st0, st1, st2);
         return;
       }
       if (threadIdx.x == 0) {
@@ -463,6 +468,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
   if constexpr (MODE == kSiluMul) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) silu_epilogue4(ep, M, 16 * mt + 4 * g, tgi, r, acc[mt]);
+    stamps::record(stamps::kRing | MODE << 8 | FIX << 12, st0, st1, st2);
     return;
   }
 #pragma unroll
@@ -473,6 +479,7 @@ gemm_ring_kernel(const bf16* __restrict__ X, int ldx, int M, const bf16* __restr
       const float partner = MODE == kQkvRope ? __shfl_xor(v, 8) : 0.f;
       epilogue<MODE>(ep, part_ks, M, N, 16 * mt + 4 * g + i, tgi, r, v, partner);
     }
+  stamps::record(stamps::kRing | MODE << 8 | FIX << 12, st0, st1, st2);
 }
 
 template <int MT, int NW, int D, int MODE, bool FIX = false>
@@ -781,3 +788,4 @@ extern "C" size_t dsse_gemm_ring_fix_floats(int nw, int S, int M, int N) {
 }
 
 DSSE_CHECK_READER(dsse_check_gemm_stream)
+DSSE_STAMPS_BINDER(dsse_stamps_bind_gemm_stream)

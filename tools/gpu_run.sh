@@ -76,6 +76,13 @@ for s in "$@"; do
       python3 tools/trace_sum.py "$(ls "$out"/prof_tp8_dec/*/run_kernel_trace.csv "$out"/prof_tp8_dec/run_kernel_trace.csv 2>/dev/null | head -1)" --div 20 --after-kernel bitwise_not --title "TP=8 rank 0, 64-stream decode step (20 replays)" > "$out/prof_tp8_dec.md" 2>&1
       step prof_tp8_pf 300 rocprofv3 --kernel-trace -d "$out/prof_tp8_pf" -o run --output-format csv -- python3 tools/bench_tp_rank.py --tp 8 --phase prefill --iters 3 --profile-marker
       python3 tools/trace_sum.py "$(ls "$out"/prof_tp8_pf/*/run_kernel_trace.csv "$out"/prof_tp8_pf/run_kernel_trace.csv 2>/dev/null | head -1)" --div 3 --after-kernel bitwise_not --title "TP=8 rank 0, 8192-token prefill (3 prompts)" > "$out/prof_tp8_pf.md" 2>&1 ;;
+    stamps64)  # step anatomy from in-kernel stamps (stamps build) + the same runner's counters (eager steps)
+      DSSE_KERNELS_VARIANT=stamps step stamps64 300 python3 tools/step_stamps.py --streams 64 --steps 4 --out "$out/stamps64.json" ;;
+    pmc64)
+      step pmc64_a 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc64_a" -o run --output-format csv -- python3 tools/step_stamps.py --pmc-pass --steps 3 --warmup 1
+      step pmc64_b 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc64_b" -o run --output-format csv -- python3 tools/step_stamps.py --pmc-pass --steps 3 --warmup 1
+      step pmc64_c 180 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc64_c" -o run --output-format csv -- python3 tools/step_stamps.py --pmc-pass --steps 3 --warmup 1
+      python3 tools/pmc_sum.py "$out/pmc64_a" "$out/pmc64_b" "$out/pmc64_c" --kernel "gemm_ring|rmsnorm_kernel<3>|paged_attention" --title "64-stream decode step kernels (eager steps)" > "$out/pmc64.md" 2>&1 ;;
     r6_tests3) step r6_tests3 900 $PYT tests/test_kernels_gpu.py -k "one_kv_head or ring_silu or paged_attention_prefill" ;;
     r6_tests) step r6_tests 900 $PYT tests/test_kernels_gpu.py -k "tp8_shard or even_partitions or paged_attention_decode or folded" tests/test_custom_ar_gpu.py tests/test_gemm_tiled_gpu.py tests/test_model_full_dims_gpu.py tests/test_tp_graph_gpu.py ;;
     soak) step soak 900 python3 tools/bench_serving.py --rates 40 --requests 2000 --max-tokens 200 ;;
