@@ -520,24 +520,6 @@ class ModelRunner:
             self.decode_forward(B)
 
     # ------------------------------------------------------------------ prefill
-    def _comm_async(self, t):
-        """all_reduce(t) on the communication side stream, ordered after everything queued on the current stream;
-        returns the event the consumer waits for (None: done synchronously, CPU / gloo)."""
-        if not t.is_cuda:
-            self.comm.all_reduce(t)
-            return None
-        main = torch.cuda.current_stream(self.device)
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
-        ready = torch.cuda.Event()
-        ready.record(main)
-        self._side.wait_event(ready)
-        with torch.cuda.stream(self._side):
-            self.comm.all_reduce(t)
-        done = torch.cuda.Event()
-        done.record(self._side)
-        return done
-
     def _proj(self, a, wt, out) -> None:
         """out = a·wᵀ in bf16 on the engine's tiled-layout GEMMs (every row count: no library GEMM)."""
         ops.gemm_out(a, wt, out)
@@ -560,23 +542,49 @@ class ModelRunner:
         ops.rmsnorm(resid[own], norm_w, x[own], self.cfg.rms_eps, delta=summed)
         self.comm.all_gather_rows(x, x[own])
 
+    def _resid_async(self, tmp, resid, norm_w, x):
+        """Residual step of one row chunk on the communication side stream, ordered after everything queued on the
+        current stream: the sequence-sharded reduce-scatter -> add + RMSNorm of this rank's rows -> all-gather when
+        the chunk's rows divide by the TP degree, else all-reduce -> replicated norm.  Returns the event the consumer
+        of x waits for (None: done synchronously, CPU / gloo)."""
+        sharded = tmp.shape[0] % self.comm.size == 0
+        if not tmp.is_cuda:
+            if sharded:
+                self._seq_sharded_norm(tmp, resid, norm_w, x)
+            else:
+                self.comm.all_reduce(tmp)
+                ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
+            return None
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self._side.wait_event(ready)
+        with torch.cuda.stream(self._side):
+            if sharded:
+                self._seq_sharded_norm(tmp, resid, norm_w, x)
+            else:
+                self.comm.all_reduce(tmp)
+                ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
+        done = torch.cuda.Event()
+        done.record(self._side)
+        return done
+
     def _prefill_post_attention(self, T: int, attn, L, w_next, resid, x, h, tmp) -> None:
         """resid += all_reduce(attn·Woᵀ); x = norm(resid); resid += all_reduce(silu-mlp(x)); x = norm(resid)·w_next.
 
-        TP, one chunk: whenever the rows divide by the TP degree, each all-reduce + replicated norm is the
-        sequence-sharded reduce-scatter -> norm on T / t rows -> all-gather (_seq_sharded_norm; VERDICT r5 missing 3):
-        the same exposed bytes as the all-reduce, 1 / t of the norm.  The chunked form below keeps the all-reduce:
-        there every chunk's all-reduce hides under the next chunks' GEMMs, while the all-gather half of the sharded
-        form would be exposed -- the next layer's column-parallel QKV needs every row of x on every rank, so the last
-        residual step's all-gathers (the whole 64 MiB at 8k rows, per layer) would have nothing left to hide under
-        (docs/operations.md, TP prefill).
+        TP: whenever the rows divide by the TP degree, each all-reduce + replicated norm is the sequence-sharded
+        reduce-scatter -> norm on T / t rows -> all-gather (_seq_sharded_norm; VERDICT r5 missing 3): the same bytes
+        on the wire as the all-reduce (a ring all-reduce is reduce-scatter + all-gather), 1 / t of the norm work.
 
         TP prefill of >= DSSE_TP_PREFILL_OVERLAP_MIN rows: these ops are row-independent, so they run in row chunks and
-        every chunk's all-reduce is issued on a side stream the moment its GEMM is done -- the O all-reduces of chunk i
-        under the O GEMM of chunk i + 1 and the MLP of chunk i - 1, the down all-reduces under the next chunks' MLP;
-        only the last chunk's second all-reduce is exposed (1 / 2n of the layer's communication, n chunks).  Every rank
-        issues the collectives in the same order.  TP = 1 or short prompts: the unchunked chain."""
-        eps = self.cfg.rms_eps
+        every chunk's residual step (collectives + its 1 / t of the norm) is issued on a side stream the moment its
+        GEMM is done -- the O steps of chunk i under the O GEMM of chunk i + 1 and the MLP of chunk i - 1, the down
+        steps under the next chunks' MLP; only the last chunk's second step is exposed (1 / 2n of the layer's
+        communication, n chunks).  Each rank's residual rows are then updated on the side stream only (nothing on the
+        main stream reads resid).  Every rank issues the collectives in the same order.  TP = 1 or short prompts: the
+        unchunked chain."""
         chunks = prefill_row_chunks(T, self.comm.size)
         if len(chunks) == 1:
             self._prefill_resid(attn, L.wo_t, resid, L.ffn_norm, x, tmp)
@@ -584,22 +592,20 @@ class ModelRunner:
             self._prefill_resid(h, L.wd_t, resid, w_next, x, tmp)
             return
         main = torch.cuda.current_stream(self.device) if tmp.is_cuda else None
-        ar1 = []
+        ev1 = []
         for a, b in chunks:
             self._proj(attn[a:b], L.wo_t, tmp[a:b])
-            ar1.append(self._comm_async(tmp[a:b]))
-        ar2 = []
-        for (a, b), ev in zip(chunks, ar1):
+            ev1.append(self._resid_async(tmp[a:b], resid[a:b], L.ffn_norm, x[a:b]))
+        ev2 = []
+        for (a, b), ev in zip(chunks, ev1):
             if ev is not None:
                 main.wait_event(ev)
-            ops.rmsnorm(resid[a:b], L.ffn_norm, x[a:b], eps, delta=tmp[a:b])
             self._gate_up(x[a:b], L, h[a:b])
-            self._proj(h[a:b], L.wd_t, tmp[a:b])  # tmp rows [a, b) are free: their O all-reduce was consumed
-            ar2.append(self._comm_async(tmp[a:b]))
-        for (a, b), ev in zip(chunks, ar2):
+            self._proj(h[a:b], L.wd_t, tmp[a:b])  # tmp rows [a, b) are free: their O step was waited for
+            ev2.append(self._resid_async(tmp[a:b], resid[a:b], w_next, x[a:b]))
+        for ev in ev2:
             if ev is not None:
                 main.wait_event(ev)
-            ops.rmsnorm(resid[a:b], w_next, x[a:b], eps, delta=tmp[a:b])
 
     def _prefill_resid(self, a, wt, resid, norm_w, x, tmp) -> None:
         """resid += a·wᵀ, x = RMSNorm(resid).  Thousands of rows: the product goes out as a bf16 tile (row-contiguous

@@ -10,9 +10,9 @@ every byte local (ShardComm below):
   * the decode step's two residual all-reduces per layer run the hand-written IPC all-reduce + RMSNorm kernel
     (allreduce.hip) of a one-rank IPC context -- the production kernel and launch sequence, minus the xGMI wait;
   * the sampling candidates' all-gather is a local replicate (copy kernel) instead of the IPC gather kernel;
-  * prefill: the chunked TP path (>= 1024 rows: O / down partial products all-reduced per row chunk on a side
-    stream) with the all-reduce itself a no-op, and the sequence-sharded reduce-scatter / all-gather of shorter
-    passes as local copies.
+  * prefill: the chunked TP path (>= 1024 rows: each row chunk's residual step -- reduce-scatter, add + RMSNorm of
+    this rank's 1 / t of the rows, all-gather -- on a side stream) with the reduce-scatter a local copy of this
+    rank's rows and the all-gather a no-op (its rows would come from the peers).
 
 So the numbers are this rank's compute + the launch structure of a real TP group, not its communication: the xGMI
 transfer time of the collectives comes on top (docs/operations.md, "TP = 8 budget").  Times: (a) the captured
@@ -80,10 +80,7 @@ def main():
             out.copy_(inp[: out.shape[0]])
 
         def all_gather_rows(self, out, own):
-            n = own.shape[0]
-            for q in range(self.size):
-                if out[q * n:(q + 1) * n].data_ptr() != own.data_ptr():
-                    out[q * n:(q + 1) * n].copy_(own)
+            return None  # the other ranks' rows would arrive over xGMI; own already sits in place
 
         def broadcast(self, t, src=0):
             return None
