@@ -74,9 +74,10 @@ PREFILL_SLAB_ROWS = 512
 
 # Prompt-chunk sizes of the captured mixed steps: one graph per (decode bucket, C).  The engine sizes each step's
 # chunk from the measured step costs (engine.PassCost.mixed_chunk); a prompt longer than the chunk is split evenly.
-# B + C stays within MIXED_MAX_ROWS: above 512 rows every projection falls off a wave-quantisation cliff (576 rows
-# = three 256-row tiles: 1.5-2.2x the 512-row time, profiles/r5/serving_r5.md), so the largest chunk of bucket B is
-# 512 - B rounded down to 64 rows.
+# B + C stays within MIXED_MAX_ROWS.  Round 5 set 512 because of a GEMM cliff at 576 rows; the round-6 cost-model
+# dispatch removed that cliff (profiles/r6/gemm_model_r6.md), and 768 was re-measured with the serving bench at
+# 40 req/s: TTFT p50 29.5 vs 29.8 ms, ITL p99 13.4 vs 10.7 ms (profiles/r6/serving_r6.md).  The bigger chunks buy no
+# TTFT and cost ITL, so 512 stays.
 MIXED_CHUNKS = (128, 256, 384, 512)
 MIXED_MAX_ROWS = 512
 
@@ -460,7 +461,7 @@ class ModelRunner:
         tmax = self.pf.tmax if self.pf is not None else 0
         if fixed > 0:
             return [c for c in [self.mixed_chunk(B)] if B + c <= tmax]
-        top = (int(os.environ.get("DSSE_MIXED_MAX_ROWS_AB", MIXED_MAX_ROWS)) - B) // PREFILL_TILE * PREFILL_TILE
+        top = (MIXED_MAX_ROWS - B) // PREFILL_TILE * PREFILL_TILE
         sizes = sorted({c for c in MIXED_CHUNKS if c <= top} | ({top} if top >= MIXED_CHUNKS[0] else set()))
         return [c for c in sizes if B + c <= tmax]
 

@@ -65,9 +65,8 @@ for s in "$@"; do
     sdef40j08) DSSE_JIT_MARGIN_MS=0.8 step sdef40j08 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
     sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
-    sdef40_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef40_768 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
-    sdef13_768) DSSE_MIXED_MAX_ROWS_AB=768 step sdef13_768 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
+    tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
       for hg in 4 2 1; do DSSE_KERNEL_CFG=flash_hg=$hg step "flash_tp8_hg$hg" 300 python -u tools/bench_prefill_attn.py --T 8192,2048 --hq 4 --hkv 1; done ;;
