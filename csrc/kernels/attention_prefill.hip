@@ -418,17 +418,17 @@ hipError_t launch_stamped(int num_work, const dsse::AttnParams* p, hipStream_t s
 // Work items: (sequence, 64-query tile) pairs; grid = num_work x Hkv workgroups, kv head fastest.  Requires
 // G = Hq/Hkv in {1, 2, 4}.  (Splitting a kv head's q heads over G workgroups for short prompts -- 256 workgroups of
 // 2 waves instead of 64 of 8 at 512 tokens -- measured 38.9 vs 28.8 us and was dropped; profiles/r4.)
-// p->kwv (mode 2): q heads per workgroup, 0 = the rule below.  Round 6: a long prompt on ONE kv head (a TP = 8
-// rank: 4 q heads) is 128 workgroups of 8 waves at 8k tokens -- half the CUs idle, the causal tail on a few -- so
-// from 64 query tiles on fewer than 256 (tile, kv head) workgroups the q heads are split in two (256 workgroups of
-// 4 waves, each staging its K / V: the L2 serves the second copy).  Short prompts keep whole groups (the round-4
-// measurement above).
+// p->kwv (mode 2): q heads per workgroup (flash_hg in DSSE_KERNEL_CFG), 0 = the whole group.  Round 6 re-measured the
+// split for a long prompt on ONE kv head (a TP = 8 rank: 4 q heads, 128 workgroups of 8 waves at 8k tokens, half the
+// CUs idle): 2 q heads per workgroup 323 us, 1 q head 383 us, the whole group 264 us at T = 8192 (85 / 94 / 72 us
+// at 2048; profiles/r6/flash_tp8_r6.log) -- every split stages the same K / V once more per workgroup, and the LDS
+// fill, not the idle CUs, sets the time.
 extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p, hipStream_t st) {
   if (num_work <= 0) return hipSuccess;
   static const char* stamps = getenv("DSSE_FLASH_STAMPS");
   if (stamps != nullptr && stamps[0] != '\0') return launch_stamped(num_work, p, st, stamps);
   int hg = p->kwv;
-  if (hg == 0) hg = (p->group == 4 && num_work >= 64 && num_work * p->hkv < 256) ? 2 : p->group;
+  if (hg == 0) hg = p->group;
   switch (p->group) {
     case 1: return launch_flash<1, 1, false>(num_work, p, st, nullptr);
     case 2: return hg == 1 ? launch_flash<2, 1, false>(num_work, p, st, nullptr)

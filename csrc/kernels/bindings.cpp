@@ -473,9 +473,11 @@ void run_gemm(int mode, const Tensor& x, const Tensor& w, dsse::GemmEpi& ep) {
   }
   if (impl == 2) {
     const SCfg c = pick_stream(M, N, K, mode);
-    // SiLU·mul split over K (a TP rank's gate_up at 17-64 rows): slices combined inside the ring kernel (round 6)
-    // instead of slabs + a splitk_reduce launch; s_fix=0 (DSSE_KERNEL_CFG) keeps the reduce launch
-    if (c.S > 1 && mode == dsse::kSiluMul && M <= 64 && env_int("s_fix", 1)) {
+    // SiLU·mul split over K (a TP rank's gate_up at 17-64 rows): s_fix=1 (DSSE_KERNEL_CFG) combines the slices
+    // inside the ring kernel instead of slabs + a splitk_reduce launch.  Off by default: on a TP = 8 rank's 64-stream
+    // step the fix-up tail costs more than the launch it saves (gate_up 19-20 us vs 10 + 5 us; step 2.27 vs 2.08 ms,
+    // profiles/r6/tp8_rank_r6.md)
+    if (c.S > 1 && mode == dsse::kSiluMul && M <= 64 && env_int("s_fix", 0)) {
       at::Tensor ws = at::empty({(int64_t)dsse_gemm_ring_fix_floats(1, c.S, M, N)}, x.options().dtype(at::kFloat));
       ep.fix_cnt = fix_counters(x.device());
       const hipError_t e = stream_launch(mode, c, c.S, 2, x.data_ptr(), M, w.data_ptr(), K, N, &ep,

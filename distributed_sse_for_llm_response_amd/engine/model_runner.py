@@ -221,20 +221,10 @@ class ModelRunner:
             return
         for li, L in enumerate(w.layers):
             self._qkv_attention(li, L, B, x, part, nparts)
-            if comm.size == 1:  # split-K slabs of the residual projection reduced inside the norm
-                ns = ops.gemm_resid_split(self.attn[r], L.wo_t, resid, self.split_part)
-                ops.rmsnorm(resid, L.ffn_norm, x, eps, part=self.split_part, nsplit=ns)
-            else:
-                ops.gemm_out(self.attn[r], L.wo_t, self.tmp[r])
-                comm.all_reduce_rmsnorm(self.tmp[r], resid, L.ffn_norm, x, eps)
+            self._resid_proj(self.attn[r], L.wo_t, resid, L.ffn_norm, x, self.tmp[r])
             ops.gemm_silu(x, L.wgu_t, self.h[r])
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
-            if comm.size == 1:
-                ns = ops.gemm_resid_split(self.h[r], L.wd_t, resid, self.split_part)
-                ops.rmsnorm(resid, w_next, x, eps, part=self.split_part, nsplit=ns)
-            else:
-                ops.gemm_out(self.h[r], L.wd_t, self.tmp[r])
-                comm.all_reduce_rmsnorm(self.tmp[r], resid, w_next, x, eps)
+            self._resid_proj(self.h[r], L.wd_t, resid, w_next, x, self.tmp[r])
         ops.gemm_out(x, w.lm_head_t, self.logits[r])
         self._sample_commit(B)
         ops.ring_advance(self.ring_counter)

@@ -552,7 +552,7 @@ def test_paged_attention_prefill(gpu, case, mode, hq):
 @pytest.mark.parametrize("case", [([4096], [4096]), ([4800, 300], [4096, 300]), ([200], [200])])
 def test_flash_prefill_one_kv_head_head_split(gpu, monkeypatch, case, hg):
     """A TP = 8 rank's prompt attention (4 q heads on ONE kv head): the flash kernel with the group's q heads split
-    over 1 / 2 / 4 workgroups (flash_hg; auto = 2 from 64 query tiles when fewer than 256 workgroups, round 6)."""
+    over 1 / 2 / 4 workgroups (flash_hg; auto = the whole group, the measured best)."""
     if hg != "auto":
         monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(flash_hg=hg))
         ops.refresh_env()
@@ -758,8 +758,8 @@ def test_tp8_shard_shapes_out_and_split_slabs(gpu, M, N, K):
 @pytest.mark.parametrize("M", [17, 33, 64])
 @pytest.mark.parametrize("fix", ["1", "0"])
 def test_ring_silu_split_k_fix_up(gpu, monkeypatch, M, fix):
-    """gate_up of a TP = 8 rank (N 3584) at decode rows: the ring kernel splits K and (s_fix=1, the default since
-    round 6) combines the slices inside the launch, else slabs + splitk_reduce; both against the fp32 reference."""
+    """gate_up of a TP = 8 rank (N 3584) at decode rows: the ring kernel splits K and (s_fix=1, opt-in) combines the
+    slices inside the launch, else (the default) slabs + splitk_reduce; both against the fp32 reference."""
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(s_fix=fix))
     ops.refresh_env()
     g = torch.Generator().manual_seed(M + int(fix))

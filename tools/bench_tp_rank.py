@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--prefill", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--phase", default="both", choices=["both", "decode", "prefill"])
+    ap.add_argument("--attn-wgs", type=int, default=0,
+                    help="decode attention workgroup target of decode_partitioning (0 = the engine default, 512): "
+                         "fewer flash-decoding partitions per sequence for an A/B")
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch one bitwise_not kernel before the timed decode replays and one before the timed "
                          "prefills (tools/trace_sum.py --after-kernel bitwise_not keeps what follows)")
@@ -57,6 +60,12 @@ def main():
     from distributed_sse_for_llm_response_amd.parallel.comm import IpcAllReduce, TPComm
 
     ops.load_library(required=True)
+    if args.attn_wgs > 0:
+        import functools
+
+        from distributed_sse_for_llm_response_amd.engine import model_runner as mr
+
+        mr.decode_partitioning = functools.partial(mr.decode_partitioning, target_wgs=args.attn_wgs)
     device = torch.device("cuda", 0)
     torch.cuda.set_device(device)
     # a one-rank host group: the IPC context's handle exchange and self-test run over it
@@ -155,7 +164,7 @@ def main():
     out = {
         "tp": args.tp, "rank": 0, "model": cfg.name, "streams": B, "prompt_len": args.prompt_len,
         "decode_step_ms": None if step_ms is None else round(step_ms, 4), "decode_collectives": "ipc kernel, 1-rank context" if ipc else "local",
-        "prefill_tokens": args.prefill, "prefill_ms": [round(t, 3) for t in times],
+        "attn_wgs": args.attn_wgs or 512, "prefill_tokens": args.prefill, "prefill_ms": [round(t, 3) for t in times],
         "prefill_ms_min": round(min(times), 3) if times else None, "health": health,
         "shard": {"qkv_N": (w.nh + 2 * w.nkv) * 128, "o_K": w.nh * 128, "gate_up_N": 2 * w.ffn, "down_K": w.ffn,
                   "kv_heads": w.nkv, "vocab_local": w.vocab_local},

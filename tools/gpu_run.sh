@@ -66,6 +66,8 @@ for s in "$@"; do
     sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
     tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
+    tp8_attn)  # decode attention partitions at TP = 8 (one kv head, 64 streams): 512 / 256 / 128 / 64 workgroups
+      for wg in 256 128 64; do step "tp8_attn$wg" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode --attn-wgs $wg; done ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
