@@ -1149,21 +1149,23 @@ Tensor kernel_checks(bool clear) {
   return out;
 }
 // Stamps build: step-anatomy records (common.h stamps::record) of the ring GEMMs and RMSNorms.  step_stamps_arm
-// (re)binds an empty buffer of `cap` records on `device` (cap 0 unbinds); step_stamps_read returns the records so
-// far as [n, 8] int64 (tag, grid, block, t0..t3, wave).  Both synchronise the device; empty in the default build.
+// (re)binds an empty buffer of `cap` records per sub-buffer on `device` (cap 0 unbinds); step_stamps_read returns
+// the records so far as [n, 8] int64 (tag, grid, block, t0..t3, wave), sub-buffer by sub-buffer (the tool sorts them
+// by time).  Both synchronise the device; empty in the default build.
 std::unordered_map<int, Tensor>& stamp_bufs() {
   static std::unordered_map<int, Tensor> m;
   return m;
 }
 bool step_stamps_arm(int64_t device, int64_t cap) {
   if (!DSSE_PIPE_STAMPS) return false;
+  using namespace dsse::stamps;
   const at::Device dev(at::kCUDA, (c10::DeviceIndex)device);
   DSSE_CHECK_HIP(hipDeviceSynchronize());
   void* p = nullptr;
   if (cap > 0) {
-    Tensor buf = at::zeros({8 + 8 * cap}, at::TensorOptions().dtype(at::kLong).device(dev));
-    const int64_t hdr[2] = {0, cap};
-    DSSE_CHECK_HIP(hipMemcpy(buf.data_ptr(), hdr, sizeof hdr, hipMemcpyHostToDevice));
+    Tensor buf = at::zeros({kHeader + 8 * cap * kSubs}, at::TensorOptions().dtype(at::kLong).device(dev));
+    const int64_t hdr = cap;
+    DSSE_CHECK_HIP(hipMemcpy(buf.data_ptr(), &hdr, sizeof hdr, hipMemcpyHostToDevice));
     stamp_bufs()[dev.index()] = buf;
     p = buf.data_ptr();
   } else {
@@ -1174,12 +1176,18 @@ bool step_stamps_arm(int64_t device, int64_t cap) {
   return true;
 }
 Tensor step_stamps_read(int64_t device) {
+  using namespace dsse::stamps;
   auto it = stamp_bufs().find((int)device);
   if (!DSSE_PIPE_STAMPS || it == stamp_bufs().end()) return at::empty({0, 8}, at::kLong);
   DSSE_CHECK_HIP(hipDeviceSynchronize());
   Tensor h = it->second.cpu();
-  const int64_t n = std::min(h[0].item<int64_t>(), h[1].item<int64_t>());
-  return h.narrow(0, 8, 8 * n).view({n, 8}).clone();
+  const int64_t cap = h[0].item<int64_t>();
+  std::vector<Tensor> parts;
+  for (int s = 0; s < kSubs; ++s) {
+    const int64_t n = std::min(h[8 + 8 * s].item<int64_t>(), cap);
+    if (n > 0) parts.push_back(h.narrow(0, kHeader + (int64_t)s * cap * 8, 8 * n).view({n, 8}));
+  }
+  return parts.empty() ? at::empty({0, 8}, at::kLong) : at::cat(parts, 0);
 }
 
 std::string kernel_check_files() {

@@ -149,16 +149,20 @@ DEV int check_index(int v, int bound, int line, int fallback) {
   }
 #endif
 
-// ---- Step anatomy stamps (diagnostic `stamps` build only, DSSE_PIPE_STAMPS; tools/step_stamps.py).  Workgroup
-// 0-thread records of s_memrealtime (100 MHz, one clock for every CU): [tag, grid x | grid y << 32, block x |
-// block y << 32, t0 entry, t1 first operands landed, t2 main loop done, t3 stores drained, 0] appended to a
-// per-translation-unit device buffer that the host binds (torch.ops.dsse.step_stamps_*): word 0 counts records,
-// word 1 is the capacity.  In the default build every call below compiles to nothing.
+// ---- Step anatomy stamps (diagnostic `stamps` build only, DSSE_PIPE_STAMPS; tools/step_stamps.py).  Per-wave
+// records of s_memrealtime (100 MHz, one clock for every CU): [tag, grid x | grid y << 32, block x | block y << 32,
+// t0 entry, t1 first operands landed, t2 main loop done, t3 stores drained, wave] appended to a per-translation-unit
+// device buffer that the host binds (torch.ops.dsse.step_stamps_*).  The buffer is kStampSubs sub-buffers, chosen
+// by the workgroup's linear index, each with its own counter on its own 64-byte line: one shared counter for every
+// wave of the chip serialised the waves' exits and stretched the kernels it measured.  Word 0 is the capacity per
+// sub-buffer.  In the default build every call below compiles to nothing.
 #ifndef DSSE_PIPE_STAMPS
 #define DSSE_PIPE_STAMPS 0
 #endif
 namespace stamps {
 enum Tag { kRing = 1, kNorm = 2, kAttn = 3, kPipe = 4 };
+constexpr int kSubs = 256;
+constexpr int kHeader = 8 + 8 * kSubs;  // u64 words before the first sub-buffer
 DEV unsigned long long now() {
 #if DSSE_PIPE_STAMPS
   return __builtin_amdgcn_s_memrealtime();
@@ -169,16 +173,18 @@ DEV unsigned long long now() {
 #if DSSE_PIPE_STAMPS
 static __device__ unsigned long long* g_rec;
 #endif
-// t3 is taken here, after this wave's stores drained (vmcnt(0)); call from one wave, after its last store
+// t3 is taken here, after this wave's stores drained (vmcnt(0)); call from every wave, after its last store
 DEV void record(int tag, unsigned long long t0, unsigned long long t1, unsigned long long t2) {
 #if DSSE_PIPE_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = now();
   unsigned long long* rec = g_rec;
   if ((threadIdx.x & 63) == 0 && rec) {
-    const unsigned long long n = atomicAdd(rec, 1ull);
-    if (n < rec[1]) {
-      unsigned long long* r = rec + 8 + 8 * n;
+    const unsigned sub = (blockIdx.x + blockIdx.y * gridDim.x) % kSubs;
+    const unsigned long long cap = rec[0];
+    const unsigned long long n = atomicAdd(rec + 8 + 8 * sub, 1ull);
+    if (n < cap) {
+      unsigned long long* r = rec + kHeader + (sub * cap + n) * 8;
       r[0] = (unsigned long long)tag;
       r[1] = gridDim.x | ((unsigned long long)gridDim.y << 32);
       r[2] = blockIdx.x | ((unsigned long long)blockIdx.y << 32);

@@ -68,6 +68,9 @@ for s in "$@"; do
     tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     tp8_attn)  # decode attention partitions at TP = 8 (one kv head, 64 streams): 512 / 256 / 128 / 64 workgroups
       for wg in 256 128 64; do step "tp8_attn$wg" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode --attn-wgs $wg; done ;;
+    tp8_chunks)  # TP = 8 rank prefill compute with 2 row chunks and unchunked (default 4)
+      DSSE_TP_PREFILL_CHUNKS=2 step tp8_chunks2 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
+      DSSE_TP_PREFILL_CHUNKS=1 step tp8_chunks1 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
@@ -78,7 +81,7 @@ for s in "$@"; do
       step prof_tp8_pf 300 rocprofv3 --kernel-trace -d "$out/prof_tp8_pf" -o run --output-format csv -- python3 tools/bench_tp_rank.py --tp 8 --phase prefill --iters 3 --profile-marker
       python3 tools/trace_sum.py "$(ls "$out"/prof_tp8_pf/*/run_kernel_trace.csv "$out"/prof_tp8_pf/run_kernel_trace.csv 2>/dev/null | head -1)" --div 3 --after-kernel bitwise_not --title "TP=8 rank 0, 8192-token prefill (3 prompts)" > "$out/prof_tp8_pf.md" 2>&1 ;;
     stamps64)  # step anatomy from in-kernel stamps (stamps build) + the same runner's counters (eager steps)
-      DSSE_KERNELS_VARIANT=stamps step stamps64 300 python3 tools/step_stamps.py --streams 64 --steps 4 --out "$out/stamps64.json" ;;
+      DSSE_KERNELS_VARIANT=stamps step stamps64 300 python3 tools/step_stamps.py --streams 64 --steps 2 --out "$out/stamps64.json.gz" ;;
     pmc64)
       step pmc64_a 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc64_a" -o run --output-format csv -- python3 tools/step_stamps.py --pmc-pass --steps 3 --warmup 1
       step pmc64_b 180 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc64_b" -o run --output-format csv -- python3 tools/step_stamps.py --pmc-pass --steps 3 --warmup 1

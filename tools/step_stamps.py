@@ -7,7 +7,8 @@ above its byte floor goes, split per kernel into first-load latency, steady stre
 
 Needs the diagnostic `stamps` build (`_build.py` KERNEL_VARIANTS; common.h `stamps::record`): every wave of the
 ring GEMMs (`gemm_ring_kernel`: qkv, o, down, gate_up, LM head at 17-64 rows) and of `rmsnorm_kernel` appends
-[tag, grid, block, t0, t1, t2, t3, wave] with s_memrealtime (100 MHz, one clock for the whole chip):
+[tag, grid, block, t0, t1, t2, t3, wave] with s_memrealtime (100 MHz, one clock for the whole chip) into one of 256
+sub-buffers (by workgroup; a single shared record counter serialised the waves' exits and stretched every kernel):
 
   * ring GEMM: t0 entry, t1 first K chunk (X + weights) landed in LDS for the whole workgroup, t2 K loop done
     (every DMA drained), t3 epilogue stores drained;
@@ -24,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import collections
+import gzip
 import json
 import os
 import statistics
@@ -84,12 +86,16 @@ def collect(args):
     armed = torch.ops.dsse.step_stamps_arm(0, args.cap)
     if not armed:
         raise SystemExit("the default kernel build records no stamps: run with DSSE_KERNELS_VARIANT=stamps")
+    e0.record()
     for _ in range(args.steps):
         r.decode(B)
+    e1.record()
     torch.cuda.synchronize()
+    stamped_ms = e0.elapsed_time(e1) / args.steps
     rec = torch.ops.dsse.step_stamps_read(0)
     torch.ops.dsse.step_stamps_arm(0, 0)
     out = {"streams": B, "prompt_len": args.prompt_len, "steps": args.steps, "step_ms_unstamped_replays": step_ms,
+           "step_ms_stamped": stamped_ms,
            "records": rec.tolist(), "health": r.health.cpu().tolist()}
     r.close()
     return out
@@ -136,7 +142,8 @@ def analyse(data, md=False):
     steps = max(1, data.get("steps", 1))
     lines = []
     lines.append(f"streams {data['streams']}, {steps} stamped steps, {len(L)} stamped launches, "
-                 f"unstamped replay {data.get('step_ms_unstamped_replays', 0):.4f} ms/step")
+                 f"replays {data.get('step_ms_unstamped_replays', 0):.4f} ms/step unstamped, "
+                 f"{data.get('step_ms_stamped', 0):.4f} stamped")
     hdr = ["kernel", "grid", "launches/step", "waves", "span", "start spread", "first load", "stream", "tail",
            "end spread", "gap before", "us/step"]
     lines.append("| " + " | ".join(hdr) + " |")
@@ -161,21 +168,21 @@ def main():
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--cap", type=int, default=1 << 20)
+    ap.add_argument("--cap", type=int, default=1 << 12, help="records per sub-buffer (256 sub-buffers)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--analyse", default=None)
     ap.add_argument("--md", action="store_true")
     ap.add_argument("--pmc-pass", action="store_true", help="eager decode steps, no stamps (a counter pass)")
     args = ap.parse_args()
     if args.analyse:
-        with open(args.analyse) as f:
+        with (gzip.open if args.analyse.endswith(".gz") else open)(args.analyse, "rt") as f:
             analyse(json.load(f), args.md)
         return
     data = collect(args)
     if data is None:
         return
-    if args.out:
-        with open(args.out, "w") as f:
+    if args.out:  # records as [n, 8] int lists; .gz: gzip (a 4-step record set is tens of MB as text)
+        with (gzip.open if args.out.endswith(".gz") else open)(args.out, "wt") as f:
             json.dump(data, f)
     analyse(data)
 
