@@ -68,6 +68,14 @@ struct AttnParams {
   int rope_len, num_slots;
   bf16* k_out;              // = k_cache, writable
   bf16* v_out;              // = v_cache, writable
+  // flash prefill key split (mode 2, round 6; nullptr = every item walks all its key blocks and writes `out`):
+  // item i walks key blocks [work_kb[2i], work_kb[2i + 1]) and, when work_slot[i] >= 0, leaves its unnormalised O
+  // and (max, sum) in partial slot work_slot[i] ([slot][Hkv][G][64 queries] of part_o / part_ml) for the combine:
+  // comb[4c ..] = (sequence, 64-query tile, first slot, slots) of split tile c, ncomb of them
+  const int* work_kb;
+  const int* work_slot;
+  const int* comb;
+  int ncomb;
 };
 
 struct SampleParams {

@@ -89,6 +89,10 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, u
   if (tile * kBQ >= qlen) return;              // uniform
   const int kmax = pos0 + wg_last_q + 1;       // keys [0, kmax) are visible to some query of the WG
   const int nblk = (kmax + kBK - 1) / kBK;
+  // key split (round 6): this item's key blocks [jb, je) and its partial slot (-1: the whole range, final output)
+  const int jb = p.work_kb ? p.work_kb[2 * item] : 0;
+  const int je = p.work_kb ? min(nblk, p.work_kb[2 * item + 1]) : nblk;
+  const int pslot = p.work_slot ? p.work_slot[item] : -1;
   const int w_last_pos = pos0 + min(qlen, q0 + 32) - 1;  // last visible key of this wave
   const int w_first_pos = pos0 + q0;
   const int head = h * G + hs * HG + wh;
@@ -141,8 +145,8 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, u
   const bf16* vh = p.v_cache + (size_t)h * kD * kBS;
   // Page-table entries are read one block ahead: the scalar load of block j + 1's pages is in flight while block j
   // is issued and retired by the next LDS wait, not by a dependent wait in front of this block's DMA.
-  int pg0 = page_block(bt, 0, npages, p), pg1 = page_block(bt, 1, npages, p);
-  int jn = 0;  // next block to issue (blocks are issued in order)
+  int pg0 = page_block(bt, 2 * jb, npages, p), pg1 = page_block(bt, 2 * jb + 1, npages, p);
+  int jn = jb;  // next block to issue (blocks are issued in order)
   // (the page bases are pinned in SGPR pairs: left to itself the compiler folds the per-lane select of two bases into
   // a per-lane select of the page index followed by a per-lane 64-bit multiply)
   auto sbase = [&](const bf16* head, int blk) {
@@ -323,11 +327,11 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, u
   issue_block(2);
   if (lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
   // unrolled by the ring size: each block's LDS slot is a compile-time offset (no per-read address arithmetic)
-  for (int j0 = 0; j0 < nblk; j0 += kRing) {
+  for (int j0 = jb; j0 < je; j0 += kRing) {
 #pragma unroll
     for (int k = 0; k < kRing; ++k) {
-      const int j = j0 + k;
-      if (j < nblk) {
+      const int j = j0 + k;  // LDS slot k = (j - jb) % kRing: block jb went to slot 0
+      if (j < je) {
         const bool vis = j * kBK <= w_last_pos;  // this wave sees at least one key of the block
         stamp(j, 0);
         if (!lag) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * IPW) : "memory");
@@ -355,6 +359,20 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, u
   }
 
   // ---- epilogue: lane (r, g) holds O[query 16qt + r][d = 16dt + 4g + i]
+  if (pslot >= 0) {  // one key range of a split tile: unnormalised O and (max, sum) for flash_combine_kernel
+    const size_t sb = ((size_t)(pslot * p.hkv + h) * G + hs * HG + wh) * kBQ;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qrow = wq * 32 + 16 * qt + r;
+      if (q0 + 16 * qt + r >= qlen) continue;
+      const float l = rows4_sum(l_part[qt][0] + l_part[qt][1]);
+      float* po = p.part_o + (sb + qrow) * kD + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = o[dt][qt];
+      if (g == 0) p.part_ml[sb + qrow] = make_float2(m_run[qt] < -1e29f ? 0.f : m_run[qt], l);
+    }
+    return;
+  }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qi = q0 + 16 * qt + r;
@@ -371,6 +389,44 @@ __global__ void __launch_bounds__(128 * HG) flash_prefill_kernel(AttnParams p, u
       v[3] = f2bf(o[dt][qt][3] * inv);
       *reinterpret_cast<bf16x4*>(op + 16 * dt) = v;
     }
+  }
+}
+
+// Merge the key ranges of split tiles (flash prefill key split): grid (ncomb, Hkv, G), 256 threads = 64 query rows x 4
+// quarters of the head dimension; each thread reads its 32 dims of every slot once (the slots' O is relative to their
+// own running max m, in log2 units: weight 2^(m - M)).
+__global__ void __launch_bounds__(256) flash_combine_kernel(AttnParams p) {
+  const int c = blockIdx.x, h = blockIdx.y, hl = blockIdx.z, G = p.group;
+  const int qrow = threadIdx.x >> 2, dq = threadIdx.x & 3;
+  const int b = p.comb[4 * c], tile = p.comb[4 * c + 1], s0 = p.comb[4 * c + 2], ns = p.comb[4 * c + 3];
+  const int qi = tile * kBQ + qrow;
+  if (qi >= p.q_len[b]) return;
+  float mm = -1e30f;
+  for (int k = 0; k < ns; ++k) mm = fmaxf(mm, p.part_ml[((size_t)((s0 + k) * p.hkv + h) * G + hl) * kBQ + qrow].x);
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ll = 0.f;
+  for (int k = 0; k < ns; ++k) {
+    const size_t row = ((size_t)((s0 + k) * p.hkv + h) * G + hl) * kBQ + qrow;
+    const float2 ml = p.part_ml[row];
+    const float wgt = __builtin_amdgcn_exp2f(ml.x - mm);
+    ll += ml.y * wgt;
+    const f32x4* po = reinterpret_cast<const f32x4*>(p.part_o + row * kD + 32 * dq);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += po[j] * wgt;
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+  bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + h * G + hl) * kD + 32 * dq;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = f2bf(acc[j][i] * inv);
+      v[4 + i] = f2bf(acc[j + 1][i] * inv);
+    }
+    *reinterpret_cast<bf16x8*>(op + 4 * j) = v;
   }
 }
 
@@ -428,16 +484,20 @@ extern "C" hipError_t dsse_flash_prefill(int num_work, const dsse::AttnParams* p
   static const char* stamps = getenv("DSSE_FLASH_STAMPS");
   if (stamps != nullptr && stamps[0] != '\0') return launch_stamped(num_work, p, st, stamps);
   int hg = p->kwv;
-  if (hg == 0) hg = p->group;
+  if (hg == 0 || p->work_kb) hg = p->group;  // the key split writes partial slots per whole group
+  hipError_t e;
   switch (p->group) {
-    case 1: return launch_flash<1, 1, false>(num_work, p, st, nullptr);
-    case 2: return hg == 1 ? launch_flash<2, 1, false>(num_work, p, st, nullptr)
-                           : launch_flash<2, 2, false>(num_work, p, st, nullptr);
-    case 4: return hg == 1 ? launch_flash<4, 1, false>(num_work, p, st, nullptr)
-                           : hg == 2 ? launch_flash<4, 2, false>(num_work, p, st, nullptr)
-                                     : launch_flash<4, 4, false>(num_work, p, st, nullptr);
+    case 1: e = launch_flash<1, 1, false>(num_work, p, st, nullptr); break;
+    case 2: e = hg == 1 ? launch_flash<2, 1, false>(num_work, p, st, nullptr)
+                        : launch_flash<2, 2, false>(num_work, p, st, nullptr); break;
+    case 4: e = hg == 1 ? launch_flash<4, 1, false>(num_work, p, st, nullptr)
+                        : hg == 2 ? launch_flash<4, 2, false>(num_work, p, st, nullptr)
+                                  : launch_flash<4, 4, false>(num_work, p, st, nullptr); break;
     default: return hipErrorInvalidValue;
   }
+  if (e != hipSuccess || !p->work_kb || p->ncomb <= 0) return e;
+  hipLaunchKernelGGL(dsse::flash_combine_kernel, dim3(p->ncomb, p->hkv, p->group), dim3(256), 0, st, *p);
+  return hipGetLastError();
 }
 
 DSSE_CHECK_READER(dsse_check_attention_prefill)

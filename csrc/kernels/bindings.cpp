@@ -831,6 +831,45 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
   else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
 }
 
+// Flash prefill with the key split (round 6): `work` = [seq | tile | (kb0, kb1) pairs | slot] over nw items (int32,
+// 5 nw), `comb` = [(seq, tile, first slot, slots)] over the split tiles (int32, 4 nc).  Items with slot -1 write `out`;
+// the others leave partial O / (max, sum) in slots [0, nslots) of part_o / part_ml and flash_combine_kernel merges
+// them (engine: ModelRunner._flash_split_plan).
+void flash_prefill_split(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                         const Tensor& q_start, const Tensor& q_len, const Tensor& ctx_len, const Tensor& work,
+                         const Tensor& comb, Tensor& out, Tensor& part_o, Tensor& part_ml, int64_t nslots) {
+  check_gpu(q, "q");
+  check_dtype(q, at::kBFloat16, "q");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  const int hq = (int)q.size(1), hkv = (int)k_cache.size(1);
+  TORCH_CHECK(hq % hkv == 0 && (hq / hkv == 1 || hq / hkv == 2 || hq / hkv == 4), "flash prefill supports G in {1, 2, 4}");
+  for (const Tensor* t : {&work, &comb}) {
+    check_gpu(*t, "split plan");
+    check_dtype(*t, at::kInt, "split plan");
+  }
+  TORCH_CHECK(work.numel() % 5 == 0 && comb.numel() % 4 == 0, "work = 5 x nw, comb = 4 x nc int32");
+  const int64_t nw = work.numel() / 5;
+  check_gpu(part_o, "part_o");
+  check_gpu(part_ml, "part_ml");
+  check_dtype(part_o, at::kFloat, "part_o");
+  check_dtype(part_ml, at::kFloat, "part_ml");
+  TORCH_CHECK(nslots >= 0 && part_o.numel() >= nslots * hkv * hq / hkv * 64 * 128 &&
+                  part_ml.numel() >= nslots * hkv * hq / hkv * 64 * 2, "part_o / part_ml too small for nslots");
+  Tensor ws = work.narrow(0, 0, nw), wt = work.narrow(0, nw, nw);
+  dsse::AttnParams p = attn_params(hq, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, ws, wt, out, part_o,
+                                   part_ml, 32, 1, 4, 1);
+  p.q = reinterpret_cast<const bf16*>(q.data_ptr());
+  p.work_kb = work.data_ptr<int>() + 2 * nw;
+  p.work_slot = work.data_ptr<int>() + 4 * nw;
+  p.comb = comb.data_ptr<int>();
+  p.ncomb = (int)(comb.numel() / 4);
+  p.part_o = part_o.data_ptr<float>();
+  p.part_ml = reinterpret_cast<float2*>(part_ml.data_ptr<float>());
+  p.kwv = 0;
+  DSSE_CHECK_HIP(dsse_flash_prefill((int)nw, &p, cur_stream()));
+}
+
 // Decode QKV projection + attention with the projection's epilogue folded into the attention kernel: the GEMM
 // leaves fp32 split-K slabs in `slabs` and attention mode 3 sums them, applies RoPE, writes this step's K / V
 // into the cache and attends -- one launch (the split-K reduce) fewer per layer.  Falls back to gemm_qkv_rope
@@ -1101,7 +1140,7 @@ void ar_gather(const Tensor& cand, Tensor& out, const Tensor& peers, int64_t ran
                                 reinterpret_cast<unsigned int*>(err.data_ptr<int>()), cur_stream()));
 }
 
-int64_t kernels_abi_version() { return 15; }
+int64_t kernels_abi_version() { return 16; }
 
 // The dispatch's choice for an (M, N, K) projection: (impl, tiled cfg, split, fix, model estimate in us) -- impl as
 // gemm_impl (4 = tiled / pipe); cfg / split / fix / estimate only for impl 4 (tools/bench_decode_gemm.py --plan).
@@ -1218,6 +1257,9 @@ TORCH_LIBRARY(dsse, m) {
   m.def("paged_attention(int mode, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(a!) out, "
         "Tensor(b!) part_o, Tensor(c!) part_ml, int part, int nparts) -> ()");
+  m.def("flash_prefill_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor q_start, "
+        "Tensor q_len, Tensor ctx_len, Tensor work, Tensor comb, Tensor(a!) out, Tensor(b!) part_o, "
+        "Tensor(c!) part_ml, int nslots) -> ()");
   m.def("qkv_attention_decode(Tensor x, Tensor w, Tensor positions, Tensor slots, Tensor rope, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, int nkv, Tensor(d!) slabs, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, Tensor work_seq, Tensor work_tile, Tensor(e!) out, "
@@ -1259,6 +1301,7 @@ TORCH_LIBRARY_IMPL(dsse, CUDA, m) {
   m.impl("decode_prep", &decode_prep);
   m.impl("ring_advance", &ring_advance);
   m.impl("paged_attention", &paged_attention);
+  m.impl("flash_prefill_split", &flash_prefill_split);
   m.impl("qkv_attention_decode", &qkv_attention_decode);
   m.impl("sample_candidates", &sample_candidates);
   m.impl("sample_pick", &sample_pick);

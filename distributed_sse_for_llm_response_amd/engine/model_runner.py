@@ -60,6 +60,37 @@ HEALTH_WORDS = ("TP peer all-reduce wait timed out",)
 # all-reduce -> norm) runs in row chunks so that each chunk's all-reduce (RCCL, a side stream) overlaps the next chunk's
 # GEMMs (SURVEY.md §2.4 C5: 64 MiB all-reduces at 8k tokens, VERDICT r3 missing 1).  Chunked from
 # DSSE_TP_PREFILL_OVERLAP_MIN rows, in DSSE_TP_PREFILL_CHUNKS chunks of whole 64-row tiles.
+def flash_split_plan(tiles: list, hkv: int, min_blocks: int = 32, fill: int = 256, min_target: int = 16):
+    """Key split of the flash prefill for an under-filled grid (round 6).  `tiles`: [(seq, tile, key blocks)]
+    heaviest first.  With fewer than `fill` (tile, kv head) workgroups and a tile of >= `min_blocks` 64-key blocks (a
+    TP = 8 rank has ONE kv head: an 8k prompt is 128 workgroups for 256 CUs, and the last tile walks 128 blocks
+    alone), every tile longer than target = max(16, blocks x Hkv / fill) blocks is cut into even key ranges; each
+    range leaves partial O in its own slot and flash_combine_kernel merges a tile's slots.  Returns None (no split)
+    or (work int32 [seq | tile | (kb0, kb1) pairs | slot], comb int32 [(seq, tile, first slot, slots)], slots), the
+    work list heaviest range first."""
+    if not tiles or len(tiles) * hkv >= fill or max(n for _, _, n in tiles) < min_blocks:
+        return None
+    target = max(min_target, -(-sum(n for _, _, n in tiles) * hkv // fill))
+    work, comb, nslots = [], [], 0
+    for b, t, n in tiles:
+        parts = -(-n // target)
+        if parts == 1:
+            work.append((n, b, t, 0, n, -1))
+            continue
+        per = -(-n // parts)
+        comb.append((b, t, nslots, parts))
+        for k in range(parts):
+            work.append((min(n, (k + 1) * per) - k * per, b, t, k * per, min(n, (k + 1) * per), nslots + k))
+        nslots += parts
+    if not comb:
+        return None
+    work.sort(key=lambda x: -x[0])
+    cols = list(zip(*work))
+    kb = [v for a, e in zip(cols[3], cols[4]) for v in (a, e)]
+    w = np.asarray(list(cols[1]) + list(cols[2]) + kb + list(cols[5]), dtype=np.int32)
+    return w, np.asarray([v for c in comb for v in c], dtype=np.int32), nslots
+
+
 def prefill_row_chunks(T: int, tp: int) -> list:
     """[(row0, row1)] of the overlapped TP prefill (one chunk when it does not apply)."""
     lo = int(os.environ.get("DSSE_TP_PREFILL_OVERLAP_MIN", "1024"))
@@ -615,9 +646,10 @@ class ModelRunner:
         self.comm.all_reduce(tmp)
         ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
 
-    def _prefill_meta(self, seqs: list, row0: int = 0):
+    def _prefill_meta(self, seqs: list, row0: int = 0, split: bool = False):
         """Packed metadata of prefill chunks whose rows start at `row0` of the activations (0 for a prefill-only
-        batch, B for the prefill rows of a mixed step): host lists + device tensors (one pinned upload)."""
+        batch, B for the prefill rows of a mixed step): host lists + device tensors (one pinned upload).  split: add
+        the flash key-split plan when the grid is under-filled (flash_split_plan: d["fw"], d["fc"], d["fslots"])."""
         dev = self.device
         n = len(seqs)
         # vectorised per sequence (an 8k-token chunk was ~25k Python list appends on the TTFT path)
@@ -643,19 +675,25 @@ class ModelRunner:
         work_seq = [i for _, i, _ in items]
         work_tile = [t for _, _, t in items]
         T = row
+        plan = None
+        if split:
+            plan = flash_split_plan([(i, t, -(-(-k) // PREFILL_TILE)) for k, i, t in items], self.w.nkv)
+        fw, fc = (plan[0], plan[1]) if plan else (np.zeros(0, np.int32), np.zeros(0, np.int32))
         empty = np.zeros(0, dtype=np.int64)
         meta = torch.from_numpy(np.concatenate(
             [np.concatenate(ids_l) if ids_l else empty, np.concatenate(pos_l) if pos_l else empty,
              np.concatenate(slots_l) if slots_l else empty,
-             np.asarray(q_start + q_len + ctx_len + work_seq + work_tile, dtype=np.int64)]).astype(np.int32))
+             np.asarray(q_start + q_len + ctx_len + work_seq + work_tile, dtype=np.int64),
+             fw.astype(np.int64), fc.astype(np.int64)]).astype(np.int32))
         if dev.type == "cuda":
             meta = meta.pin_memory().to(dev, non_blocking=True)
             bt = bt.pin_memory().to(dev, non_blocking=True)
         d, o = {}, 0
         for name, k in (("ids", T), ("pos", T), ("slots", T), ("qs", n), ("ql", n), ("ctx", n),
-                        ("ws", len(work_seq)), ("wt", len(work_seq))):
+                        ("ws", len(work_seq)), ("wt", len(work_seq)), ("fw", len(fw)), ("fc", len(fc))):
             d[name], o = meta[o:o + k], o + k
         d["bt"] = bt
+        d["fslots"] = plan[2] if plan else 0
         return T, q_start, q_len, ctx_len, d
 
     def _prefill_sample(self, seqs: list, x, q_start: list, q_len: list, ring_row: int) -> None:
@@ -710,9 +748,12 @@ class ModelRunner:
             return
         w, dev = self.w, self.device
         nh, nkv, F, H = w.nh, w.nkv, w.ffn, self.cfg.hidden_size
-        T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs)
+        T, q_start, q_len, ctx_len, d = self._prefill_meta(seqs, split=True)
         f32 = dict(device=dev, dtype=torch.float32)
         bf = dict(device=dev, dtype=torch.bfloat16)
+        if d["fslots"]:  # partial slots of the flash key split: [slots][Hkv][G][64 queries] x (128 dims | (m, l))
+            d.update(fpo=torch.empty(d["fslots"] * nh * PREFILL_TILE * 128, **f32),
+                     fpm=torch.empty(d["fslots"] * nh * PREFILL_TILE * 2, **f32))
         d.update(resid=torch.empty(T, H, **f32), x=torch.empty(T, H, **bf), q=torch.empty(T, nh, 128, **bf),
                  attn=torch.empty(T, nh, 128, **bf), h=torch.empty(T, F, **bf), tmp=torch.empty(T, H, **bf),
                  qkv=torch.empty(T, (nh + 2 * nkv) * 128, **bf), part=math.ceil(max(ctx_len) / 32) * 32)
@@ -733,8 +774,12 @@ class ModelRunner:
             # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
             self._proj(x, L.wqkv_t, qkv)
             ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
-            ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
-                                d["wt"], attn, self.part_o, self.part_ml, d["part"], 1)
+            if d.get("fslots"):
+                ops.flash_prefill_split(q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"],
+                                        d["fw"], d["fc"], attn, d["fpo"], d["fpm"], d["fslots"])
+            else:
+                ops.paged_attention(2, q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"], d["ws"],
+                                    d["wt"], attn, self.part_o, self.part_ml, d["part"], 1)
             w_next = w.layers[li + 1].attn_norm if li + 1 < nl else w.final_norm
             self._prefill_post_attention(T, attn.view(T, nh * 128), L, w_next, resid, x, h, tmp)
 

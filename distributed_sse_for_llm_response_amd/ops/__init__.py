@@ -182,6 +182,20 @@ def paged_attention(mode, q, k_cache, v_cache, block_tables, q_start, q_len, ctx
                             out, part_o, part_ml, part, nparts)
 
 
+def flash_prefill_split(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work, comb, out, part_o, part_ml,
+                        nslots: int) -> None:
+    """Flash prefill with long causal tiles split over key ranges (work = [seq | tile | (kb0, kb1) pairs | slot],
+    comb = [(seq, tile, first slot, slots)]; ModelRunner._flash_split_plan): the parts leave partial O in slots that
+    a combine kernel merges.  Same result as paged_attention mode 2 up to fp32 summation order."""
+    if _hip(q):
+        torch.ops.dsse.flash_prefill_split(q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work, comb, out,
+                                           part_o, part_ml, nslots)
+    else:  # the split is a schedule: the reference computes each tile whole (a split tile's items repeat it)
+        nw = work.numel() // 5
+        ref.paged_attention(2, q, k_cache, v_cache, block_tables, q_start, q_len, ctx_len, work[:nw], work[nw:2 * nw],
+                            out, part_o, part_ml, 32, 1)
+
+
 def qkv_attention_decode(x, w, positions, slots, rope, q_out, k_cache, v_cache, nh, nkv, slabs, block_tables, q_start,
                          q_len, ctx_len, work_seq, work_tile, out, part_o, part_ml, part, nparts) -> int:
     """Decode QKV projection + RoPE + KV write + attention.  HIP: the GEMM leaves fp32 split-K slabs in `slabs`

@@ -576,6 +576,48 @@ def test_flash_prefill_one_kv_head_head_split(gpu, monkeypatch, case, hg):
     _close(out_g, out, 1e-2, 2e-2, f"flash prefill, one kv head, hg {hg}")
 
 
+@pytest.mark.parametrize("case", [
+    ((1, 4), [2048], [2048]),                   # a TP = 8 rank's prompt: one kv head
+    ((1, 4), [1500, 700], [1500, 300]),         # two sequences, the second a later chunk of its prompt
+    ((2, 2), [1333], [1333]),                   # G = 2, two kv heads, a ragged last tile
+    ((2, 1), [1100, 1030], [1100, 1030]),       # G = 1
+])
+def test_flash_prefill_key_split(gpu, case):
+    """Flash prefill with long causal tiles cut into key ranges (ModelRunner flash_split_plan; partial slots merged
+    by flash_combine_kernel) against the fp32 reference -- forced with small ranges so every shape splits."""
+    from distributed_sse_for_llm_response_amd.engine.model_runner import flash_split_plan
+
+    (hkv, G), ctxs, qlens = case
+    hq = hkv * G
+    g = torch.Generator().manual_seed(sum(ctxs) + hq)
+    B = len(ctxs)
+    kc, vc, bt, q, q_start = _attn_setup(ctxs, qlens, hq=hq, hkv=hkv, gen=g)
+    qlen, ctx = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
+    tiles = []
+    for b in range(B):
+        pos0 = ctxs[b] - qlens[b]
+        for t in range(math.ceil(qlens[b] / 64)):
+            tiles.append((b, t, math.ceil((pos0 + min(qlens[b], 64 * (t + 1))) / 64)))
+    tiles.sort(key=lambda x: -x[2])
+    plan = flash_split_plan(tiles, hkv, min_blocks=4, fill=1 << 20, min_target=5)
+    assert plan is not None
+    work, comb, nslots = plan
+    assert len(comb) > 0 and nslots > len(comb) // 4
+    out = torch.zeros_like(q)
+    ws = torch.tensor([b for b, _, _ in tiles], dtype=torch.int32)
+    wt = torch.tensor([t for _, t, _ in tiles], dtype=torch.int32)
+    R.paged_attention(2, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out, None, None, 32, 1)
+    out_g = torch.full_like(q, float("nan")).to(gpu)
+    po = torch.zeros(nslots * hq * 64 * 128, device=gpu)
+    pm = torch.zeros(nslots * hq * 64 * 2, device=gpu)
+    for _ in range(2):  # repeatable
+        ops.flash_prefill_split(q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu),
+                                ctx.to(gpu), torch.from_numpy(work).to(gpu), torch.from_numpy(comb).to(gpu), out_g, po,
+                                pm, nslots)
+    assert not torch.isnan(out_g).any(), "a query row was never written"
+    _close(out_g, out, 1e-2, 2e-2, f"flash prefill key split {case}")
+
+
 def _sampler_inputs(B, V, gen, temps, topk, topp):
     logits = torch.randn(B, V, generator=gen) * 3
     t = torch.tensor(temps, dtype=torch.float32)
@@ -668,7 +710,7 @@ def test_gpu_path_has_no_fallback(gpu):
     """GPU tensors must run the HIP library (the op is registered and loaded from the in-tree .so)."""
     assert ops.load_library(required=True)
     assert os.path.exists(ops.library_path())
-    assert torch.ops.dsse.kernels_abi_version() == 15
+    assert torch.ops.dsse.kernels_abi_version() == 16
     assert not torch.ops.dsse.kernels_checked() and ops.kernel_checks() == []  # default build: checks compiled out
 
 

@@ -243,3 +243,32 @@ def test_tp_ranks_ignore_their_own_pass_costs(monkeypatch):
         return chunks
 
     assert run(0.001) == run(0.02)
+
+
+def test_flash_split_plan_covers_every_key_block_once():
+    """flash_split_plan (ModelRunner, the flash prefill key split): only an under-filled grid with long tiles is
+    split; every tile's key blocks are covered once, by one direct item or by its consecutive slots."""
+    from distributed_sse_for_llm_response_amd.engine.model_runner import flash_split_plan
+
+    tiles = [(0, t, t + 1) for t in reversed(range(128))]  # an 8k prompt, fresh: tile t walks t + 1 blocks
+    assert flash_split_plan(tiles, 8) is None               # 1024 workgroups: already fills the chip
+    assert flash_split_plan(tiles[-20:], 1) is None         # short tiles only
+    work, comb, nslots = flash_split_plan(tiles, 1)
+    nw = len(work) // 5
+    seq, tile, kb, slot = work[:nw], work[nw:2 * nw], work[2 * nw:4 * nw].reshape(nw, 2), work[4 * nw:]
+    assert nw > 256 and max(e - a for a, e in kb) <= 33
+    ranges = {}
+    for i in range(nw):
+        ranges.setdefault(int(tile[i]), []).append((int(kb[i, 0]), int(kb[i, 1]), int(slot[i])))
+    cmap = {int(comb[4 * c + 1]): (int(comb[4 * c + 2]), int(comb[4 * c + 3])) for c in range(len(comb) // 4)}
+    for t, rs in ranges.items():
+        rs.sort()
+        assert rs[0][0] == 0 and rs[-1][1] == t + 1
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+        if len(rs) == 1:
+            assert rs[0][2] == -1 and t not in cmap
+        else:
+            s0, n = cmap[t]
+            assert sorted(r[2] for r in rs) == list(range(s0, s0 + n))
+    assert nslots == sum(n for _, n in cmap.values())
+    assert (seq == 0).all()
