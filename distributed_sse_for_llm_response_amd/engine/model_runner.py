@@ -24,6 +24,8 @@ batch bucket into a torch.cuda.CUDAGraph (a hipGraph on ROCm).
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import math
 import os
 import time
@@ -40,6 +42,21 @@ from .weights import EngineWeights
 
 RING_SIZE = 64
 SAMPLE_CHUNKS = 16  # vocab chunks per row in the candidate pass (B x 16 workgroups)
+@contextlib.contextmanager
+def _capture(graph, **kw):
+    """torch.cuda.graph with the garbage collector off for the capture: a collection inside it could run a finaliser
+    that destroys another object's graph or event (a HIP call that stream capture forbids: the process aborts)."""
+    enabled = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, **kw):
+            yield
+    finally:
+        if enabled:
+            gc.enable()
+
+
 PREFILL_TILE = 64   # query tokens per flash-prefill workgroup (attention_prefill.hip)
 # Prefill batches of up to 2048 tokens replay a captured graph per row bucket (padded rows: slot -1, no K/V write,
 # no attention work); larger batches (long prompts at an idle budget) run eagerly.  DSSE_PREFILL_GRAPHS=0 disables.
@@ -101,6 +118,9 @@ def prefill_row_chunks(T: int, tp: int) -> list:
 
 # prompt passes up to this many rows send the residual projections' split-K slabs to the norm (_prefill_resid)
 PREFILL_SLAB_ROWS = 512
+# prompt passes up to this many rows run QKV with the RoPE + KV-write epilogue fused (gemm_qkv_rope: the split-K
+# reduce applies it, or the in-launch fix-up) instead of a bf16 tile + splitk_reduce + rope_kv_write
+PREFILL_QKV_FUSED_ROWS = 1024
 
 
 # Prompt-chunk sizes of the captured mixed steps: one graph per (decode bucket, C).  The engine sizes each step's
@@ -371,7 +391,7 @@ class ModelRunner:
             torch.cuda.current_stream(self.device).wait_stream(s)
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _capture(g):
                 self.comm.all_reduce(t)
             t.fill_(1.0)
             g.replay()
@@ -429,7 +449,7 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         for B in sorted(buckets, reverse=True):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
+            with _capture(g, pool=self.graph_pool):
                 self.decode_forward(B)
             if self.graph_pool is None:
                 self.graph_pool = g.pool()
@@ -460,7 +480,7 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         for tb in sorted(buckets, reverse=True):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
+            with _capture(g, pool=self.graph_pool):
                 self._prefill_layers(tb, self.pf.views(tb))
                 self._graph_sample()
             if self.graph_pool is None:
@@ -505,7 +525,7 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         for B, C in sorted(pairs, reverse=True):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
+            with _capture(g, pool=self.graph_pool):
                 self._mixed_layers(B, C)
                 self._graph_sample()
             self.mx_graphs.setdefault(B, []).insert(0, (C, g))
@@ -770,10 +790,15 @@ class ModelRunner:
         # projections on the engine's tiled-layout GEMMs (gemm_pipe.hip / gemm_tiled.hip for T > 128 rows; gate_up with
         # its fused SiLU·mul epilogue): no library GEMM
         for li, L in enumerate(w.layers):
-            # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
-            # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md)
-            self._proj(x, L.wqkv_t, qkv)
-            ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
+            # long passes: QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel (the fused
+            # per-element RoPE epilogue measured +200 us per 8192-row layer, profiles/r2/prefill_kernels_8k.md);
+            # short ones fuse it: one launch fewer (two with the in-launch split-K fix-up)
+            if T <= PREFILL_QKV_FUSED_ROWS:
+                ops.gemm_qkv_rope(x, L.wqkv_t, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh,
+                                  nkv)
+            else:
+                self._proj(x, L.wqkv_t, qkv)
+                ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             if d.get("fslots"):
                 ops.flash_prefill_split(q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"],
                                         d["fw"], d["fc"], attn, d["fpo"], d["fpm"], d["fslots"])
@@ -900,7 +925,9 @@ class _PrefillStatic:
     write) and token 0; sequence index NS is the empty sequence (q_len 0) that padded work items point at."""
 
     def __init__(self, runner: ModelRunner, tmax: int):
-        self.r, self.tmax = runner, tmax
+        # no back-reference to the runner: a runner <-> buffers cycle kept captured graphs alive until a garbage
+        # collection, which could then run inside ANOTHER runner's capture and free a graph pool mid-capture (abort)
+        self.tmax = tmax
         w, cfg, dev = runner.w, runner.cfg, runner.device
         nh, nkv, F, H = w.nh, w.nkv, w.ffn, cfg.hidden_size
         self.ns = PREFILL_GRAPH_SEQS

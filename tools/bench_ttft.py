@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--decode-steps", type=int, default=16)
+    ap.add_argument("--qkv-fused-rows", type=int, default=-1,
+                    help="A/B: model_runner.PREFILL_QKV_FUSED_ROWS (-1 = the engine default)")
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch one bitwise_not kernel after the warm-up iteration: tools/trace_sum.py --after-kernel "
                          "bitwise_not then keeps only the timed iterations of a rocprofv3 kernel trace")
@@ -43,6 +45,10 @@ def main():
     from distributed_sse_for_llm_response_amd.engine.weights import random_engine_weights
     from distributed_sse_for_llm_response_amd.models.mistral import get_config
     from distributed_sse_for_llm_response_amd.parallel.comm import TPComm, init_distributed
+    from distributed_sse_for_llm_response_amd.engine import model_runner as _mr
+
+    if args.qkv_fused_rows >= 0:
+        _mr.PREFILL_QKV_FUSED_ROWS = args.qkv_fused_rows
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local)
@@ -59,16 +65,20 @@ def main():
     r.capture([B])
     gen = torch.Generator().manual_seed(5)
 
+    # the slots' block tables and sampling parameters are set once, so a profiled iteration holds only the prefill
+    # (and decode) kernels: no torch fill / copy kernels between the trace marker and the first prefill launch
+    for s in range(B):
+        r.block_tables[s, :per] = torch.tensor(list(range(s * per, (s + 1) * per)), dtype=torch.int32, device=device)
+    r.temperature.fill_(1.0)
+    r.top_p.fill_(1.0)
+    r.active.zero_()
+
     def one_iter():
         seqs = []
         for s in range(B):
             blocks = list(range(s * per, (s + 1) * per))
-            r.block_tables[s, :per] = torch.tensor(blocks, dtype=torch.int32, device=device)
             toks = torch.randint(3, cfg.vocab_size, (args.prompt_len,), generator=gen).tolist()
             seqs.append((s, toks, blocks))
-        r.temperature.fill_(1.0)
-        r.top_p.fill_(1.0)
-        r.active.zero_()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -80,11 +90,14 @@ def main():
                       ring_row=0)
         first = r.ids[:B].cpu()  # D2H: the first token is on the host
         ttft = time.perf_counter() - t0
-        r.active[:B] = 1
+        if args.decode_steps:
+            r.active[:B] = 1
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.decode_steps):
             r.decode(B)
+        if args.decode_steps:
+            r.active.zero_()
         torch.cuda.synchronize()
         itl = (time.perf_counter() - t1) / max(1, args.decode_steps)
         return ttft, itl, first
