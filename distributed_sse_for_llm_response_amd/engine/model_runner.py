@@ -118,9 +118,6 @@ def prefill_row_chunks(T: int, tp: int) -> list:
 
 # prompt passes up to this many rows send the residual projections' split-K slabs to the norm (_prefill_resid)
 PREFILL_SLAB_ROWS = 512
-# prompt passes up to this many rows run QKV with the RoPE + KV-write epilogue fused (gemm_qkv_rope: the split-K
-# reduce applies it, or the in-launch fix-up) instead of a bf16 tile + splitk_reduce + rope_kv_write
-PREFILL_QKV_FUSED_ROWS = 1024
 
 
 # Prompt-chunk sizes of the captured mixed steps: one graph per (decode bucket, C).  The engine sizes each step's
@@ -790,15 +787,12 @@ class ModelRunner:
         # projections on the engine's tiled-layout GEMMs (gemm_pipe.hip / gemm_tiled.hip for T > 128 rows; gate_up with
         # its fused SiLU·mul epilogue): no library GEMM
         for li, L in enumerate(w.layers):
-            # long passes: QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel (the fused
-            # per-element RoPE epilogue measured +200 us per 8192-row layer, profiles/r2/prefill_kernels_8k.md);
-            # short ones fuse it: one launch fewer (two with the in-launch split-K fix-up)
-            if T <= PREFILL_QKV_FUSED_ROWS:
-                ops.gemm_qkv_rope(x, L.wqkv_t, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh,
-                                  nkv)
-            else:
-                self._proj(x, L.wqkv_t, qkv)
-                ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
+            # QKV out as a plain bf16 tile, then the vectorised RoPE + paged-KV-write kernel: the fused
+            # per-element RoPE epilogue measured +200 us per 8192-row layer (profiles/r2/prefill_kernels_8k.md), and
+            # at 512 rows (gemm_qkv_rope, one launch fewer) 9.21-9.37 vs 9.15-9.33 ms TTFT, alternating
+            # (profiles/r6/ttft512_qkv_fused_ab_r6.log)
+            self._proj(x, L.wqkv_t, qkv)
+            ops.rope_kv_write(qkv, d["pos"], d["slots"], self.rope, q, self.kv.k[li], self.kv.v[li], nh, nkv)
             if d.get("fslots"):
                 ops.flash_prefill_split(q, self.kv.k[li], self.kv.v[li], d["bt"], d["qs"], d["ql"], d["ctx"],
                                         d["fw"], d["fc"], attn, d["fpo"], d["fpm"], d["fslots"])

@@ -29,8 +29,6 @@ def main():
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--decode-steps", type=int, default=16)
-    ap.add_argument("--qkv-fused-rows", type=int, default=-1,
-                    help="A/B: model_runner.PREFILL_QKV_FUSED_ROWS (-1 = the engine default)")
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch one bitwise_not kernel after the warm-up iteration: tools/trace_sum.py --after-kernel "
                          "bitwise_not then keeps only the timed iterations of a rocprofv3 kernel trace")
@@ -45,10 +43,6 @@ def main():
     from distributed_sse_for_llm_response_amd.engine.weights import random_engine_weights
     from distributed_sse_for_llm_response_amd.models.mistral import get_config
     from distributed_sse_for_llm_response_amd.parallel.comm import TPComm, init_distributed
-    from distributed_sse_for_llm_response_amd.engine import model_runner as _mr
-
-    if args.qkv_fused_rows >= 0:
-        _mr.PREFILL_QKV_FUSED_ROWS = args.qkv_fused_rows
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local)

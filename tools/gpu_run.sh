@@ -44,11 +44,6 @@ for s in "$@"; do
     prof256) step prof256 600 rocprofv3 --kernel-trace --stats -d "$out/prof256" -o run --output-format csv -- python3 bench.py --steps 8 --warmup 2 --streams 256 ;;
     ttft8k) step ttft8k 600 python3 tools/bench_ttft.py --prompt-len 8192 ;;
     ttft512) step ttft512 600 python3 tools/bench_ttft.py --prompt-len 512 ;;
-    ttft512_ab)  # QKV + RoPE fused for short passes (default) vs the bf16 tile + rope_kv_write, alternating
-      for i in 1 2; do
-        step "ttft512_fused$i" 300 python3 tools/bench_ttft.py --prompt-len 512 --iters 9
-        step "ttft512_unfused$i" 300 python3 tools/bench_ttft.py --prompt-len 512 --iters 9 --qkv-fused-rows 0
-      done ;;
     profttft8k)
       step profttft8k 600 rocprofv3 --kernel-trace -d "$out/profttft8k" -o run --output-format csv -- python3 tools/bench_ttft.py --prompt-len 8192 --decode-steps 0 --profile-marker
       python3 tools/trace_sum.py "$(ls "$out"/profttft8k/*/run_kernel_trace.csv "$out"/profttft8k/run_kernel_trace.csv 2>/dev/null | head -1)" --div 3 --after-kernel bitwise_not --title "8k-token prefill, per prompt (3 timed prompts, setup and warm-up excluded)" > "$out/profttft8k.md" 2>&1 ;;
