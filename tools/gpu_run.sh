@@ -65,6 +65,12 @@ for s in "$@"; do
     sdef40j08) DSSE_JIT_MARGIN_MS=0.8 step sdef40j08 600 python3 tools/bench_serving.py --rates 40 --requests 600 --max-tokens 200 ;;
     sdef13nojit) DSSE_JIT_MARGIN_MS=0 step sdef13nojit 600 python3 tools/bench_serving.py --rates 13 --requests 600 --max-tokens 1000 ;;
     mixedb) step mixedb 300 python3 tools/bench_mixed.py --streams 64,128 ;;
+    launch_env_ab)  # HIP runtime launch settings vs the default, 64-stream step (graph replays)
+      step "le_default" 300 python3 bench.py --gpus 1 --steps 40 --warmup 5
+      HIP_FORCE_DEV_KERNARG=1 step "le_devkernarg" 300 python3 bench.py --gpus 1 --steps 40 --warmup 5
+      DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 step "le_nopacketcap" 300 python3 bench.py --gpus 1 --steps 40 --warmup 5
+      DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 step "le_packetcap" 300 python3 bench.py --gpus 1 --steps 40 --warmup 5
+      step "le_default2" 300 python3 bench.py --gpus 1 --steps 40 --warmup 5 ;;
     tp8_rank) step tp8_rank 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     tp8_attn)  # decode attention partitions at TP = 8 (one kv head, 64 streams): 512 / 256 / 128 / 64 workgroups
       for wg in 256 128 64; do step "tp8_attn$wg" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode --attn-wgs $wg; done ;;
