@@ -62,6 +62,11 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
   __syncthreads();
   const unsigned int e = e_s;
   const size_t doff = ar_data_off(rows) + (((size_t)(e & 1) * rows + b) * H + (size_t)tid * 8) * 2;
+  // this thread's residual and norm-weight slices do not depend on the peers: loaded first, so their round trip
+  // overlaps the flag exchange instead of following it
+  float* rp = resid + (size_t)b * H + tid * 8;
+  float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
+  const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + tid * 8);
   // 2. partial row -> own IPC buffer (write-through stores, drained before the barrier)
   const unsigned long long mine_u = peers[rank];
   char* mine = reinterpret_cast<char*>(mine_u);
@@ -70,11 +75,30 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
                                     (unsigned)__builtin_amdgcn_readfirstlane((unsigned)mine_u)), 0x7FFFFFFF);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   u32x4 v;
+  // the peer flag this thread will write (tid < world): its address loaded now, not after the release fence
+  unsigned int* pflag = tid < world ? reinterpret_cast<unsigned int*>(peers[tid]) + (size_t)rank * rows + b : nullptr;
   if (part) {
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int sidx = 0; sidx < nsplit; ++sidx) {  // slab order = splitk_reduce's summation order
-      const float* sp = part + ((size_t)sidx * M + b) * H + tid * 8;
-      const float4 p0 = *reinterpret_cast<const float4*>(sp), p1 = *reinterpret_cast<const float4*>(sp + 4);
+    // four slabs' loads in flight per step (as rmsnorm_kernel<3>), summed in slab order = splitk_reduce's order
+    const float* sp = part + (size_t)b * H + tid * 8;
+    const size_t slab = (size_t)M * H;
+    int sidx = 0;
+    for (; sidx + 4 <= nsplit; sidx += 4) {
+      float4 q0[4], q1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        q0[u] = *reinterpret_cast<const float4*>(sp + (sidx + u) * slab);
+        q1[u] = *reinterpret_cast<const float4*>(sp + (sidx + u) * slab + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[0] += q0[u].x; a[1] += q0[u].y; a[2] += q0[u].z; a[3] += q0[u].w;
+        a[4] += q1[u].x; a[5] += q1[u].y; a[6] += q1[u].z; a[7] += q1[u].w;
+      }
+    }
+    for (; sidx < nsplit; ++sidx) {
+      const float4 p0 = *reinterpret_cast<const float4*>(sp + sidx * slab);
+      const float4 p1 = *reinterpret_cast<const float4*>(sp + sidx * slab + 4);
       a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
       a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
     }
@@ -92,8 +116,7 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
   if (tid < world) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned int* pf = reinterpret_cast<unsigned int*>(peers[tid]) + (size_t)rank * rows + b;
-    __hip_atomic_store(pf, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(pflag, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned int* mf = reinterpret_cast<const unsigned int*>(mine) + (size_t)tid * rows + b;
     int spins = 0;
     while (__hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e && ++spins < kArSpinLimit)
@@ -122,8 +145,6 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
     if (q < world)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(d[q][j]);
-  float* rp = resid + (size_t)b * H + tid * 8;
-  float4 r0 = *reinterpret_cast<const float4*>(rp), r1 = *reinterpret_cast<const float4*>(rp + 4);
   r0.x += acc[0]; r0.y += acc[1]; r0.z += acc[2]; r0.w += acc[3];
   r1.x += acc[4]; r1.y += acc[5]; r1.z += acc[6]; r1.w += acc[7];
   *reinterpret_cast<float4*>(rp) = r0;
@@ -136,7 +157,6 @@ ar_rmsnorm_kernel(const bf16* __restrict__ tmp, float* __restrict__ resid, const
   float tot = 0.f;
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
   const float inv = rsqrtf(tot / (float)H + eps);
-  const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + tid * 8);
   const float rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
   bf16x8 o;
 #pragma unroll
