@@ -5,7 +5,9 @@ above its byte floor goes, split per kernel into first-load latency, steady stre
     python tools/step_stamps.py --analyse stamps.json
     rocprofv3 --pmc ... -- python3 tools/step_stamps.py --pmc-pass    (eager steps for a counter pass)
 
-Needs the diagnostic `stamps` build (`_build.py` KERNEL_VARIANTS; common.h `stamps::record`): every wave of the
+Needs the diagnostic `stamps` build (`python -c "from distributed_sse_for_llm_response_amd import _build;
+_build.build_kernels(variant='stamps')"`; `.gpurunignore` keeps it off GPU pushes, so drop that line for a run on the
+box; common.h `stamps::record`): every wave of the
 ring GEMMs (`gemm_ring_kernel`: qkv, o, down, gate_up, LM head at 17-64 rows) and of `rmsnorm_kernel` appends
 [tag, grid, block, t0, t1, t2, t3, wave] with s_memrealtime (100 MHz, one clock for the whole chip) into one of 256
 sub-buffers (by workgroup; a single shared record counter serialised the waves' exits and stretched every kernel):
