@@ -112,3 +112,43 @@ def test_engine_forward_has_no_library_gemm():
                                      for L in w.layers)
     assert all(not hasattr(L, "wo_s") for L in w.layers)
     assert w.nbytes() > 0
+
+
+
+@pytest.mark.gpu
+def test_engine_prefill_flash_key_split_matches_unsplit(gpu, monkeypatch):
+    """The engine's eager prefill of a long prompt on ONE kv head (a TP = 8 rank's shape) takes the flash key split
+    (flash_split_plan -> packed metadata -> flash_prefill_split + combine): every layer's attention output equals
+    the unsplit flash kernel's on the same inputs, within fp32-summation-order rounding."""
+    from distributed_sse_for_llm_response_amd import ops
+    from distributed_sse_for_llm_response_amd.engine import model_runner as mr
+    from distributed_sse_for_llm_response_amd.models.mistral import MistralConfig
+
+    cfg = MistralConfig(name="mistral-1kv-test", vocab_size=1024, hidden_size=512, intermediate_size=1024,
+                        num_layers=2, num_heads=4, num_kv_heads=1, max_position=4096)
+    std = init_standard_weights(cfg, seed=4)
+    w = convert_standard(cfg, std, device=gpu)
+    n = 2300  # > the largest prefill graph bucket (eager path); 36 tiles, the longest 36 key blocks: split
+    r = ModelRunner(w, num_blocks=96, max_batch=2, max_model_len=4096, device=gpu, use_graphs=False)
+    bt = list(range(0, 80))
+    r.block_tables[0, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
+    seen = []
+    orig = ops.flash_prefill_split
+
+    def checked(q, kc, vc, btab, qs, ql, ctx, work, comb, out, po, pm, nslots):
+        orig(q, kc, vc, btab, qs, ql, ctx, work, comb, out, po, pm, nslots)
+        nw = work.numel() // 5
+        ref = torch.full_like(out, float("nan"))
+        ops.paged_attention(2, q, kc, vc, btab, qs, ql, ctx, work[:nw], work[nw:2 * nw], ref, r.part_o, r.part_ml,
+                            32, 1)
+        torch.cuda.synchronize()
+        assert not torch.isnan(out).any() and not torch.isnan(ref).any()
+        seen.append((comb.numel() // 4, (out.float() - ref.float()).abs().max().item()))
+
+    monkeypatch.setattr(mr.ops, "flash_prefill_split", checked)
+    toks = [(i * 37) % (cfg.vocab_size - 3) + 3 for i in range(n)]
+    r.prefill([PrefillSeq(0, toks, 0, bt, True)], ring_row=0)
+    torch.cuda.synchronize()
+    assert len(seen) == cfg.num_layers and all(c > 0 for c, _ in seen), seen
+    assert max(e for _, e in seen) < 2e-2, seen
+    assert 3 <= int(r.ids[0]) < cfg.vocab_size
