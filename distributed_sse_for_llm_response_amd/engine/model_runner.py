@@ -77,17 +77,24 @@ HEALTH_WORDS = ("TP peer all-reduce wait timed out",)
 # all-reduce -> norm) runs in row chunks so that each chunk's all-reduce (RCCL, a side stream) overlaps the next chunk's
 # GEMMs (64 MiB all-reduces at 8k tokens, VERDICT r3 missing 1).  Chunked from
 # DSSE_TP_PREFILL_OVERLAP_MIN rows, in DSSE_TP_PREFILL_CHUNKS chunks of whole 64-row tiles.
-def flash_split_plan(tiles: list, hkv: int, min_blocks: int = 32, fill: int = 256, min_target: int = 16):
+def flash_split_plan(tiles: list, hkv: int, min_blocks: int = 32, fill: int = 256, min_target: int = 16,
+                     one_round: bool = True):
     """Key split of the flash prefill for an under-filled grid (round 6).  `tiles`: [(seq, tile, key blocks)]
     heaviest first.  With fewer than `fill` (tile, kv head) workgroups and a tile of >= `min_blocks` 64-key blocks (a
     TP = 8 rank has ONE kv head: an 8k prompt is 128 workgroups for 256 CUs, and the last tile walks 128 blocks
-    alone), every tile longer than target = max(16, blocks x Hkv / fill) blocks is cut into even key ranges; each
-    range leaves partial O in its own slot and flash_combine_kernel merges a tile's slots.  Returns None (no split)
+    alone), every tile longer than `target` blocks is cut into even key ranges: target = max(16, blocks x Hkv / fill),
+    raised (one_round) until the ranges fit one round of `fill` workgroups.  Each range leaves partial O in its own
+    slot and flash_combine_kernel merges a tile's slots.  Returns None (no split)
     or (work int32 [seq | tile | (kb0, kb1) pairs | slot], comb int32 [(seq, tile, first slot, slots)], slots), the
     work list heaviest range first."""
     if not tiles or len(tiles) * hkv >= fill or max(n for _, _, n in tiles) < min_blocks:
         return None
+    # the smallest range length whose parts still fit one round of `fill` workgroups (one flash workgroup per CU):
+    # a second round of leftover ranges would cost a whole range's time again
+    nmax = max(n for _, _, n in tiles)
     target = max(min_target, -(-sum(n for _, _, n in tiles) * hkv // fill))
+    while one_round and target < nmax and sum(-(-n // target) for _, _, n in tiles) * hkv > fill:
+        target += 1
     work, comb, nslots = [], [], 0
     for b, t, n in tiles:
         parts = -(-n // target)

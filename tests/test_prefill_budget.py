@@ -256,7 +256,7 @@ def test_flash_split_plan_covers_every_key_block_once():
     work, comb, nslots = flash_split_plan(tiles, 1)
     nw = len(work) // 5
     seq, tile, kb, slot = work[:nw], work[nw:2 * nw], work[2 * nw:4 * nw].reshape(nw, 2), work[4 * nw:]
-    assert nw > 256 and max(e - a for a, e in kb) <= 33
+    assert nw <= 256 and max(e - a for a, e in kb) <= 43  # one round of 256 workgroups
     ranges = {}
     for i in range(nw):
         ranges.setdefault(int(tile[i]), []).append((int(kb[i, 0]), int(kb[i, 1]), int(slot[i])))

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--prefill", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--phase", default="both", choices=["both", "decode", "prefill"])
+    ap.add_argument("--split-any-rounds", action="store_true",
+                    help="A/B: the flash key split's range length without the one-round rule (flash_split_plan)")
     ap.add_argument("--attn-wgs", type=int, default=0,
                     help="decode attention workgroup target of decode_partitioning (0 = the engine default, 512): "
                          "fewer flash-decoding partitions per sequence for an A/B")
@@ -60,9 +62,13 @@ def main():
     from distributed_sse_for_llm_response_amd.parallel.comm import IpcAllReduce, TPComm
 
     ops.load_library(required=True)
-    if args.attn_wgs > 0:
-        import functools
+    import functools
 
+    if args.split_any_rounds:
+        from distributed_sse_for_llm_response_amd.engine import model_runner as mr
+
+        mr.flash_split_plan = functools.partial(mr.flash_split_plan, one_round=False)
+    if args.attn_wgs > 0:
         from distributed_sse_for_llm_response_amd.engine import model_runner as mr
 
         mr.decode_partitioning = functools.partial(mr.decode_partitioning, target_wgs=args.attn_wgs)

@@ -77,6 +77,11 @@ for s in "$@"; do
     tp8_chunks)  # TP = 8 rank prefill compute with 2 row chunks and unchunked (default 4)
       DSSE_TP_PREFILL_CHUNKS=2 step tp8_chunks2 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
       DSSE_TP_PREFILL_CHUNKS=1 step tp8_chunks1 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill ;;
+    tp8_split_ab)  # flash key split: ranges sized for one round of 256 workgroups (default) vs the plain length rule
+      for i in 1 2; do
+        DSSE_TP_PREFILL_CHUNKS=1 step "tp8_split_oneround$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
+        DSSE_TP_PREFILL_CHUNKS=1 step "tp8_split_anyround$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill --split-any-rounds
+      done ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
