@@ -117,18 +117,18 @@ def test_engine_forward_has_no_library_gemm():
 
 @pytest.mark.gpu
 def test_engine_prefill_flash_key_split_matches_unsplit(gpu, monkeypatch):
-    """The engine's eager prefill of a long prompt on ONE kv head (a TP = 8 rank's shape) takes the flash key split
-    (flash_split_plan -> packed metadata -> flash_prefill_split + combine): every layer's attention output equals
-    the unsplit flash kernel's on the same inputs, within fp32-summation-order rounding."""
+    """The engine's eager prefill of a long prompt on few kv heads (an under-filled flash grid, as on a TP = 8 rank)
+    takes the flash key split (flash_split_plan -> packed metadata -> flash_prefill_split + combine): every layer's
+    attention output equals the unsplit flash kernel's on the same inputs, within fp32-summation-order rounding."""
     from distributed_sse_for_llm_response_amd import ops
     from distributed_sse_for_llm_response_amd.engine import model_runner as mr
     from distributed_sse_for_llm_response_amd.models.mistral import MistralConfig
 
-    cfg = MistralConfig(name="mistral-1kv-test", vocab_size=1024, hidden_size=512, intermediate_size=1024,
-                        num_layers=2, num_heads=4, num_kv_heads=1, max_position=4096)
+    cfg = MistralConfig(name="mistral-2kv-test", vocab_size=1024, hidden_size=1024, intermediate_size=1024,
+                        num_layers=2, num_heads=8, num_kv_heads=2, max_position=4096)
     std = init_standard_weights(cfg, seed=4)
     w = convert_standard(cfg, std, device=gpu)
-    n = 2300  # > the largest prefill graph bucket (eager path); 36 tiles, the longest 36 key blocks: split
+    n = 2300  # > the largest prefill graph bucket (eager path); 36 tiles x 2 kv heads, the longest 36 key blocks
     r = ModelRunner(w, num_blocks=96, max_batch=2, max_model_len=4096, device=gpu, use_graphs=False)
     bt = list(range(0, 80))
     r.block_tables[0, : len(bt)] = torch.tensor(bt, dtype=torch.int32)
