@@ -35,6 +35,10 @@ struct GemmEpi {
   int* fix_cnt;
 };
 constexpr int kFixTiles = 8192;  // tiles of one fix-up launch at most
+// the per-device counter block (bindings.cpp fix_state): [4 words][2 kFixTiles GEMM fix-up counters]
+// [kFixTiles decode-attention combine tickets][stamps build: per-workgroup stamps]
+constexpr int kAttnCntOff = 4 + 2 * kFixTiles;
+constexpr int kStampOff = 4 + 3 * kFixTiles;
 
 
 struct AttnParams {
@@ -76,6 +80,10 @@ struct AttnParams {
   const int* work_slot;
   const int* comb;
   int ncomb;
+  // decode partitions (nparts > 1, one query tile per workgroup) combined by the last partition of each (item, kv
+  // head) to finish instead of attn_combine_kernel (round 6): [num_work * hkv] arrival tickets, zero between
+  // launches (the last arriver resets its ticket); null = the combine kernel
+  int* comb_cnt;
 };
 
 struct SampleParams {

@@ -386,6 +386,46 @@ paged_attention_kernel(AttnParams p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) po[16 * dt + 4 * g + i] = o[dt][i];
     if (g == 0) p.part_ml[base * 16 + r] = make_float2(m_run, l_run);
+    if constexpr (QW == 1) {
+      // Last-arriver combine (round 6; decode, one query tile): the wave left in this workgroup publishes its partial
+      // (stores drained, agent-scope release) and takes a ticket on its (item, kv head); the partition that draws
+      // the last ticket -- every other non-empty partition has released before taking its own -- acquires, merges
+      // them (attn_combine_kernel's arithmetic) and resets the ticket for the next launch.  Nobody waits.
+      if (p.comb_cnt) {
+        const int np = min(p.nparts, (kmax + part - 1) / part);  // the partitions that did not exit empty
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        int* cnt = p.comb_cnt + (size_t)item * p.hkv + h;
+        int ticket = 0;
+        if (lane == 0) ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ticket = __builtin_amdgcn_readfirstlane(ticket);
+        if (ticket != np - 1) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const size_t base0 = ((size_t)item * p.hkv + h) * p.nparts;
+        float mm = -1e30f;
+        for (int z = 0; z < np; ++z) mm = fmaxf(mm, p.part_ml[(base0 + z) * 16 + r].x);
+        f32x4 acc[8];
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float ll = 0.f;
+        for (int z = 0; z < np; ++z) {
+          const float2 ml = p.part_ml[(base0 + z) * 16 + r];
+          const float sc = exp2f(ml.x - mm);
+          ll += ml.y * sc;
+          const float* pz_o = p.part_o + (base0 + z) * 16 * kD + (size_t)r * kD + 4 * g;
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) acc[dt] += *reinterpret_cast<const f32x4*>(pz_o + 16 * dt) * sc;
+        }
+        if (!col_valid) return;
+        const float inv = ll > 0.f ? 1.f / ll : 0.f;
+        bf16* op = p.out + ((size_t)(p.q_start[b] + qi) * p.hq + h * G + (r % G)) * kD;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) op[16 * dt + 4 * g + i] = f2bf(acc[dt][i] * inv);
+      }
+    }
   }
 }
 
@@ -467,7 +507,7 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     else if (p->group == 4) e = launch_folded<4>(kwv, pd, grid, *p, st);
     else return hipErrorInvalidValue;
     if (e != hipSuccess) return e;
-    if (p->nparts > 1)
+    if (p->nparts > 1 && !p->comb_cnt)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else if (mode == 0) {
     // decode: p->kwv (attn_kwv in DSSE_KERNEL_CFG, read by the bindings) = waves per workgroup splitting the keys (1/2/4/8).
@@ -483,7 +523,7 @@ extern "C" hipError_t dsse_paged_attention(int mode, int num_work, const dsse::A
     else if (kwv == 1) hipLaunchKernelGGL((paged_attention_kernel<1, 1, 1>), grid, dim3(64), 0, st, *p);
     else if (kwv == 2) hipLaunchKernelGGL((paged_attention_kernel<1, 2, 1>), grid, dim3(128), 0, st, *p);
     else hipLaunchKernelGGL((paged_attention_kernel<1, 4, 1>), grid, dim3(256), 0, st, *p);
-    if (p->nparts > 1)
+    if (p->nparts > 1 && !p->comb_cnt)
       hipLaunchKernelGGL((attn_combine_kernel<1>), dim3(num_work, p->hkv, 1), dim3(256), 0, st, *p);
   } else {
     hipLaunchKernelGGL((paged_attention_kernel<4, 1>), dim3(num_work, p->hkv, p->nparts), dim3(256),

@@ -256,7 +256,7 @@ at::Tensor& fix_state(const at::Device& dev) {
   static std::unordered_map<int, at::Tensor> per_dev;
   auto it = per_dev.find(dev.index());
   if (it == per_dev.end()) {
-    const int64_t n = 4 + 2 * kFixTiles + (DSSE_PIPE_STAMPS ? kStampWgs * 16 : 0);
+    const int64_t n = dsse::kStampOff + (DSSE_PIPE_STAMPS ? kStampWgs * 16 : 0);
     it = per_dev.emplace(dev.index(), at::zeros({n}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
   }
   return it->second;
@@ -806,6 +806,13 @@ dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cach
   return p;
 }
 
+// Decode partitions combined by their last arriver (attention.hip, round 6) instead of attn_combine_kernel:
+// attn_comb=0 (DSSE_KERNEL_CFG) keeps the combine launch.  Needs a ticket per (item, kv head).
+void attn_last_arriver(dsse::AttnParams& p, int num_work, const at::Device& dev) {
+  if (p.nparts > 1 && env_int("attn_comb", 1) && (long)num_work * p.hkv <= dsse::kFixTiles)
+    p.comb_cnt = fix_counters(dev) + dsse::kAttnCntOff;
+}
+
 void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                      const Tensor& block_tables, const Tensor& q_start, const Tensor& q_len,
                      const Tensor& ctx_len, const Tensor& work_seq, const Tensor& work_tile,
@@ -827,6 +834,7 @@ void paged_attention(int64_t mode, const Tensor& q, const Tensor& k_cache, const
     const int hg = env_int("flash_hg", 0);
     p.kwv = (hg == 1 || hg == 2 || hg == 4) && (hq / hkv) % hg == 0 ? hg : 0;
   }
+  if (mode == 0) attn_last_arriver(p, num_work, q.device());
   if (mode == 2) DSSE_CHECK_HIP(dsse_flash_prefill(num_work, &p, cur_stream()));
   else DSSE_CHECK_HIP(dsse_paged_attention((int)mode, num_work, &p, cur_stream()));
 }
@@ -948,6 +956,7 @@ int64_t qkv_attention_decode(const Tensor& x, const Tensor& w, const Tensor& pos
   p.num_slots = (int)(k_cache.size(0) * dsse::kBS);
   p.k_out = reinterpret_cast<bf16*>(k_cache.data_ptr());
   p.v_out = reinterpret_cast<bf16*>(v_cache.data_ptr());
+  attn_last_arriver(p, (int)work_seq.numel(), x.device());
   DSSE_CHECK_HIP(dsse_paged_attention(3, (int)work_seq.numel(), &p, cur_stream()));
   return S;
 }
@@ -1155,7 +1164,7 @@ std::tuple<int64_t, int64_t, int64_t, bool, double> gemm_plan(int64_t M, int64_t
 at::Tensor gemm_fix_stamps(int64_t device) {
   const at::Device dev(at::kCUDA, (c10::DeviceIndex)device);
   if (!DSSE_PIPE_STAMPS) return at::empty({0}, at::kLong);
-  return fix_state(dev).narrow(0, 4 + 2 * kFixTiles, kStampWgs * 16).view(at::kLong).view({kStampWgs, 8}).cpu();
+  return fix_state(dev).narrow(0, dsse::kStampOff, kStampWgs * 16).view(at::kLong).view({kStampWgs, 8}).cpu();
 }
 
 // Timed-out waits of the in-launch split-K fix-up on `device` since load (0 unless a writer never counted itself).

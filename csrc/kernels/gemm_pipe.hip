@@ -49,7 +49,7 @@ namespace gp {
 DEV void stamp(const GemmEpi& ep, int k, unsigned long long v) {
   if constexpr (DSSE_PIPE_STAMPS) {
     if (threadIdx.x == 0 && ep.fix_cnt)
-      reinterpret_cast<unsigned long long*>(ep.fix_cnt + 4 + 2 * kFixTiles)[(size_t)blockIdx.x * 8 + k] = v;
+      reinterpret_cast<unsigned long long*>(ep.fix_cnt + kStampOff)[(size_t)blockIdx.x * 8 + k] = v;
   }
 }
 DEV unsigned long long now() { return DSSE_PIPE_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull; }

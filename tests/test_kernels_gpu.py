@@ -429,9 +429,14 @@ def test_paged_attention_decode(gpu, ctxs, part):
 
 @pytest.mark.parametrize("ctxs", [[1, 31, 32, 33, 300], [2000, 4096, 77], [1, 1, 1], [560] * 8])
 @pytest.mark.parametrize("nparts", [2, 4, 8])
-def test_paged_attention_decode_even_partitions(gpu, ctxs, nparts):
+@pytest.mark.parametrize("comb", ["1", "0"])
+def test_paged_attention_decode_even_partitions(gpu, monkeypatch, ctxs, nparts, comb):
     """part = 0 (round 6): every sequence's keys split evenly over the nparts flash-decoding partitions in whole
-    pages (attention.hip part_keys) instead of fixed max-context partitions; against the fp32 reference."""
+    pages (attention.hip part_keys) instead of fixed max-context partitions; the partitions merged by their last
+    arriver (attn_comb=1, the default) or by attn_combine_kernel; against the fp32 reference, three calls in a row
+    (the last arriver leaves its ticket at zero for the next launch)."""
+    monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(attn_comb=comb))
+    ops.refresh_env()
     g = torch.Generator().manual_seed(sum(ctxs) + nparts)
     B = len(ctxs)
     kc, vc, bt, q, q_start = _attn_setup(ctxs, [1] * B, gen=g)
@@ -443,11 +448,13 @@ def test_paged_attention_decode_even_partitions(gpu, ctxs, nparts):
     out_g = torch.zeros_like(q).to(gpu)
     po = torch.zeros(B * 8 * nparts * 16 * 128, device=gpu)
     pml = torch.zeros(B * 8 * nparts * 16 * 2, device=gpu)
-    ops.paged_attention(0, q.to(gpu), kc.to(gpu), vc.to(gpu), bt.to(gpu), q_start.to(gpu), qlen.to(gpu), ctx.to(gpu),
-                        ws.to(gpu), wt.to(gpu), out_g, po, pml, 0, nparts)
+    args = [t.to(gpu) for t in (q, kc, vc, bt, q_start, qlen, ctx, ws, wt)]
     R.paged_attention(0, q, kc, vc, bt, q_start, qlen, ctx, ws, wt, out)
     live = qlen.bool()
-    _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, "decode attention, even partitions")
+    for _ in range(3):
+        out_g.zero_()
+        ops.paged_attention(0, *args, out_g, po, pml, 0, nparts)
+        _close(out_g.cpu()[live], out[live], 1e-2, 2e-2, f"decode attention, even partitions, attn_comb={comb}")
 
 
 @pytest.mark.parametrize("kwv", ["1", "2", "4"])

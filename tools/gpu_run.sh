@@ -82,6 +82,15 @@ for s in "$@"; do
         DSSE_TP_PREFILL_CHUNKS=1 step "tp8_split_oneround$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
         DSSE_TP_PREFILL_CHUNKS=1 step "tp8_split_anyround$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill --split-any-rounds
       done ;;
+    tp_ranks24)  # one TP = 2 / 4 rank of Mistral-7B (per-rank compute, as tp8_rank)
+      step tp2_rank 300 python3 tools/bench_tp_rank.py --tp 2
+      step tp4_rank 300 python3 tools/bench_tp_rank.py --tp 4 ;;
+    attn_comb_ab)  # decode partitions merged by their last arriver (default) vs attn_combine_kernel, TP = 8 rank
+      for i in 1 2; do
+        step "tp8_comb$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode
+        DSSE_KERNEL_CFG=attn_comb=0 step "tp8_nocomb$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode
+      done ;;
+    attn_tests) step attn_tests 600 $PYT tests/test_kernels_gpu.py -k "paged_attention_decode or qkv_attention_decode or folded" tests/test_tp_gpu.py tests/test_tp_graph_gpu.py ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
