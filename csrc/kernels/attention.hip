@@ -387,7 +387,8 @@ paged_attention_kernel(AttnParams p) {
       for (int i = 0; i < 4; ++i) po[16 * dt + 4 * g + i] = o[dt][i];
     if (g == 0) p.part_ml[base * 16 + r] = make_float2(m_run, l_run);
     if constexpr (QW == 1) {
-      // Last-arriver combine (round 6; decode, one query tile): the wave left in this workgroup publishes its partial
+      // Last-arriver combine (round 6, opt-in attn_comb=1: measured slower than the combine launch on a TP = 8 rank,
+      // bindings.cpp attn_last_arriver; decode, one query tile): the wave left in this workgroup publishes its partial
       // (stores drained, agent-scope release) and takes a ticket on its (item, kv head); the partition that draws
       // the last ticket -- every other non-empty partition has released before taking its own -- acquires, merges
       // them (attn_combine_kernel's arithmetic) and resets the ticket for the next launch.  Nobody waits.

@@ -806,10 +806,12 @@ dsse::AttnParams attn_params(int hq, const Tensor& k_cache, const Tensor& v_cach
   return p;
 }
 
-// Decode partitions combined by their last arriver (attention.hip, round 6) instead of attn_combine_kernel:
-// attn_comb=0 (DSSE_KERNEL_CFG) keeps the combine launch.  Needs a ticket per (item, kv head).
+// Decode partitions combined by their last arriver (attention.hip, round 6) instead of attn_combine_kernel: opt-in,
+// attn_comb=1 (DSSE_KERNEL_CFG).  Measured slower on a TP = 8 rank's 64-stream step, 2.20 vs 1.975 ms
+// (profiles/r6/attn_comb_ab_r6.log): each partition's agent-scope release costs more than the combine launch it
+// saves -- as for the GEMM fix-ups.  Needs a ticket per (item, kv head).
 void attn_last_arriver(dsse::AttnParams& p, int num_work, const at::Device& dev) {
-  if (p.nparts > 1 && env_int("attn_comb", 1) && (long)num_work * p.hkv <= dsse::kFixTiles)
+  if (p.nparts > 1 && env_int("attn_comb", 0) && (long)num_work * p.hkv <= dsse::kFixTiles)
     p.comb_cnt = fix_counters(dev) + dsse::kAttnCntOff;
 }
 

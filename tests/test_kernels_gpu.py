@@ -432,9 +432,9 @@ def test_paged_attention_decode(gpu, ctxs, part):
 @pytest.mark.parametrize("comb", ["1", "0"])
 def test_paged_attention_decode_even_partitions(gpu, monkeypatch, ctxs, nparts, comb):
     """part = 0 (round 6): every sequence's keys split evenly over the nparts flash-decoding partitions in whole
-    pages (attention.hip part_keys) instead of fixed max-context partitions; the partitions merged by their last
-    arriver (attn_comb=1, the default) or by attn_combine_kernel; against the fp32 reference, three calls in a row
-    (the last arriver leaves its ticket at zero for the next launch)."""
+    pages (attention.hip part_keys) instead of fixed max-context partitions; the partitions merged by
+    attn_combine_kernel (the default) or by their last arriver (attn_comb=1); against the fp32 reference, three calls
+    in a row (the last arriver leaves its ticket at zero for the next launch)."""
     monkeypatch.setenv("DSSE_KERNEL_CFG", ops.kernel_cfg_env(attn_comb=comb))
     ops.refresh_env()
     g = torch.Generator().manual_seed(sum(ctxs) + nparts)
