@@ -125,6 +125,9 @@ for s in "$@"; do
       step pmc_attn_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_attn_a" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
       step pmc_attn_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_attn_b" -o run --output-format csv -- python3 tools/bench_prefill_attn.py --T 8192 --rounds 1 --iters 3
       python3 tools/pmc_sum.py "$out/pmc_attn_a" "$out/pmc_attn_b" --kernel flash_prefill --title "flash prefill, 8k causal, 32/8 heads" > "$out/pmc_attn.md" 2>&1 ;;
+    pmc_gemm8k_ta)  # the 8192-row gate_up pipe GEMM: texture-address / LDS-DMA load path (2 TA counters per pass)
+      step pmc_g8k_ta 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY -d "$out/pmc_g8k_ta" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
+      python3 tools/pmc_sum.py "$out/pmc_g8k_ta" --kernel gemm_pipe --title "gate_up GEMM at M = 8192: load path" > "$out/pmc_g8k_ta.md" 2>&1 ;;
     pmc_gemm)
       step pmc_gemm_a 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES -d "$out/pmc_gemm_a" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
       step pmc_gemm_b 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum -d "$out/pmc_gemm_b" -o run --output-format csv -- python3 tools/bench_gemm_tiled.py --M 8192,256 --shapes gate_up --cfg auto --no-library --rounds 1 --iters 3
