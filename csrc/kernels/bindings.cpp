@@ -285,8 +285,12 @@ struct TCfg {
 // next kernel (the norm or attention consumer, else splitk_reduce) that reads S x M x N x 4 bytes at ~4.5 TB/s
 // after ~5.7 us.  Constants least-squares fitted to 238 measured launches at 192-1024 rows (12 % rms error).
 double pipe_est_us(int M, int N, int K, int bm, int S, bool fix, int out_bytes = 0) {
+  // kFixSync: the fit gave 7.06 us over isolated launches; 12 after the TP = 8 rank's prefill, where the fix-up GEMMs
+  // (gate_up at 2048-row chunks, qkv at 8192 rows, model ties with slab forms) run beside the side stream's
+  // collectives and lost 2 ms per 8k prompt to the slab forms (25.2 vs 23.3 ms, profiles/r6/tp8_fix_ab_r6.log); 12
+  // keeps the fix-up where isolated launches measured it ahead (gate_up at 576 rows)
   constexpr double kFill = 43.76e3, kMfma = 5.006e6, kT0 = 3.35, kPartial = 0.666, kSlotRead = 26.48e3,
-                   kFixSync = 7.06, kNext = 5.68, kHbm = 4.458e6, kCUs = 256;
+                   kFixSync = 12.0, kNext = 5.68, kHbm = 4.458e6, kCUs = 256;
   const int nbm = (M + bm - 1) / bm, rows = std::min(bm, M);
   const double Kr = (double)K / S;
   const long wgs = (long)nbm * (N / 256) * S;
@@ -306,12 +310,14 @@ double pipe_est_us(int M, int N, int K, int bm, int S, bool fix, int out_bytes =
 TCfg pipe_plan(int M, int N, int K, bool slab_consumer) {
   TCfg best{};
   best.ok = false;
+  const bool no_fix = env_int("t_fix", -1) == 0;  // t_fix=0 (DSSE_KERNEL_CFG): slabs only, for A/Bs
   for (int bm : {256, 192, 128}) {
     const long tiles = (long)((M + bm - 1) / bm) * (N / 256);
     for (int S = 1; S <= 16; S *= 2) {
       if (K % (128 * S) != 0) break;
       for (int fix = 0; fix < 2; ++fix) {
         if (S == 1 && fix) continue;
+        if (fix && no_fix) continue;
         if (fix && (tiles > dsse::kFixTiles || (double)tiles * (S - 1) * bm * 256 * 4 > (1u << 30))) continue;
         const double t = pipe_est_us(M, N, K, bm, S, fix, slab_consumer ? 0 : 2);
         if (!best.ok || t < best.est_us * 0.98) {  // ties: the simpler (earlier) form

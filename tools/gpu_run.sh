@@ -91,6 +91,11 @@ for s in "$@"; do
         DSSE_KERNEL_CFG=attn_comb=0 step "tp8_nocomb$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase decode
       done ;;
     attn_tests) step attn_tests 600 $PYT tests/test_kernels_gpu.py -k "paged_attention_decode or qkv_attention_decode or folded" tests/test_tp_gpu.py tests/test_tp_graph_gpu.py ;;
+    tp8_fix_ab)  # TP = 8 rank prefill: the cost model with (default) and without (t_fix=0) the in-launch fix-up
+      for i in 1 2; do
+        step "tp8_pf_fix$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
+        DSSE_KERNEL_CFG=t_fix=0 step "tp8_pf_nofix$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
+      done ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
