@@ -583,7 +583,14 @@ class ModelRunner:
         t, r = self.comm.size, self.comm.rank
         n = tmp.shape[0] // t
         own = slice(r * n, (r + 1) * n)
-        summed = torch.empty(n, tmp.shape[1], device=tmp.device, dtype=tmp.dtype)
+        # one reduce-scatter target per shape, reused: every use of it is ordered on one stream (the side stream in
+        # the chunked path, the current one otherwise, and the two paths are ordered against each other by the
+        # chunked path's events); no allocation on the host's per-chunk path
+        key = (n, tmp.shape[1], tmp.dtype, tmp.device)
+        cache = self.__dict__.setdefault("_rs_bufs", {})
+        summed = cache.get(key)
+        if summed is None:
+            summed = cache[key] = torch.empty(n, tmp.shape[1], device=tmp.device, dtype=tmp.dtype)
         self.comm.reduce_scatter_rows(summed, tmp)
         ops.rmsnorm(resid[own], norm_w, x[own], self.cfg.rms_eps, delta=summed)
         self.comm.all_gather_rows(x, x[own])
@@ -604,7 +611,12 @@ class ModelRunner:
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
-        ready = torch.cuda.Event()
+            # a ring of event pairs, reused: every wait on an event is enqueued before the event is recorded again
+            # (the ring outlasts a layer's 2 x chunks residual steps)
+            self._side_evs = [(torch.cuda.Event(), torch.cuda.Event()) for _ in range(32)]
+            self._side_ev_i = 0
+        ready, done = self._side_evs[self._side_ev_i]
+        self._side_ev_i = (self._side_ev_i + 1) % len(self._side_evs)
         ready.record(main)
         self._side.wait_event(ready)
         with torch.cuda.stream(self._side):
@@ -613,7 +625,6 @@ class ModelRunner:
             else:
                 self.comm.all_reduce(tmp)
                 ops.rmsnorm(resid, norm_w, x, self.cfg.rms_eps, delta=tmp)
-        done = torch.cuda.Event()
         done.record(self._side)
         return done
 
