@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--prefill", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--phase", default="both", choices=["both", "decode", "prefill"])
+    ap.add_argument("--host-profile", action="store_true",
+                    help="cProfile one timed prefill and print the top host functions (where the host time goes)")
     ap.add_argument("--split-any-rounds", action="store_true",
                     help="A/B: the flash key split's range length without the one-round rule (flash_split_plan)")
     ap.add_argument("--attn-wgs", type=int, default=0,
@@ -167,6 +169,23 @@ def main():
         p1.record()
         torch.cuda.synchronize()
         times.append(p0.elapsed_time(p1))
+    if args.host_profile and args.phase in ("both", "prefill"):
+        import cProfile
+        import pstats
+        import time
+
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r.prefill([seq], ring_row=0)
+        host_ms = (time.perf_counter() - t0) * 1e3  # enqueue time (the GPU may still be running)
+        torch.cuda.synchronize()
+        prof = cProfile.Profile()
+        prof.enable()
+        r.prefill([seq], ring_row=0)
+        prof.disable()
+        torch.cuda.synchronize()
+        print(f"host enqueue of one prefill: {host_ms:.2f} ms (unprofiled)", flush=True)
+        pstats.Stats(prof).sort_stats("tottime").print_stats(18)
     out = {
         "tp": args.tp, "rank": 0, "model": cfg.name, "streams": B, "prompt_len": args.prompt_len,
         "decode_step_ms": None if step_ms is None else round(step_ms, 4), "decode_collectives": "ipc kernel, 1-rank context" if ipc else "local",
