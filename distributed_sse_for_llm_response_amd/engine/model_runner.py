@@ -93,8 +93,16 @@ def flash_split_plan(tiles: list, hkv: int, min_blocks: int = 32, fill: int = 25
     # a second round of leftover ranges would cost a whole range's time again
     nmax = max(n for _, _, n in tiles)
     target = max(min_target, -(-sum(n for _, _, n in tiles) * hkv // fill))
-    while one_round and target < nmax and sum(-(-n // target) for _, _, n in tiles) * hkv > fill:
-        target += 1
+    if one_round:  # the smallest fitting length (the part count falls as the length grows): binary search
+        ns = [n for _, _, n in tiles]
+        lo, hi = target, max(target, nmax)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if sum(-(-n // mid) for n in ns) * hkv > fill:
+                lo = mid + 1
+            else:
+                hi = mid
+        target = lo
     work, comb, nslots = [], [], 0
     for b, t, n in tiles:
         parts = -(-n // target)
