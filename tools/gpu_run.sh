@@ -97,6 +97,7 @@ for s in "$@"; do
         DSSE_KERNEL_CFG=t_fix=0 step "tp8_pf_nofix$i" 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill
       done ;;
     tp8_host) step tp8_host 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill --iters 2 --host-profile ;;
+    runner_test) step runner_test 600 $PYT tests/test_model_runner.py tests/test_model_full_dims_gpu.py -m gpu ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
