@@ -98,6 +98,9 @@ for s in "$@"; do
       done ;;
     tp8_host) step tp8_host 300 python3 tools/bench_tp_rank.py --tp 8 --phase prefill --iters 2 --host-profile ;;
     runner_test) step runner_test 600 $PYT tests/test_model_runner.py tests/test_model_full_dims_gpu.py -m gpu ;;
+    checked_r6)  # the device index-check build: the checked-kernel tool, and the round-6 attention paths under it
+      DSSE_KERNELS_VARIANT=checked step check_kernels 300 python3 tools/check_kernels.py
+      DSSE_KERNELS_VARIANT=checked step checked_attn 600 $PYT tests/test_kernels_gpu.py -k "key_split or even_partitions or one_kv_head or folded_even" tests/test_model_runner.py -m gpu ;;
     tp8_rank_nofix) DSSE_KERNEL_CFG=s_fix=0 step tp8_rank_nofix 300 python3 tools/bench_tp_rank.py --tp 8 ;;
     r6_tests2) step r6_tests2 900 $PYT tests/test_kernels_gpu.py -k "ring_silu or tp8_shard or ring_lds or gemm_silu or resid_split" tests/test_tp_graph_gpu.py tests/test_custom_ar_gpu.py ;;
     flash_tp8)  # a TP = 8 rank's prompt attention (4 q heads, 1 kv head): q-head split 4 (whole group) / 2 / 1
